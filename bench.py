@@ -1,0 +1,188 @@
+"""Benchmark: weights quantized GB/s for Llama-2-7B 4-bit g=128 pseudo_quantize_tensor (BASELINE.json
+metric / configs[1]) on MI355X, one process per GPU.
+
+One step = one pass of the hot path over one batch of synthetic input: ALL 224 Linear weights of a
+Llama-2-7B (32 x {q,k,v,o: 4096x4096, gate,up: 11008x4096, down: 4096x11008}, 6.476e9 fp16
+weights = 12.95 GB) quantized INT4 g=128 asymmetric (quant_funcs.pseudo_quantize_tensor defaults
+zero_point=True, out-of-place) in ONE persistent multi-tensor launch, writing the dequantized fp16
+weights plus fp16 scales/zeros.  Inputs are generated on the device (oracle/synth.py's counter
+generator) and resident in HBM before the timed region.
+
+Multi-GPU (torchrun, one rank per GPU): every rank quantizes its own 7B-sized shard of layers
+(weak scaling, no data-path collective; the layers are independent).
+value = total fp16 input bytes of all ranks / max-over-ranks time.
+
+Also reported: "roofline" for the quantize kernel (algorithmic bytes / measured HIP-event time vs
+8 TB/s), "traffic" from a committed rocprofv3 PMC summary when present, and "cpu_baseline": the
+reference's CPU arithmetic (oracle/torch_ref.py, pinned to the reference) timed on a bounded
+sample on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "weights quantized GB/s + PPL delta, Llama-2-7B 4-bit g=128 at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+LLAMA2_7B_LAYER = [("q_proj", 4096, 4096), ("k_proj", 4096, 4096), ("v_proj", 4096, 4096),
+                   ("o_proj", 4096, 4096), ("gate_proj", 11008, 4096), ("up_proj", 11008, 4096),
+                   ("down_proj", 4096, 11008)]
+N_LAYERS = 32
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--symmetric", action="store_true")
+    ap.add_argument("--layers", type=int, default=N_LAYERS)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def init_dist(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, ws):
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_weights(rank, layers):
+    from iron_weight_only_quant_amd import kernels
+    ws = []
+    for li in range(layers):
+        for pi, (_, r, c) in enumerate(LLAMA2_7B_LAYER):
+            t = torch.empty((r, c), dtype=torch.float16, device="cuda")
+            kernels.fill_synthetic(t, seed=1_000_000 * rank + 16 * li + pi)
+            ws.append(t)
+    return ws
+
+
+def cpu_baseline(weights, bits, group, symmetric, budget_s):
+    """Reference CPU arithmetic on whole tensors of the same workload until the budget is spent."""
+    from oracle.torch_ref import minmax_fake_quant_cpu
+    threads = torch.get_num_threads()
+    done_bytes, spent, n = 0, 0.0, 0
+    for w in weights:
+        x = w.cpu()
+        t0 = time.perf_counter()
+        minmax_fake_quant_cpu(x, bits, not symmetric, group)
+        spent += time.perf_counter() - t0
+        done_bytes += x.numel() * 2
+        n += 1
+        if spent >= budget_s:
+            break
+    return {"value": round(done_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of the 224 Llama-2-7B weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
+                      f"oracle/torch_ref.py (reference quant_funcs.py:16-38 op sequence, torch CPU, "
+                      f"{threads} threads), {spent:.1f} s"}
+
+
+def main():
+    args = parse()
+    ws_n, rank, _ = init_dist(args)
+    from iron_weight_only_quant_amd import kernels
+
+    weights = make_weights(rank, args.layers)
+    numel = sum(w.numel() for w in weights)
+    plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        plan.run()
+    torch.cuda.synchronize()
+    assert plan.nan_flag.item() == 0
+
+    barrier(ws_n)
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        plan.run(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(ws_n)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
+    wall_max = max_over_ranks(wall, ws_n)
+    ms_per_step = wall_max / args.steps * 1e3
+
+    in_bytes = numel * 2
+    groups = numel // args.group
+    alg_bytes = numel * 2 + numel * 2 + groups * 2 * (1 if args.symmetric else 2)  # read w, write deq, s(,z)
+    value = ws_n * in_bytes / (ms_per_step / 1e3) / 1e9
+    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+
+    traffic = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tf = json.load(open(args.traffic_file))
+            if tf.get("workload_numel") == numel and tf.get("bits") == args.bits and tf.get("group") == args.group:
+                traffic = tf.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and ws_n == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(weights, args.bits, args.group, args.symmetric, args.cpu_seconds)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ws_n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "config": {"workload": f"Llama-2-7B all {len(weights)} Linear weights per GPU "
+                                   f"({numel} fp16 weights), INT{args.bits} g={args.group} "
+                                   f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
+                                   f"out-of-place dequant + scales/zeros, one batched launch per step",
+                       "layers": args.layers, "bits": args.bits, "group": args.group,
+                       "parallelism": f"layer-shard x{ws_n} (no collective)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_group<f16,128,asym,batched>", "kernel_ms": round(kernel_ms, 4),
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "ppl_delta": None,
+        }
+        print(json.dumps(rec), flush=True)
+    if ws_n > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+/*
+ * iwq.h — C-ABI of the MI355X-native weight-only min-max quantization path.
+ *
+ * Drop-in boundary for the reference's hot path (LiuTielong/Iron_weight_only_quant):
+ *   quant_funcs.pseudo_quantize_tensor            quant_funcs.py:4-46
+ *   QuantLinear.quantize_weight (INT branch)      quant_linear.py:885-956 (+ quant_dim, :640-647)
+ *   quant_wrapper.quantize_model RTN loop         quant_wrapper.py:52-82 (batched entry below)
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers unless the name says host (h_*).  The library allocates
+ *     nothing and frees nothing; the caller owns every buffer (SURVEY.md §8b "Ownership").
+ *   - Every compute entry takes an explicit hipStream_t (passed as void*) and is asynchronous.
+ *     There is no global mutable state: the library is reentrant across devices and streams.
+ *   - Return value: IWQ_OK (0) or an iwq_status error code; no exceptions cross the ABI.
+ *   - The NaN check of quant_funcs.py:40 is a device flag (uint32) OR-ed by the kernels; the
+ *     caller reads it once (no extra pass over the output).
+ *   - Storage dtype of weights, dequantized output, scales and zeros: IWQ_F16 / IWQ_BF16 / IWQ_F32.
+ *     The arithmetic reproduces ATen's per-op rounding to that dtype bit-exactly.
+ *
+ * Group modes (quant_linear.py:896-906): group > 0 per-group along the (possibly transposed)
+ * last dimension, IWQ_GROUP_PER_TENSOR (-1), IWQ_GROUP_PER_CHANNEL (-2: one group per row of the
+ * grouped view).  quant_dim = 1 groups along dim 0 of the [rows, cols] weight (weight.t()).
+ *
+ * Grouped view and output ordering: let V = W (quant_dim 0) or W^T (quant_dim 1), shape [vr, vc].
+ * Groups are consecutive runs of L elements of V flattened row-major (L = group, vc, or vr*vc),
+ * group j -> scales[j], zeros[j]; exactly the reference's reshape(-1, L) order, so scales/zeros
+ * are byte-identical to QuantLinear.scales/.zeros flattened ([G,1] -> [G]).
+ *
+ * Packed codes (new format; the reference keeps no integer codes): laid out in
+ * the ORIGINAL weight orientation [rows, cols] (row-major, dense):
+ *   n_bits <= 4 : rows x (cols/2) bytes, element (r, c) in byte r*(cols/2) + c/2,
+ *                 low nibble = even c (cols must be even)
+ *   n_bits 5..8 : rows x cols bytes
+ *   code = q (asymmetric, q in [0, 2^b-1]) or q + 2^(b-1) (symmetric, q in [-2^(b-1), 2^(b-1)-1]).
+ *   Dequant from codes: (code - zero) * scale (asym) / (code - 2^(b-1)) * scale (sym), each op
+ *   rounded to the storage dtype, reproduces out_deq bit-exactly.
+ */
+#ifndef IWQ_H_
+#define IWQ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum iwq_dtype { IWQ_F16 = 0, IWQ_BF16 = 1, IWQ_F32 = 2 };
+
+enum iwq_status {
+  IWQ_OK = 0,
+  IWQ_ERR_SHAPE = 1,      /* non-positive dims, ld < cols, ...                       (quant_funcs.py:15)  */
+  IWQ_ERR_GROUP = 2,      /* grouped last dim % group != 0  (AssertionError, quant_funcs.py:11, quant_linear.py:897) */
+  IWQ_ERR_GROUP_MODE = 3, /* group not > 0, -1 or -2  (ValueError "Invalid w_group_size", quant_linear.py:906) */
+  IWQ_ERR_BITS = 4,       /* n_bits outside [1, 24]                                                  */
+  IWQ_ERR_DTYPE = 5,      /* unknown storage dtype                                                   */
+  IWQ_ERR_WORKSPACE = 6,  /* workspace missing or smaller than iwq_workspace_bytes()                 */
+  IWQ_ERR_CODES = 7,      /* codes requested with n_bits > 8, or odd cols for nibble packing         */
+  IWQ_ERR_HIP = 8,        /* a HIP runtime call failed (see iwq_last_hip_error)                      */
+  IWQ_ERR_ARG = 9         /* null pointer where one is required, bad flags, ...                      */
+};
+
+#define IWQ_GROUP_PER_TENSOR (-1)
+#define IWQ_GROUP_PER_CHANNEL (-2)
+
+/* flags */
+#define IWQ_FLAG_FORCE_GENERIC 0x1u  /* use the universal segmented path (testing / A-B)            */
+#define IWQ_FLAG_BATCH_CODES 0x100u  /* batched entry: every entry carries out_codes              */
+
+/* Bytes of device workspace iwq_quantize_minmax needs for this problem (0 if none). */
+int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant_dim);
+
+/*
+ * Quantize -> dequantize one 2-D weight (replaces quant_funcs.py:16-38 and quant_linear.py:909-949).
+ *   w          [rows, cols], leading dimension ld_w elements (row-major)
+ *   out_deq    [rows, cols], ld_out; may equal w (in-place, quant_funcs.py:31-34 / quant_linear.py:949); nullable
+ *   out_codes  packed codes (layout above); nullable
+ *   out_scales [G] storage dtype; nullable
+ *   out_zeros  [G] storage dtype; ignored when symmetric; nullable
+ *   nan_flag   device uint32, OR-ed with 1 if any dequantized value is NaN; nullable
+ *   symmetric  0 -> zero_point=True path (:16-22), 1 -> absmax path (:23-29)
+ */
+int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int n_bits,
+                        int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out,
+                        void* out_codes, void* out_scales, void* out_zeros, void* workspace,
+                        int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags, void* stream);
+
+/*
+ * Batched form: quantize many independent contiguous weights in ONE persistent launch
+ * (a whole model's Linear layers: the RTN loop of quant_wrapper.py:52-82).
+ * Build the table on the host with iwq_batch_plan (validates every entry and fills the
+ * work prefix), copy it to device memory, then call iwq_quantize_minmax_batched.
+ * Supported: group > 0 with 8 <= group <= 512 a power of two, quant_dim 0, contiguous weights,
+ * n_bits <= 8.  Use iwq_quantize_minmax per tensor for anything else.
+ */
+typedef struct iwq_batch_entry {
+  const void* w;      /* [rows, cols] contiguous */
+  void* out_deq;      /* [rows, cols] contiguous, may equal w; nullable */
+  void* out_codes;    /* nullable */
+  void* out_scales;   /* nullable */
+  void* out_zeros;    /* nullable */
+  int64_t rows;
+  int64_t cols;
+  int64_t unit_begin; /* filled by iwq_batch_plan */
+} iwq_batch_entry;
+
+int iwq_batch_plan(iwq_batch_entry* h_entries, int32_t n_entries, int dtype, int n_bits, int64_t group,
+                   int64_t* h_total_units);
+
+int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units,
+                                int dtype, int n_bits, int64_t group, int symmetric, uint32_t* nan_flag,
+                                unsigned flags, void* stream);
+
+/* Deterministic synthetic weights (oracle/synth.py bit-for-bit), written to [rows, cols] contiguous. */
+int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t index_offset, void* stream);
+
+/* Diagnostics */
+const char* iwq_status_string(int status);
+int iwq_last_hip_error(void);            /* last hipError_t seen by this thread (0 = none) */
+const char* iwq_build_info(void);        /* arch, compile flags, version */
+
+/* Test-only self check of the reciprocal-corrected fp32 division used in the hot loop against IEEE
+ * division, over every finite fp16 numerator x every fp16 divisor in [2^-24, 65504].  Writes the
+ * mismatch counts (fp32 bits, fp16-rounded) to d_counts[0..1]. */
+int iwq_selftest_division(uint64_t* d_counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IWQ_H_ */

@@ -1,0 +1,114 @@
+"""Loader for the in-tree HIP library (include/iwq.h C-ABI) via ctypes.
+
+The product path has NO CPU fallback: if the library is missing, or no ROCm GPU is
+visible when a kernel is requested, these functions raise.  PyTorch is only the
+allocator/stream provider; the C-ABI takes raw device pointers and a hipStream_t.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # imported first: torch's libamdhip64.so.7 becomes THE HIP runtime of the process
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "libiwq.so")
+
+IWQ_F16, IWQ_BF16, IWQ_F32 = 0, 1, 2
+DTYPE_CODE = {torch.float16: IWQ_F16, torch.bfloat16: IWQ_BF16, torch.float32: IWQ_F32}
+
+IWQ_OK = 0
+IWQ_ERR_SHAPE, IWQ_ERR_GROUP, IWQ_ERR_GROUP_MODE, IWQ_ERR_BITS, IWQ_ERR_DTYPE = 1, 2, 3, 4, 5
+IWQ_ERR_WORKSPACE, IWQ_ERR_CODES, IWQ_ERR_HIP, IWQ_ERR_ARG = 6, 7, 8, 9
+
+IWQ_FLAG_FORCE_GENERIC = 0x1
+IWQ_FLAG_BATCH_CODES = 0x100
+
+EXPORTS = (
+    "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",
+    "iwq_fill_synthetic", "iwq_status_string", "iwq_last_hip_error", "iwq_build_info",
+    "iwq_selftest_division",
+)
+
+
+class IwqBatchEntry(ctypes.Structure):
+    """Mirror of `iwq_batch_entry` (include/iwq.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("out_deq", ctypes.c_void_p), ("out_codes", ctypes.c_void_p),
+                ("out_scales", ctypes.c_void_p), ("out_zeros", ctypes.c_void_p), ("rows", ctypes.c_int64),
+                ("cols", ctypes.c_int64), ("unit_begin", ctypes.c_int64)]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+class IwqError(RuntimeError):
+    def __init__(self, status, what):
+        self.status = status
+        super().__init__(f"{what}: {status_string(status)} (status {status})")
+
+
+def load():
+    """Load libiwq.so (raises OSError if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"iwq HIP library not built: {LIB_PATH} missing (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        lib = ctypes.CDLL(LIB_PATH)
+        i64, i32, u32, vp, u64 = ctypes.c_int64, ctypes.c_int, ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint64
+        lib.iwq_workspace_bytes.argtypes = [i64, i64, i64, i32]
+        lib.iwq_workspace_bytes.restype = i64
+        lib.iwq_quantize_minmax.argtypes = [vp, i64, i64, i64, i32, i32, i64, i32, i32, vp, i64, vp, vp, vp, vp, i64,
+                                            vp, u32, vp]
+        lib.iwq_quantize_minmax.restype = i32
+        lib.iwq_batch_plan.argtypes = [ctypes.POINTER(IwqBatchEntry), ctypes.c_int32, i32, i32, i64,
+                                       ctypes.POINTER(i64)]
+        lib.iwq_batch_plan.restype = i32
+        lib.iwq_quantize_minmax_batched.argtypes = [vp, ctypes.c_int32, i64, i32, i32, i64, i32, vp, u32, vp]
+        lib.iwq_quantize_minmax_batched.restype = i32
+        lib.iwq_fill_synthetic.argtypes = [vp, i64, i32, u64, i64, vp]
+        lib.iwq_fill_synthetic.restype = i32
+        lib.iwq_status_string.argtypes = [i32]
+        lib.iwq_status_string.restype = ctypes.c_char_p
+        lib.iwq_last_hip_error.argtypes = []
+        lib.iwq_last_hip_error.restype = i32
+        lib.iwq_build_info.argtypes = []
+        lib.iwq_build_info.restype = ctypes.c_char_p
+        lib.iwq_selftest_division.argtypes = [vp, vp]
+        lib.iwq_selftest_division.restype = i32
+        _lib = lib
+        return lib
+
+
+def status_string(status):
+    try:
+        return load().iwq_status_string(int(status)).decode()
+    except OSError:
+        return "unknown"
+
+
+def check(status, what):
+    if status != IWQ_OK:
+        if status == IWQ_ERR_HIP:
+            raise IwqError(status, f"{what} (hipError {load().iwq_last_hip_error()})")
+        raise IwqError(status, what)
+
+
+def require_device(t):
+    """The HIP path only runs on ROCm devices: fail loudly instead of falling back to the CPU."""
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError("iron_weight_only_quant_amd: tensors must live on a ROCm GPU (device 'cuda'); "
+                           "there is no CPU fallback — use oracle/ only as a test checker")
+    if torch.version.hip is None:
+        raise RuntimeError("iron_weight_only_quant_amd requires a ROCm build of PyTorch")
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None

@@ -1,0 +1,824 @@
+// iwq_minmax.hip — gfx950 kernels + C-ABI for min-max weight quantization.
+//
+// Replaces (reference, /root/reference):
+//   quant_funcs.pseudo_quantize_tensor                quant_funcs.py:4-46
+//   QuantLinear.quantize_weight INT branch            quant_linear.py:885-956 (quant_dim: :640-647)
+//   the per-layer RTN loop of quantize_model          quant_wrapper.py:52-82   (batched entry)
+//
+// Kernels:
+//   k_group    contiguous groups, 8 <= g <= 512 (power of two): 8 elements per lane, a group spans
+//              g/8 lanes, min/max by DPP; persistent grid-stride over 512-element units; optional
+//              multi-tensor table (whole model in one launch).  HBM-bound, 4 B/elem (fp16 in/out).
+//   k_rowwave  one wavefront per long contiguous group (per-channel rows, g > 512), the group
+//              held in registers between the reduction and the quantize pass.
+//   k_column   quant_dim = 1: groups run down a column; each lane owns 8 adjacent columns and
+//              (TY row slices per block) reduces through LDS.
+//   k_seg_*    universal path (any layout / length / n_bits): init keys, atomic segmented
+//              min/max, apply.  Per-tensor (-1) always uses it.
+#include "iwq_common.cuh"
+#include "../../include/iwq.h"
+
+#include <stdio.h>
+#include <string.h>
+
+using namespace iwq;
+
+namespace {
+
+thread_local int g_last_hip_error = 0;
+
+#define IWQ_HIP(call)                                   \
+  do {                                                  \
+    hipError_t e_ = (call);                             \
+    if (e_ != hipSuccess) {                             \
+      g_last_hip_error = (int)e_;                       \
+      return IWQ_ERR_HIP;                               \
+    }                                                   \
+  } while (0)
+
+constexpr int BLOCK = 256;
+constexpr int WAVES_PER_BLOCK = BLOCK / WAVE;
+constexpr int UNIT = WAVE * 8;  // elements per wave-instruction span (k_group)
+
+int device_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+__device__ __forceinline__ void flag_nan(uint32_t* nan_flag, bool any_nan) {
+  // one atomic per wave at most
+  uint64_t m = __ballot(any_nan);
+  if (m != 0 && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(m) && nan_flag) atomicOr(nan_flag, 1u);
+}
+
+// =============================================================================================
+// k_group: contiguous groups of G in {8..512}
+// =============================================================================================
+struct GroupTensor {
+  const void* w;
+  void* out;
+  void* codes;
+  void* scales;
+  void* zeros;
+  int64_t numel;
+};
+
+struct GroupArgs {
+  GroupTensor single;              // used when !BATCHED
+  const iwq_batch_entry* entries;  // used when BATCHED
+  int32_t n_entries;
+  int64_t total_units;
+  int n_bits;
+  uint32_t* nan_flag;
+};
+
+template <int DT, int G, bool SYM, int CODES>
+__device__ __forceinline__ bool group_unit(const GroupTensor& t, int64_t unit_in_tensor, int lane, int n_bits) {
+  using F = Fmt<DT>;
+  constexpr int LPG = G / 8;  // lanes per group
+  const int64_t e0 = unit_in_tensor * UNIT + (int64_t)lane * 8;
+  const bool valid = e0 < t.numel;
+  Vec8<DT> v;
+  if (valid) v.load(static_cast<const char*>(t.w) + e0 * F::BYTES);
+  else v.zero();
+
+  // ---- per-lane 8-element reduction on order keys, then DPP all-reduce over the group's lanes
+  int32_t mn, mx;
+  if constexpr (SYM) {
+    mx = mag_key<DT>(v.get(0));
+#pragma unroll
+    for (int i = 1; i < 8; ++i) mx = max(mx, mag_key<DT>(v.get(i)));
+    group_max<LPG>(mx);
+  } else {
+    mn = mx = key_of<DT>(v.get(0));
+#pragma unroll
+    for (int i = 1; i < 8; ++i) {
+      int32_t k = key_of<DT>(v.get(i));
+      mn = min(mn, k);
+      mx = max(mx, k);
+    }
+    group_minmax<LPG>(mn, mx);
+  }
+  GroupParams p;
+  if constexpr (SYM) p = params_sym<DT>(F::to_f(bits_of_key<DT>(mx)), n_bits);
+  else p = params_asym<DT>(F::to_f(bits_of_key<DT>(mn)), F::to_f(bits_of_key<DT>(mx)), n_bits);
+
+  // ---- quantize -> dequantize
+  Vec8<DT> o;
+  uint32_t c[8];
+  bool any_nan = false;
+  if (p.fast) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float cf;
+      float y = quant_fast_f16<SYM>(F::to_f(v.get(i)), p, cf);
+      o.set(i, F::from_f(y));
+      c[i] = (uint32_t)(int32_t)cf + (SYM ? (1u << (n_bits - 1)) : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float cf;
+      float y = quant_exact<DT, SYM>(F::to_f(v.get(i)), p, cf);
+      any_nan |= (y != y);
+      o.set(i, F::from_f(y));
+      c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (n_bits - 1)) : 0u) : 0u;
+    }
+  }
+  if (valid) {
+    if (t.out) o.store(static_cast<char*>(t.out) + e0 * F::BYTES);
+    if constexpr (CODES != 0) store_codes8<CODES>(static_cast<uint8_t*>(t.codes), e0, c);
+    if ((lane % LPG) == 0) {
+      const int64_t gidx = e0 / G;
+      if (t.scales) {
+        if constexpr (F::NB == 16) static_cast<uint16_t*>(t.scales)[gidx] = (uint16_t)F::from_f(p.s);
+        else static_cast<uint32_t*>(t.scales)[gidx] = F::from_f(p.s);
+      }
+      if (!SYM && t.zeros) {
+        if constexpr (F::NB == 16) static_cast<uint16_t*>(t.zeros)[gidx] = (uint16_t)F::from_f(p.z);
+        else static_cast<uint32_t*>(t.zeros)[gidx] = F::from_f(p.z);
+      }
+    }
+  }
+  return valid && any_nan;
+}
+
+template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+  bool any_nan = false;
+  int32_t cur = 0;  // batched: monotone cursor into the entry table (wave-uniform)
+  for (int64_t u0 = wave * UNROLL; u0 < a.total_units; u0 += nwaves * UNROLL) {
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const int64_t u = u0 + k;
+      if (u >= a.total_units) break;
+      if constexpr (BATCHED) {
+        while (cur + 1 < a.n_entries && u >= a.entries[cur + 1].unit_begin) ++cur;
+        cur = __builtin_amdgcn_readfirstlane(cur);
+        const iwq_batch_entry& e = a.entries[cur];
+        GroupTensor t{e.w, e.out_deq, e.out_codes, e.out_scales, e.out_zeros, e.rows * e.cols};
+        any_nan |= group_unit<DT, G, SYM, CODES>(t, u - e.unit_begin, lane, a.n_bits);
+      } else {
+        any_nan |= group_unit<DT, G, SYM, CODES>(a.single, u, lane, a.n_bits);
+      }
+    }
+  }
+  flag_nan(a.nan_flag, any_nan);
+}
+
+// =============================================================================================
+// k_rowwave: one wavefront per contiguous group of length L (L % 8 == 0, L <= CPL*512)
+// =============================================================================================
+struct RowArgs {
+  const char* w;
+  char* out;
+  uint8_t* codes;
+  void* scales;
+  void* zeros;
+  int64_t ld_w, ld_out;   // elements
+  int64_t cols;           // row length of the weight (codes layout)
+  int64_t L;              // group length
+  int64_t gpr;            // groups per row = cols / L
+  int64_t G;              // number of groups
+  int n_bits;
+  uint32_t* nan_flag;
+};
+
+template <int DT, int CPL, bool SYM, int CODES>
+__global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
+  using F = Fmt<DT>;
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= a.G) return;  // whole wave exits together
+  const int64_t row = j / a.gpr;
+  const int64_t col0 = (j - row * a.gpr) * a.L;
+  const char* src = a.w + (row * a.ld_w + col0) * F::BYTES;
+  Vec8<DT> v[CPL];
+  const int64_t nchunks = a.L / 8;
+  int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int64_t ch = (int64_t)k * WAVE + lane;
+    if (ch < nchunks) {
+      v[k].load(src + ch * 8 * F::BYTES);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (SYM) {
+          mx = max(mx, mag_key<DT>(v[k].get(i)));
+        } else {
+          int32_t kk = key_of<DT>(v[k].get(i));
+          mn = min(mn, kk);
+          mx = max(mx, kk);
+        }
+      }
+    } else {
+      v[k].zero();
+    }
+  }
+  GroupParams p;
+  if constexpr (SYM) {
+    group_max<64>(mx);
+    p = params_sym<DT>(F::to_f(bits_of_key<DT>(mx)), a.n_bits);
+  } else {
+    group_minmax<64>(mn, mx);
+    p = params_asym<DT>(F::to_f(bits_of_key<DT>(mn)), F::to_f(bits_of_key<DT>(mx)), a.n_bits);
+  }
+  bool any_nan = false;
+  char* dst = a.out ? a.out + (row * a.ld_out + col0) * F::BYTES : nullptr;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int64_t ch = (int64_t)k * WAVE + lane;
+    if (ch < nchunks) {
+      Vec8<DT> o;
+      uint32_t c[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float cf, y;
+        if (p.fast) y = quant_fast_f16<SYM>(F::to_f(v[k].get(i)), p, cf);
+        else y = quant_exact<DT, SYM>(F::to_f(v[k].get(i)), p, cf);
+        any_nan |= (y != y);
+        o.set(i, F::from_f(y));
+        c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
+      }
+      if (dst) o.store(dst + ch * 8 * F::BYTES);
+      if constexpr (CODES != 0) store_codes8<CODES>(a.codes, row * a.cols + col0 + ch * 8, c);
+    }
+  }
+  if (lane == 0) {
+    if (a.scales) {
+      if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[j] = (uint16_t)F::from_f(p.s);
+      else static_cast<uint32_t*>(a.scales)[j] = F::from_f(p.s);
+    }
+    if (!SYM && a.zeros) {
+      if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[j] = (uint16_t)F::from_f(p.z);
+      else static_cast<uint32_t*>(a.zeros)[j] = F::from_f(p.z);
+    }
+  }
+  flag_nan(a.nan_flag, any_nan);
+}
+
+// =============================================================================================
+// k_column: quant_dim = 1.  Groups of g consecutive ROWS in one column of W [rows, cols].
+// Block = TX column-chunks (8 columns each) x TY row slices; grid = (cols/(8*TX), rows/g).
+// Group j of column c sits at scales[c * (rows/g) + jr] (reference order of weight.t()).
+// =============================================================================================
+struct ColArgs {
+  const char* w;
+  char* out;
+  uint8_t* codes;
+  void* scales;
+  void* zeros;
+  int64_t rows, cols, ld_w, ld_out;
+  int64_t g;      // rows per group
+  int n_bits;
+  uint32_t* nan_flag;
+};
+
+template <int DT, bool SYM, int CODES, int TX, int TY>
+__global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
+  using F = Fmt<DT>;
+  __shared__ int32_t s_mn[TY][TX * 8];
+  __shared__ int32_t s_mx[TY][TX * 8];
+  const int tx = threadIdx.x % TX;
+  const int ty = threadIdx.x / TX;
+  const int64_t c0 = ((int64_t)blockIdx.x * TX + tx) * 8;     // first of this lane's 8 columns
+  const int64_t jr = blockIdx.y;                               // group index along rows
+  const int64_t r0 = jr * a.g;
+  const bool cvalid = c0 < a.cols;
+  int32_t mn[8], mx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mn[i] = 0x7FFFFFFF; mx[i] = (int32_t)0x80000000; }
+  if (cvalid) {
+    for (int64_t r = r0 + ty; r < r0 + a.g; r += TY) {
+      Vec8<DT> v;
+      v.load(a.w + (r * a.ld_w + c0) * F::BYTES);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (SYM) {
+          mx[i] = max(mx[i], mag_key<DT>(v.get(i)));
+        } else {
+          int32_t k = key_of<DT>(v.get(i));
+          mn[i] = min(mn[i], k);
+          mx[i] = max(mx[i], k);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s_mn[ty][tx * 8 + i] = mn[i]; s_mx[ty][tx * 8 + i] = mx[i]; }
+  __syncthreads();
+  GroupParams p[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
+    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][tx * 8 + i]); a_mx = max(a_mx, s_mx[y][tx * 8 + i]); }
+    if constexpr (SYM) p[i] = params_sym<DT>(F::to_f(bits_of_key<DT>(a_mx)), a.n_bits);
+    else p[i] = params_asym<DT>(F::to_f(bits_of_key<DT>(a_mn)), F::to_f(bits_of_key<DT>(a_mx)), a.n_bits);
+  }
+  bool any_nan = false;
+  if (cvalid) {
+    if (ty == 0) {
+      const int64_t ng = a.rows / a.g;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t gidx = (c0 + i) * ng + jr;
+        if (a.scales) {
+          if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[gidx] = (uint16_t)F::from_f(p[i].s);
+          else static_cast<uint32_t*>(a.scales)[gidx] = F::from_f(p[i].s);
+        }
+        if (!SYM && a.zeros) {
+          if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[gidx] = (uint16_t)F::from_f(p[i].z);
+          else static_cast<uint32_t*>(a.zeros)[gidx] = F::from_f(p[i].z);
+        }
+      }
+    }
+    for (int64_t r = r0 + ty; r < r0 + a.g; r += TY) {
+      Vec8<DT> v, o;
+      v.load(a.w + (r * a.ld_w + c0) * F::BYTES);
+      uint32_t c[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float cf, y;
+        if (p[i].fast) y = quant_fast_f16<SYM>(F::to_f(v.get(i)), p[i], cf);
+        else y = quant_exact<DT, SYM>(F::to_f(v.get(i)), p[i], cf);
+        any_nan |= (y != y);
+        o.set(i, F::from_f(y));
+        c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
+      }
+      if (a.out) o.store(a.out + (r * a.ld_out + c0) * F::BYTES);
+      if constexpr (CODES != 0) store_codes8<CODES>(a.codes, r * a.cols + c0, c);
+    }
+  }
+  flag_nan(a.nan_flag, any_nan);
+}
+
+// =============================================================================================
+// universal segmented path: groups of L consecutive elements of the grouped view V
+// (V = W or W^T), any L, any strides, any n_bits.
+// =============================================================================================
+struct SegArgs {
+  const char* w;
+  char* out;
+  uint8_t* codes;
+  void* scales;
+  void* zeros;
+  int32_t* keys;      // [2*G]: (min key, max key) — symmetric uses the max slot only
+  int64_t rows, cols, ld_w, ld_out;
+  int64_t vc;         // columns of V
+  int64_t L, G, total;
+  int quant_dim;
+  int n_bits;
+  int codes_bits;     // 0, 4, 8
+  uint32_t* nan_flag;
+};
+
+constexpr int SEG_RUN = 16;
+
+__device__ __forceinline__ void seg_locate(const SegArgs& a, int64_t f, int64_t& off_w, int64_t& off_o,
+                                           int64_t& r, int64_t& c) {
+  const int64_t vr_i = f / a.vc;
+  const int64_t vc_i = f - vr_i * a.vc;
+  if (a.quant_dim == 0) { r = vr_i; c = vc_i; }
+  else { r = vc_i; c = vr_i; }
+  off_w = r * a.ld_w + c;
+  off_o = r * a.ld_out + c;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_seg_init(int32_t* keys, int64_t G) {
+  for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < G; j += (int64_t)gridDim.x * BLOCK) {
+    keys[2 * j] = 0x7FFFFFFF;
+    keys[2 * j + 1] = (int32_t)0x80000000;
+  }
+}
+
+template <int DT, bool SYM>
+__global__ __launch_bounds__(BLOCK) void k_seg_reduce(SegArgs a) {
+  using F = Fmt<DT>;
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  int64_t curj = -1;
+  int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
+  for (int64_t f0 = tid * SEG_RUN; f0 < a.total; f0 += nthreads * SEG_RUN) {
+    const int64_t fend = min(f0 + SEG_RUN, a.total);
+    for (int64_t f = f0; f < fend; ++f) {
+      const int64_t j = f / a.L;
+      if (j != curj) {
+        if (curj >= 0) {
+          if (!SYM) atomicMin(&a.keys[2 * curj], mn);
+          atomicMax(&a.keys[2 * curj + 1], mx);
+        }
+        curj = j;
+        mn = 0x7FFFFFFF;
+        mx = (int32_t)0x80000000;
+      }
+      int64_t ow, oo, r, c;
+      seg_locate(a, f, ow, oo, r, c);
+      uint32_t b;
+      if constexpr (F::NB == 16) b = reinterpret_cast<const uint16_t*>(a.w)[ow];
+      else b = reinterpret_cast<const uint32_t*>(a.w)[ow];
+      if constexpr (SYM) {
+        mx = max(mx, mag_key<DT>(b));
+      } else {
+        int32_t k = key_of<DT>(b);
+        mn = min(mn, k);
+        mx = max(mx, k);
+      }
+    }
+  }
+  // flush: combine across the wave first when every lane holds the same group (per-tensor case)
+  const int64_t j0 = __shfl(curj, 0);
+  const bool same = __all(curj == j0);
+  if (same) {
+    if (j0 >= 0) {
+      int32_t m1 = mn, m2 = mx;
+      group_minmax<64>(m1, m2);
+      if ((threadIdx.x & 63) == 0) {
+        if (!SYM) atomicMin(&a.keys[2 * j0], m1);
+        atomicMax(&a.keys[2 * j0 + 1], m2);
+      }
+    }
+  } else if (curj >= 0) {
+    if (!SYM) atomicMin(&a.keys[2 * curj], mn);
+    atomicMax(&a.keys[2 * curj + 1], mx);
+  }
+}
+
+template <int DT, bool SYM>
+__global__ __launch_bounds__(BLOCK) void k_seg_apply(SegArgs a) {
+  using F = Fmt<DT>;
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  int64_t curj = -1;
+  GroupParams p{};
+  bool any_nan = false;
+  for (int64_t f0 = tid * SEG_RUN; f0 < a.total; f0 += nthreads * SEG_RUN) {
+    const int64_t fend = min(f0 + SEG_RUN, a.total);
+    for (int64_t f = f0; f < fend; ++f) {
+      const int64_t j = f / a.L;
+      if (j != curj) {
+        curj = j;
+        if constexpr (SYM) p = params_sym<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
+        else p = params_asym<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j])), F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
+        if (f == j * a.L) {
+          if (a.scales) {
+            if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[j] = (uint16_t)F::from_f(p.s);
+            else static_cast<uint32_t*>(a.scales)[j] = F::from_f(p.s);
+          }
+          if (!SYM && a.zeros) {
+            if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[j] = (uint16_t)F::from_f(p.z);
+            else static_cast<uint32_t*>(a.zeros)[j] = F::from_f(p.z);
+          }
+        }
+      }
+      int64_t ow, oo, r, c;
+      seg_locate(a, f, ow, oo, r, c);
+      uint32_t b;
+      if constexpr (F::NB == 16) b = reinterpret_cast<const uint16_t*>(a.w)[ow];
+      else b = reinterpret_cast<const uint32_t*>(a.w)[ow];
+      float cf;
+      float y = quant_exact<DT, SYM>(F::to_f(b), p, cf);
+      any_nan |= (y != y);
+      const uint32_t yb = F::from_f(y);
+      if (a.out) {
+        if constexpr (F::NB == 16) reinterpret_cast<uint16_t*>(a.out)[oo] = (uint16_t)yb;
+        else reinterpret_cast<uint32_t*>(a.out)[oo] = yb;
+      }
+      if (a.codes_bits) {
+        const uint32_t code = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
+        const int64_t e = r * a.cols + c;
+        if (a.codes_bits == 8) {
+          a.codes[e] = (uint8_t)code;
+        } else {
+          // nibbles: OR into the (pre-zeroed) 32-bit word; neighbours may belong to other threads
+          const int64_t byte = e >> 1;
+          const int shift = (int)((byte & 3) * 8 + (e & 1) * 4);
+          atomicOr(reinterpret_cast<uint32_t*>(a.codes + (byte & ~(int64_t)3)), (code & 0xFu) << shift);
+        }
+      }
+    }
+  }
+  flag_nan(a.nan_flag, any_nan);
+}
+
+// =============================================================================================
+// host-side dispatch
+// =============================================================================================
+bool is_pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
+
+template <int DT, int G, bool SYM, int CODES, bool BATCHED>
+hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
+  constexpr int UNROLL = 2;
+  const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
+  int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  const int64_t cap = (int64_t)device_cu_count() * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_group<DT, G, SYM, CODES, BATCHED, UNROLL>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int DT, bool SYM, int CODES, bool BATCHED>
+hipError_t launch_group_g(int64_t g, const GroupArgs& a, hipStream_t st) {
+  switch (g) {
+    case 8: return launch_group_t<DT, 8, SYM, CODES, BATCHED>(a, st);
+    case 16: return launch_group_t<DT, 16, SYM, CODES, BATCHED>(a, st);
+    case 32: return launch_group_t<DT, 32, SYM, CODES, BATCHED>(a, st);
+    case 64: return launch_group_t<DT, 64, SYM, CODES, BATCHED>(a, st);
+    case 128: return launch_group_t<DT, 128, SYM, CODES, BATCHED>(a, st);
+    case 256: return launch_group_t<DT, 256, SYM, CODES, BATCHED>(a, st);
+    case 512: return launch_group_t<DT, 512, SYM, CODES, BATCHED>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <bool BATCHED>
+hipError_t launch_group(int dt, int64_t g, bool sym, int codes, const GroupArgs& a, hipStream_t st) {
+#define IWQ_G_CODES(DT, SYM)                                                          \
+  switch (codes) {                                                                    \
+    case 0: return launch_group_g<DT, SYM, 0, BATCHED>(g, a, st);                     \
+    case 4: return launch_group_g<DT, SYM, 4, BATCHED>(g, a, st);                     \
+    default: return launch_group_g<DT, SYM, 8, BATCHED>(g, a, st);                    \
+  }
+  if (dt == IWQ_F16) { if (sym) { IWQ_G_CODES(DT_F16, true) } else { IWQ_G_CODES(DT_F16, false) } }
+  if (dt == IWQ_BF16) { if (sym) { IWQ_G_CODES(DT_BF16, true) } else { IWQ_G_CODES(DT_BF16, false) } }
+  if (sym) { IWQ_G_CODES(DT_F32, true) } else { IWQ_G_CODES(DT_F32, false) }
+#undef IWQ_G_CODES
+}
+
+template <int DT, int CPL, bool SYM>
+hipError_t launch_row_t(int codes, const RowArgs& a, hipStream_t st) {
+  const int64_t blocks = (a.G + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  if (codes == 0) hipLaunchKernelGGL((k_rowwave<DT, CPL, SYM, 0>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  else if (codes == 4) hipLaunchKernelGGL((k_rowwave<DT, CPL, SYM, 4>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  else hipLaunchKernelGGL((k_rowwave<DT, CPL, SYM, 8>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int DT, bool SYM>
+hipError_t launch_row_c(int codes, const RowArgs& a, hipStream_t st) {
+  const int64_t chunks = a.L / 8;
+  if (chunks <= 64 * 1) return launch_row_t<DT, 1, SYM>(codes, a, st);
+  if (chunks <= 64 * 2) return launch_row_t<DT, 2, SYM>(codes, a, st);
+  if (chunks <= 64 * 4) return launch_row_t<DT, 4, SYM>(codes, a, st);
+  if (chunks <= 64 * 8) return launch_row_t<DT, 8, SYM>(codes, a, st);
+  if (chunks <= 64 * 12) return launch_row_t<DT, 12, SYM>(codes, a, st);
+  if (chunks <= 64 * 16) return launch_row_t<DT, 16, SYM>(codes, a, st);
+  if (chunks <= 64 * 24) return launch_row_t<DT, 24, SYM>(codes, a, st);
+  return launch_row_t<DT, 32, SYM>(codes, a, st);
+}
+constexpr int64_t ROW_MAX_L = 32 * 64 * 8;  // 16384 elements held in registers
+
+hipError_t launch_row(int dt, bool sym, int codes, const RowArgs& a, hipStream_t st) {
+  if (dt == IWQ_F16) return sym ? launch_row_c<DT_F16, true>(codes, a, st) : launch_row_c<DT_F16, false>(codes, a, st);
+  if (dt == IWQ_BF16) return sym ? launch_row_c<DT_BF16, true>(codes, a, st) : launch_row_c<DT_BF16, false>(codes, a, st);
+  return sym ? launch_row_c<DT_F32, true>(codes, a, st) : launch_row_c<DT_F32, false>(codes, a, st);
+}
+
+template <int DT, bool SYM, int CODES>
+hipError_t launch_col_t(const ColArgs& a, hipStream_t st) {
+  constexpr int TX = 8, TY = 32;
+  dim3 grid((unsigned)((a.cols + 8 * TX - 1) / (8 * TX)), (unsigned)(a.rows / a.g));
+  hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, dim3(TX * TY), 0, st, a);
+  return hipGetLastError();
+}
+template <int DT, bool SYM>
+hipError_t launch_col_c(int codes, const ColArgs& a, hipStream_t st) {
+  if (codes == 0) return launch_col_t<DT, SYM, 0>(a, st);
+  if (codes == 4) return launch_col_t<DT, SYM, 4>(a, st);
+  return launch_col_t<DT, SYM, 8>(a, st);
+}
+hipError_t launch_col(int dt, bool sym, int codes, const ColArgs& a, hipStream_t st) {
+  if (dt == IWQ_F16) return sym ? launch_col_c<DT_F16, true>(codes, a, st) : launch_col_c<DT_F16, false>(codes, a, st);
+  if (dt == IWQ_BF16) return sym ? launch_col_c<DT_BF16, true>(codes, a, st) : launch_col_c<DT_BF16, false>(codes, a, st);
+  return sym ? launch_col_c<DT_F32, true>(codes, a, st) : launch_col_c<DT_F32, false>(codes, a, st);
+}
+
+template <int DT, bool SYM>
+hipError_t launch_seg_t(const SegArgs& a, hipStream_t st) {
+  const int64_t cap = (int64_t)device_cu_count() * 8;
+  int64_t ib = (a.G + BLOCK - 1) / BLOCK;
+  if (ib > cap) ib = cap;
+  hipLaunchKernelGGL(k_seg_init, dim3((unsigned)ib), dim3(BLOCK), 0, st, a.keys, a.G);
+  int64_t blocks = (a.total + (int64_t)BLOCK * SEG_RUN - 1) / ((int64_t)BLOCK * SEG_RUN);
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_seg_reduce<DT, SYM>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  hipLaunchKernelGGL((k_seg_apply<DT, SYM>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_seg(int dt, bool sym, const SegArgs& a, hipStream_t st) {
+  if (dt == IWQ_F16) return sym ? launch_seg_t<DT_F16, true>(a, st) : launch_seg_t<DT_F16, false>(a, st);
+  if (dt == IWQ_BF16) return sym ? launch_seg_t<DT_BF16, true>(a, st) : launch_seg_t<DT_BF16, false>(a, st);
+  return sym ? launch_seg_t<DT_F32, true>(a, st) : launch_seg_t<DT_F32, false>(a, st);
+}
+
+int group_geometry(int64_t rows, int64_t cols, int64_t group, int quant_dim, int64_t& L, int64_t& G) {
+  const int64_t vr = quant_dim == 1 ? cols : rows;
+  const int64_t vc = quant_dim == 1 ? rows : cols;
+  if (group > 0) {
+    if (vc % group != 0) return IWQ_ERR_GROUP;
+    L = group;
+    G = vr * vc / group;
+  } else if (group == IWQ_GROUP_PER_TENSOR) {
+    L = vr * vc;
+    G = 1;
+  } else if (group == IWQ_GROUP_PER_CHANNEL) {
+    L = vc;
+    G = vr;
+  } else {
+    return IWQ_ERR_GROUP_MODE;
+  }
+  return IWQ_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant_dim) {
+  int64_t L = 0, G = 0;
+  if (rows <= 0 || cols <= 0) return 0;
+  if (group_geometry(rows, cols, group, quant_dim, L, G) != IWQ_OK) return 0;
+  return ((8 * G + 255) / 256) * 256;
+}
+
+int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int n_bits,
+                        int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out,
+                        void* out_codes, void* out_scales, void* out_zeros, void* workspace,
+                        int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags, void* stream) {
+  if (dtype != IWQ_F16 && dtype != IWQ_BF16 && dtype != IWQ_F32) return IWQ_ERR_DTYPE;
+  if (!w) return IWQ_ERR_ARG;
+  if (rows <= 0 || cols <= 0 || ld_w < cols || (out_deq && ld_out < cols)) return IWQ_ERR_SHAPE;
+  if (quant_dim != 0 && quant_dim != 1) return IWQ_ERR_ARG;
+  if (n_bits < 1 || n_bits > 24) return IWQ_ERR_BITS;
+  if (symmetric && n_bits < 2) return IWQ_ERR_BITS;
+  int64_t L = 0, G = 0;
+  int st = group_geometry(rows, cols, group, quant_dim, L, G);
+  if (st != IWQ_OK) return st;
+  int codes = 0;
+  if (out_codes) {
+    if (n_bits > 8) return IWQ_ERR_CODES;
+    codes = n_bits <= 4 ? 4 : 8;
+    if (codes == 4 && (cols & 1)) return IWQ_ERR_CODES;
+  }
+  const bool sym = symmetric != 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int eb = elem_bytes(dtype);
+  const bool generic = (flags & IWQ_FLAG_FORCE_GENERIC) != 0;
+  const bool al = aligned16(w) && (!out_deq || aligned16(out_deq)) && (ld_w * eb) % 16 == 0 &&
+                  (!out_deq || (ld_out * eb) % 16 == 0) && (!out_codes || aligned16(out_codes));
+  const bool fastbits = n_bits <= 8;
+
+  if (!generic && quant_dim == 0 && group > 0 && group >= 8 && group <= 512 && is_pow2(group) && al &&
+      fastbits && ld_w == cols && (!out_deq || ld_out == cols)) {
+    GroupArgs a{};
+    a.single = GroupTensor{w, out_deq, out_codes, out_scales, sym ? nullptr : out_zeros, rows * cols};
+    a.total_units = (rows * cols + UNIT - 1) / UNIT;
+    a.n_entries = 1;
+    a.n_bits = n_bits;
+    a.nan_flag = nan_flag;
+    IWQ_HIP(launch_group<false>(dtype, group, sym, codes, a, s));
+    return IWQ_OK;
+  }
+  if (!generic && quant_dim == 0 && group != IWQ_GROUP_PER_TENSOR && L % 8 == 0 && L <= ROW_MAX_L && al && fastbits) {
+    RowArgs a{};
+    a.w = static_cast<const char*>(w);
+    a.out = static_cast<char*>(out_deq);
+    a.codes = static_cast<uint8_t*>(out_codes);
+    a.scales = out_scales;
+    a.zeros = sym ? nullptr : out_zeros;
+    a.ld_w = ld_w;
+    a.ld_out = ld_out;
+    a.cols = cols;
+    a.L = L;
+    a.gpr = cols / L;
+    a.G = G;
+    a.n_bits = n_bits;
+    a.nan_flag = nan_flag;
+    IWQ_HIP(launch_row(dtype, sym, codes, a, s));
+    return IWQ_OK;
+  }
+  if (!generic && quant_dim == 1 && group != IWQ_GROUP_PER_TENSOR && cols % 8 == 0 && al && fastbits) {
+    ColArgs a{};
+    a.w = static_cast<const char*>(w);
+    a.out = static_cast<char*>(out_deq);
+    a.codes = static_cast<uint8_t*>(out_codes);
+    a.scales = out_scales;
+    a.zeros = sym ? nullptr : out_zeros;
+    a.rows = rows;
+    a.cols = cols;
+    a.ld_w = ld_w;
+    a.ld_out = ld_out;
+    a.g = L;  // rows per group (L = group, or rows for per-channel)
+    a.n_bits = n_bits;
+    a.nan_flag = nan_flag;
+    IWQ_HIP(launch_col(dtype, sym, codes, a, s));
+    return IWQ_OK;
+  }
+  // universal path
+  const int64_t need = iwq_workspace_bytes(rows, cols, group, quant_dim);
+  if (!workspace || workspace_bytes < need || !aligned16(workspace)) return IWQ_ERR_WORKSPACE;
+  if (codes == 4) {
+    const int64_t nbytes = rows * (cols / 2);
+    if ((reinterpret_cast<uintptr_t>(out_codes) & 3u) != 0) return IWQ_ERR_ARG;
+    IWQ_HIP(hipMemsetAsync(out_codes, 0, (size_t)nbytes, s));
+  }
+  SegArgs a{};
+  a.w = static_cast<const char*>(w);
+  a.out = static_cast<char*>(out_deq);
+  a.codes = static_cast<uint8_t*>(out_codes);
+  a.scales = out_scales;
+  a.zeros = sym ? nullptr : out_zeros;
+  a.keys = static_cast<int32_t*>(workspace);
+  a.rows = rows;
+  a.cols = cols;
+  a.ld_w = ld_w;
+  a.ld_out = ld_out;
+  a.vc = quant_dim == 1 ? rows : cols;
+  a.L = L;
+  a.G = G;
+  a.total = rows * cols;
+  a.quant_dim = quant_dim;
+  a.n_bits = n_bits;
+  a.codes_bits = codes;
+  a.nan_flag = nan_flag;
+  IWQ_HIP(launch_seg(dtype, sym, a, s));
+  return IWQ_OK;
+}
+
+int iwq_batch_plan(iwq_batch_entry* h_entries, int32_t n_entries, int dtype, int n_bits, int64_t group,
+                   int64_t* h_total_units) {
+  if (!h_entries || n_entries <= 0 || !h_total_units) return IWQ_ERR_ARG;
+  if (dtype != IWQ_F16 && dtype != IWQ_BF16 && dtype != IWQ_F32) return IWQ_ERR_DTYPE;
+  if (n_bits < 2 || n_bits > 8) return IWQ_ERR_BITS;
+  if (!(group >= 8 && group <= 512 && is_pow2(group))) return IWQ_ERR_GROUP_MODE;
+  int64_t u = 0;
+  for (int32_t i = 0; i < n_entries; ++i) {
+    iwq_batch_entry& e = h_entries[i];
+    if (!e.w || e.rows <= 0 || e.cols <= 0) return IWQ_ERR_SHAPE;
+    if (e.cols % group != 0) return IWQ_ERR_GROUP;
+    if (!aligned16(e.w) || (e.out_deq && !aligned16(e.out_deq)) || (e.out_codes && !aligned16(e.out_codes)))
+      return IWQ_ERR_ARG;
+    if (e.out_codes && n_bits <= 4 && (e.cols & 1)) return IWQ_ERR_CODES;
+    e.unit_begin = u;
+    u += (e.rows * e.cols + UNIT - 1) / UNIT;
+  }
+  *h_total_units = u;
+  return IWQ_OK;
+}
+
+int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units,
+                                int dtype, int n_bits, int64_t group, int symmetric, uint32_t* nan_flag,
+                                unsigned flags, void* stream) {
+  if (!d_entries || n_entries <= 0 || total_units <= 0) return IWQ_ERR_ARG;
+  if (dtype != IWQ_F16 && dtype != IWQ_BF16 && dtype != IWQ_F32) return IWQ_ERR_DTYPE;
+  if (n_bits < 2 || n_bits > 8) return IWQ_ERR_BITS;
+  if (!(group >= 8 && group <= 512 && is_pow2(group))) return IWQ_ERR_GROUP_MODE;
+  (void)flags;
+  GroupArgs a{};
+  a.entries = d_entries;
+  a.n_entries = n_entries;
+  a.total_units = total_units;
+  a.n_bits = n_bits;
+  a.nan_flag = nan_flag;
+  // the codes width is a template parameter and the entries are device-resident, so the caller
+  // states with IWQ_FLAG_BATCH_CODES that every entry carries out_codes.
+  const int codes = (flags & IWQ_FLAG_BATCH_CODES) ? (n_bits <= 4 ? 4 : 8) : 0;
+  IWQ_HIP(launch_group<true>(dtype, group, symmetric != 0, codes, a, static_cast<hipStream_t>(stream)));
+  return IWQ_OK;
+}
+
+const char* iwq_status_string(int status) {
+  switch (status) {
+    case IWQ_OK: return "ok";
+    case IWQ_ERR_SHAPE: return "bad shape";
+    case IWQ_ERR_GROUP: return "last dimension not divisible by group size";
+    case IWQ_ERR_GROUP_MODE: return "Invalid w_group_size";
+    case IWQ_ERR_BITS: return "unsupported n_bits";
+    case IWQ_ERR_DTYPE: return "unsupported dtype";
+    case IWQ_ERR_WORKSPACE: return "workspace missing or too small";
+    case IWQ_ERR_CODES: return "codes output unsupported for this n_bits / shape";
+    case IWQ_ERR_HIP: return "HIP runtime error";
+    case IWQ_ERR_ARG: return "bad argument";
+  }
+  return "unknown status";
+}
+
+int iwq_last_hip_error(void) { return g_last_hip_error; }
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+"""Torch-facing wrappers over the C-ABI (include/iwq.h).
+
+These only marshal device pointers, strides and the current HIP stream; all arithmetic runs in the
+gfx950 kernels of csrc/iwq_minmax.hip.  Error statuses are mapped onto the exception types the
+reference raises (quant_funcs.py:11/15/40, quant_linear.py:897/906).
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from . import _lib as L
+
+FAST_GROUPS = (8, 16, 32, 64, 128, 256, 512)
+
+
+@dataclass
+class QuantResult:
+    out: Optional[torch.Tensor]       # dequantized weight (same shape/dtype as input) or None
+    scales: Optional[torch.Tensor]    # [G] storage dtype
+    zeros: Optional[torch.Tensor]     # [G] storage dtype (asymmetric) or None
+    codes: Optional[torch.Tensor]     # packed uint8 codes (include/iwq.h layout) or None
+    nan_flag: torch.Tensor            # [1] int32 on device; nonzero if the output holds a NaN
+
+    def has_nan(self) -> bool:
+        return bool(self.nan_flag.item() != 0)
+
+
+def group_geometry(rows, cols, group, quant_dim):
+    """(L, G) of the grouped view, or raise like the reference (quant_linear.py:896-906)."""
+    vr, vc = (cols, rows) if quant_dim == 1 else (rows, cols)
+    if group > 0:
+        assert vc % group == 0
+        return group, vr * vc // group
+    if group == -1:
+        return vr * vc, 1
+    if group == -2:
+        return vc, vr
+    raise ValueError("Invalid w_group_size")
+
+
+def codes_nbytes(rows, cols, n_bits):
+    return rows * (cols // 2) if n_bits <= 4 else rows * cols
+
+
+def _raise_for(status, what):
+    if status == L.IWQ_ERR_GROUP:
+        raise AssertionError(f"{what}: last dimension not divisible by the group size")
+    if status == L.IWQ_ERR_GROUP_MODE:
+        raise ValueError("Invalid w_group_size")
+    L.check(status, what)
+
+
+def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, quant_dim: int = 0,
+                    out: Optional[torch.Tensor] = None, want_deq: bool = True, want_codes: bool = False,
+                    want_scales: bool = True, flags: int = 0) -> QuantResult:
+    """Min-max fake-quantize a 2-D weight on the GPU.
+
+    w       [rows, cols] fp16/bf16/fp32 CUDA tensor with unit column stride (any row stride).
+    out     destination for the dequantized weight (may be `w` itself for in-place), else a new
+            contiguous tensor is allocated when want_deq.
+    """
+    L.require_device(w)
+    if w.dim() != 2:
+        raise AssertionError("weight must be 2-D")
+    if w.dtype not in L.DTYPE_CODE:
+        raise TypeError(f"unsupported dtype {w.dtype}")
+    lib = L.load()
+    if w.stride(1) != 1 or w.stride(0) < w.shape[1]:
+        w = w.contiguous()
+    rows, cols = w.shape
+    Lg, G = group_geometry(rows, cols, group, quant_dim)
+    dev = w.device
+    if out is None and want_deq:
+        out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
+    if out is not None:
+        if out.shape != w.shape or out.dtype != w.dtype or out.device != dev or out.stride(1) != 1:
+            raise ValueError("out must match w in shape/dtype/device and have unit column stride")
+    scales = torch.empty(G, dtype=w.dtype, device=dev) if want_scales else None
+    zeros = torch.empty(G, dtype=w.dtype, device=dev) if (want_scales and not symmetric) else None
+    codes = None
+    if want_codes:
+        if n_bits > 8:
+            raise ValueError("packed codes need n_bits <= 8")
+        codes = torch.empty(codes_nbytes(rows, cols, n_bits), dtype=torch.uint8, device=dev)
+    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev) if wsb > 0 else None
+    with torch.cuda.device(dev):
+        st = lib.iwq_quantize_minmax(
+            L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group), int(bool(symmetric)),
+            int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols), L.ptr(codes), L.ptr(scales),
+            L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev))
+    _raise_for(st, "iwq_quantize_minmax")
+    return QuantResult(out, scales, zeros, codes, nan_flag)
+
+
+class BatchPlan:
+    """Device-resident work table for quantizing many weights in one launch (quant_wrapper.py:52-82).
+
+    Built once per set of tensors; `run()` may be replayed (e.g. by bench.py) without host work
+    beyond one kernel launch."""
+
+    def __init__(self, weights: List[torch.Tensor], n_bits: int, group: int, symmetric: bool,
+                 outs: Optional[List[torch.Tensor]] = None, want_scales: bool = True, want_codes: bool = False):
+        if not weights:
+            raise ValueError("empty batch")
+        lib = L.load()
+        dev = weights[0].device
+        dt = weights[0].dtype
+        for w in weights:
+            L.require_device(w)
+            if w.device != dev or w.dtype != dt or w.dim() != 2 or not w.is_contiguous():
+                raise ValueError("batched weights must be contiguous 2-D tensors of one dtype on one device")
+            if w.shape[1] % group != 0:
+                raise AssertionError("last dimension not divisible by the group size")
+        if group not in FAST_GROUPS or not (2 <= n_bits <= 8):
+            raise ValueError("batched path supports power-of-two groups 8..512 and 2 <= n_bits <= 8")
+        self.device, self.dtype = dev, dt
+        self.n_bits, self.group, self.symmetric = int(n_bits), int(group), bool(symmetric)
+        self.weights = weights
+        self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
+        self.scales = [torch.empty(w.numel() // group, dtype=dt, device=dev) if want_scales else None for w in weights]
+        self.zeros = [torch.empty(w.numel() // group, dtype=dt, device=dev) if (want_scales and not symmetric) else None
+                      for w in weights]
+        self.codes = [torch.empty(codes_nbytes(w.shape[0], w.shape[1], n_bits), dtype=torch.uint8, device=dev)
+                      if want_codes else None for w in weights]
+        self.want_codes = want_codes
+        n = len(weights)
+        table = (L.IwqBatchEntry * n)()
+        for i, w in enumerate(weights):
+            table[i].w = w.data_ptr()
+            table[i].out_deq = self.outs[i].data_ptr() if self.outs[i] is not None else None
+            table[i].out_codes = self.codes[i].data_ptr() if self.codes[i] is not None else None
+            table[i].out_scales = self.scales[i].data_ptr() if self.scales[i] is not None else None
+            table[i].out_zeros = self.zeros[i].data_ptr() if self.zeros[i] is not None else None
+            table[i].rows, table[i].cols = w.shape
+        total = ctypes.c_int64(0)
+        _raise_for(lib.iwq_batch_plan(table, n, L.DTYPE_CODE[dt], self.n_bits, self.group, ctypes.byref(total)),
+                   "iwq_batch_plan")
+        self.total_units = total.value
+        host = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8)
+        self.d_table = host.to(dev)
+        self.n = n
+        self.nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.numel = sum(w.numel() for w in weights)
+
+    def run(self, stream=None):
+        lib = L.load()
+        flags = L.IWQ_FLAG_BATCH_CODES if self.want_codes else 0
+        sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
+        with torch.cuda.device(self.device):
+            st = lib.iwq_quantize_minmax_batched(L.ptr(self.d_table), self.n, self.total_units,
+                                                 L.DTYPE_CODE[self.dtype], self.n_bits, self.group,
+                                                 int(self.symmetric), L.ptr(self.nan_flag), flags, sh)
+        _raise_for(st, "iwq_quantize_minmax_batched")
+
+
+def fill_synthetic(t: torch.Tensor, seed: int, index_offset: int = 0):
+    """Fill a contiguous tensor with oracle/synth.py's deterministic weights (bit-identical)."""
+    L.require_device(t)
+    assert t.is_contiguous() and t.dtype in L.DTYPE_CODE
+    lib = L.load()
+    with torch.cuda.device(t.device):
+        st = lib.iwq_fill_synthetic(L.ptr(t), t.numel(), L.DTYPE_CODE[t.dtype], int(seed), int(index_offset),
+                                    L.stream_handle(t.device))
+    L.check(st, "iwq_fill_synthetic")
+    return t
+
+
+def selftest_division(device="cuda"):
+    """(fp32 mismatches, fp16 mismatches) of the hot loop's corrected division vs IEEE division."""
+    lib = L.load()
+    counts = torch.zeros(2, dtype=torch.int64, device=device)
+    with torch.cuda.device(counts.device):
+        L.check(lib.iwq_selftest_division(L.ptr(counts), L.stream_handle(counts.device)), "iwq_selftest_division")
+    return tuple(int(x) for x in counts.cpu())

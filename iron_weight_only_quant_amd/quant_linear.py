@@ -1,0 +1,184 @@
+"""Drop-in for the reference's QuantLinear (quant_linear.py:395-1033), INT weight format.
+
+Same constructor signature, buffers (quantized / scales / zeros / weight_fp4/6/8 / weight_bfp_*),
+`quantize_weight()`, `forward()` and `from_linear()` semantics:
+  * `from_linear` aliases the original Linear's weight storage and overwrites it in place with the
+    dequantized weight (:1021-1024, :949), scales/zeros become [G,1] buffers of the weight dtype
+    (:924-932), w_bit >= 16 leaves the layer unquantized (:887-892).
+  * Errors: ValueError for an unknown weight_format (:440-441) or group size (:906),
+    AssertionError when the grouped dimension does not divide (:897).
+Differences by design (documented in DESIGN.md):
+  * the throw-away kaiming init of a fresh [out,in] weight that from_linear immediately replaces
+    (:444, :464; 75 % of the reference's from_linear time) is skipped on that path;
+  * quantization runs in the gfx950 kernels (no CPU path);
+  * `keep_codes=True` additionally keeps the packed integer codes (`qweight`, include/iwq.h layout)
+    for the fused dequant->GEMM forward.
+The FP4/FP6/FP8/BFP and "approximate" research formats (:470-883) are not part of this round's
+hot path and raise NotImplementedError.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import kernels
+
+_FORMATS = {"int", "fp4", "fp6", "fp8", "bfp"}
+
+
+class QuantLinear(nn.Module):
+    def __init__(self, in_features, out_features, bias=True, w_bit=4, w_group_size=128, symmetric=True, mode=0,
+                 weight_format: str = "int", approximate: bool = False, quant_dim: int = 0,
+                 fp8_hi_align_start: int = 12, fp8_hi_align_exp_field: int = 15, fp8_tail_pad_bits: int = 1,
+                 double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
+                 fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
+                 fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, _init_weight: bool = True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.w_bit = w_bit
+        self.w_group_size = w_group_size
+        self.symmetric = symmetric
+        self.mode = mode
+        self.quant_dim = quant_dim
+        raw_format = weight_format.lower()
+        self.weight_format = "bfp" if raw_format.startswith("bfp") else raw_format
+        self.approximate = approximate
+        self.double_approximate = double_approximate
+        self.fp8_hi_align_start = fp8_hi_align_start
+        self.fp8_hi_align_exp_field = fp8_hi_align_exp_field
+        self.fp8_tail_pad_bits = fp8_tail_pad_bits
+        self.fp6_hi_align_start = fp6_hi_align_start
+        self.fp6_hi_align_exp_field = fp6_hi_align_exp_field
+        self.fp6_tail_pad_bits = fp6_tail_pad_bits
+        self.fp4_hi_align_start = fp4_hi_align_start
+        self.fp4_hi_align_exp_field = fp4_hi_align_exp_field
+        self.fp4_tail_pad_bits = fp4_tail_pad_bits
+        self.keep_codes = keep_codes
+        if self.weight_format not in _FORMATS:
+            raise ValueError(f"Unsupported weight_format: {weight_format}")
+
+        if _init_weight:
+            self.weight = nn.Parameter(torch.Tensor(out_features, in_features))
+            if bias:
+                self.bias = nn.Parameter(torch.Tensor(out_features))
+            else:
+                self.register_parameter("bias", None)
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+
+        self.register_buffer("quantized", torch.tensor(False))
+        self.register_buffer("scales", None)
+        self.register_buffer("zeros", None)
+        self.register_buffer("weight_fp4", None)
+        self.register_buffer("weight_fp6", None)
+        self.register_buffer("weight_fp8", None)
+        self.register_buffer("weight_bfp_mantissa", None)
+        self.register_buffer("weight_bfp_exponent", None)
+        self.register_buffer("qweight", None)
+        if _init_weight:
+            self.reset_parameters()
+
+    def reset_parameters(self):
+        nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
+        if self.bias is not None:
+            fan_in, _ = nn.init._calculate_fan_in_and_fan_out(self.weight)
+            bound = 1 / fan_in ** 0.5
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    # ------------------------------------------------------------------------------------------
+    def _scale_shape(self, G):
+        return (G, 1)
+
+    def quantize_weight(self):
+        """quant_linear.py:635-958 — INT branch on the GPU; in-place on self.weight."""
+        with torch.no_grad():
+            if self.approximate or self.weight_format != "int":
+                raise NotImplementedError(
+                    f"weight_format={self.weight_format!r} approximate={self.approximate}: only the INT "
+                    "min-max format is on this build's hot path (SURVEY.md §8f lists the FP codec next)")
+            if self.w_bit >= 16:
+                self.quantized.fill_(False)
+                self.weight_fp4 = None
+                self.weight_fp6 = None
+                self.weight_fp8 = None
+                return
+            if self.w_group_size not in (-1, -2) and not self.w_group_size > 0:
+                raise ValueError("Invalid w_group_size")
+            w = self.weight.data
+            res = kernels.quantize_minmax(w, self.w_bit, self.w_group_size, bool(self.symmetric), self.quant_dim,
+                                          out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None,
+                                          want_codes=self.keep_codes and self.w_bit <= 8)
+            if res.out is not w:
+                w.copy_(res.out)
+            self.scales = res.scales.view(-1, 1)
+            self.zeros = res.zeros.view(-1, 1) if res.zeros is not None else None
+            self.qweight = res.codes
+            self.weight_fp4 = None
+            self.weight_fp6 = None
+            self.weight_fp8 = None
+            self.quantized.fill_(True)
+
+    def forward(self, input):
+        """quant_linear.py:960-972: the dequantized weight already sits in self.weight."""
+        if not self.quantized:
+            return F.linear(input, self.weight, self.bias)
+        original_input_shape = input.shape
+        weight = self.weight.to(input.dtype)
+        out = F.linear(input, weight, self.bias)
+        if input.dim() > 2:
+            out = out.reshape(original_input_shape[:-1] + (self.out_features,))
+        return out
+
+    @classmethod
+    def from_linear(cls, linear_layer, w_bit=4, w_group_size=128, symmetric=False, mode=0,
+                    weight_format: str = "int", approximate: bool = False, quant_dim: int = 0,
+                    fp8_hi_align_start: int = 12, fp8_hi_align_exp_field: int = 15, fp8_tail_pad_bits: int = 1,
+                    double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
+                    fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
+                    fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, quantize: bool = True):
+        """quant_linear.py:974-1033.  `quantize=False` is used by the batched model transform,
+        which has already quantized the weight in one multi-tensor launch."""
+        assert isinstance(linear_layer, nn.Linear), "Input layer must be nn.Linear"
+        q = cls(in_features=linear_layer.in_features, out_features=linear_layer.out_features,
+                bias=linear_layer.bias is not None, w_bit=w_bit, w_group_size=w_group_size, symmetric=symmetric,
+                mode=mode, weight_format=weight_format, approximate=approximate, quant_dim=quant_dim,
+                fp8_hi_align_start=fp8_hi_align_start, fp8_hi_align_exp_field=fp8_hi_align_exp_field,
+                fp8_tail_pad_bits=fp8_tail_pad_bits, double_approximate=double_approximate,
+                fp6_hi_align_start=fp6_hi_align_start, fp6_hi_align_exp_field=fp6_hi_align_exp_field,
+                fp6_tail_pad_bits=fp6_tail_pad_bits, fp4_hi_align_start=fp4_hi_align_start,
+                fp4_hi_align_exp_field=fp4_hi_align_exp_field, fp4_tail_pad_bits=fp4_tail_pad_bits,
+                keep_codes=keep_codes, _init_weight=False)
+        q.weight = nn.Parameter(linear_layer.weight.data.detach(), requires_grad=False)
+        if linear_layer.bias is not None:
+            q.bias = nn.Parameter(linear_layer.bias.data.detach(), requires_grad=False)
+        if quantize:
+            q.quantize_weight()
+        return q
+
+
+class GPTQQuantLinear(nn.Module):
+    """quant_linear.py:1035-1065 — holder for externally quantized weights; forward = F.linear."""
+
+    def __init__(self, weight: torch.Tensor, bias=None):
+        super().__init__()
+        assert weight.dim() == 2, "Weight tensor must be 2-dimensional"
+        self.out_features, self.in_features = weight.shape
+        self.weight = nn.Parameter(weight.clone().detach(), requires_grad=False)
+        if bias is not None:
+            self.bias = nn.Parameter(bias.clone().detach(), requires_grad=False)
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, input):
+        return F.linear(input, self.weight, self.bias)
+
+    @classmethod
+    def from_linear(cls, linear_layer):
+        assert isinstance(linear_layer, nn.Linear), "Input layer must be nn.Linear"
+        layer = cls(linear_layer.weight.data, linear_layer.bias.data if linear_layer.bias is not None else None)
+        if getattr(linear_layer, "scales", None) is not None:
+            layer.scales = linear_layer.scales.clone().detach()
+        if getattr(linear_layer, "zeros", None) is not None:
+            layer.zeros = linear_layer.zeros.clone().detach()
+        return layer

@@ -1,0 +1,91 @@
+"""Drop-in for the reference's quant_wrapper.quantize_model (quant_wrapper.py:7-84), RTN branch.
+
+Same contract: every nn.Linear whose qualified name contains neither 'lm_head' nor 'output_layer'
+is replaced (setattr on its parent) by a QuantLinear that aliases and overwrites the original
+weight storage; weight-only runs need 0 < w_bit < 16 and a_bit None or >= 16 (:10-11).
+
+MI355X-first difference: instead of quantizing layer after layer (one ~16-op ATen chain plus an
+empty_cache per layer, :52-82), all eligible layers that live on one GPU and share a dtype are
+quantized by ONE persistent multi-tensor launch (kernels.BatchPlan) when the group size is a
+power of two in [8, 512]; any other configuration uses one launch per layer.
+"""
+import torch
+
+from . import kernels
+from .quant_linear import QuantLinear
+
+
+def _eligible(name, module):
+    return isinstance(module, torch.nn.Linear) and "lm_head" not in name and "output_layer" not in name
+
+
+def _set_module(model, name, new):
+    parent = model
+    path = name.split(".")
+    for p in path[:-1]:
+        parent = getattr(parent, p)
+    setattr(parent, path[-1], new)
+
+
+def _qkw(args, w_format):
+    return dict(
+        w_bit=args.w_bit, w_group_size=args.w_group_size, symmetric=args.w_symmetric,
+        mode=getattr(args, "mode", 0), weight_format=w_format, approximate=getattr(args, "approximate", False),
+        quant_dim=getattr(args, "quant_dim", 0),
+        fp8_hi_align_start=getattr(args, "fp8_hi_align_start", 12),
+        fp8_hi_align_exp_field=getattr(args, "fp8_hi_align_exp_field", 15),
+        fp8_tail_pad_bits=getattr(args, "fp8_tail_pad_bits", 1),
+        double_approximate=getattr(args, "double_approximate", False),
+        fp6_hi_align_start=getattr(args, "fp6_hi_align_start", 4),
+        fp6_hi_align_exp_field=getattr(args, "fp6_hi_align_exp_field", 7),
+        fp6_tail_pad_bits=getattr(args, "fp6_tail_pad_bits", 2),
+        fp4_hi_align_start=getattr(args, "fp4_hi_align_start", 1),
+        fp4_hi_align_exp_field=getattr(args, "fp4_hi_align_exp_field", 1),
+        fp4_tail_pad_bits=getattr(args, "fp4_tail_pad_bits", 0),
+    )
+
+
+def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True):
+    if not ((args.w_bit is not None and args.w_bit < 16) and (args.a_bit is None or args.a_bit >= 16)):
+        return model
+    assert args.w_bit > 0 and args.w_bit < 16, \
+        "Weight bitwidth should be an integer between [1, 16] for weigth-only quantization, please check."
+    w_format = getattr(args, "w_format", "int").lower()
+    is_bfp = w_format.startswith("bfp")
+    if is_bfp and getattr(args, "w_group_size", -1) <= 0:
+        raise ValueError("BFP quantization needs a positive w_group_size (e.g. 128)")
+    if getattr(args, "gptq", False):
+        raise NotImplementedError("GPTQ calibration is outside this build's hot path (SURVEY.md §2 #8)")
+    if verbose:
+        print("Using RTN (Round-to-Nearest) quantization")
+    kw = _qkw(args, w_format)
+    layers = [(n, m) for n, m in model.named_modules() if _eligible(n, m)]
+
+    done = set()
+    g = kw["w_group_size"]
+    if (batched and w_format == "int" and not kw["approximate"] and kw["quant_dim"] == 0
+            and g in kernels.FAST_GROUPS and 2 <= kw["w_bit"] <= 8 and layers):
+        buckets = {}
+        for n, m in layers:
+            w = m.weight.data
+            if (w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous() and w.shape[1] % g == 0
+                    and w.dtype in (torch.float16, torch.bfloat16, torch.float32)
+                    and w.data_ptr() % 16 == 0):
+                buckets.setdefault((w.device, w.dtype), []).append((n, m))
+        for (dev, dt), items in buckets.items():
+            ws = [m.weight.data for _, m in items]
+            plan = kernels.BatchPlan(ws, kw["w_bit"], g, bool(kw["symmetric"]), outs=ws)
+            plan.run()
+            for i, (n, m) in enumerate(items):
+                q = QuantLinear.from_linear(m, quantize=False, **kw)
+                q.scales = plan.scales[i].view(-1, 1)
+                q.zeros = plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None
+                q.quantized.fill_(True)
+                _set_module(model, n, q)
+                done.add(n)
+    for n, m in layers:
+        if n in done:
+            continue
+        q = QuantLinear.from_linear(m, **kw)
+        _set_module(model, n, q)
+    return model

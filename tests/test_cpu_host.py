@@ -1,0 +1,133 @@
+"""CPU-only checks of the host side: the C-ABI library loads and exports every function that
+include/iwq.h declares, struct layouts agree, host validation and error mapping behave like the
+reference, and nothing silently falls back to the CPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "iwq.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(iwq_[a-z_0-9]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from iron_weight_only_quant_amd import _lib
+    return _lib.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    from iron_weight_only_quant_amd import _lib
+    names = header_functions()
+    assert len(names) >= 9
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(_lib.EXPORTS)
+
+
+def test_build_info_and_status_strings(lib):
+    assert b"gfx950" in lib.iwq_build_info()
+    assert lib.iwq_status_string(0) == b"ok"
+    assert lib.iwq_status_string(3) == b"Invalid w_group_size"
+
+
+def test_batch_entry_layout():
+    from iron_weight_only_quant_amd._lib import IwqBatchEntry
+    assert ctypes.sizeof(IwqBatchEntry) == 64
+
+
+def test_workspace_bytes(lib):
+    assert lib.iwq_workspace_bytes(4096, 4096, 128, 0) == 8 * 4096 * 32
+    assert lib.iwq_workspace_bytes(4096, 4096, -1, 0) == 256
+    assert lib.iwq_workspace_bytes(100, 64, -2, 1) == 512
+    assert lib.iwq_workspace_bytes(4096, 100, 128, 0) == 0  # invalid geometry
+
+
+def test_host_validation_without_gpu(lib):
+    """Argument validation happens on the host before any HIP call."""
+    vp = ctypes.c_void_p
+    call = lib.iwq_quantize_minmax
+    dummy = vp(16)
+    # bad group divisibility (AssertionError in the reference, quant_funcs.py:11)
+    assert call(dummy, 8, 100, 100, 0, 4, 128, 0, 0, None, 100, None, None, None, None, 0, None, 0, None) == 2
+    # invalid group mode (ValueError "Invalid w_group_size", quant_linear.py:906)
+    assert call(dummy, 8, 128, 128, 0, 4, -3, 0, 0, None, 128, None, None, None, None, 0, None, 0, None) == 3
+    # bad dtype / bits / shape
+    assert call(dummy, 8, 128, 128, 7, 4, 128, 0, 0, None, 128, None, None, None, None, 0, None, 0, None) == 5
+    assert call(dummy, 8, 128, 128, 0, 0, 128, 0, 0, None, 128, None, None, None, None, 0, None, 0, None) == 4
+    assert call(dummy, 8, 128, 64, 0, 4, 128, 0, 0, None, 128, None, None, None, None, 0, None, 0, None) == 1
+    # codes with n_bits > 8
+    assert call(dummy, 8, 128, 128, 0, 9, 128, 0, 0, None, 128, dummy, None, None, None, 0, None, 0, None) == 7
+
+
+def test_batch_plan_host(lib):
+    from iron_weight_only_quant_amd._lib import IwqBatchEntry
+    t = (IwqBatchEntry * 3)()
+    shapes = [(4096, 4096), (11008, 4096), (4096, 11008)]
+    for i, (r, c) in enumerate(shapes):
+        t[i].w = 4096 * (i + 1)
+        t[i].out_deq = 4096 * (i + 10)
+        t[i].rows, t[i].cols = r, c
+    total = ctypes.c_int64()
+    assert lib.iwq_batch_plan(t, 3, 0, 4, 128, ctypes.byref(total)) == 0
+    units = [r * c // 512 for r, c in shapes]
+    assert [t[i].unit_begin for i in range(3)] == [0, units[0], units[0] + units[1]]
+    assert total.value == sum(units)
+    t[1].cols = 4100
+    assert lib.iwq_batch_plan(t, 3, 0, 4, 128, ctypes.byref(total)) == 2
+    assert lib.iwq_batch_plan(t, 3, 0, 4, 96, ctypes.byref(total)) == 3
+
+
+def test_no_cpu_fallback():
+    from iron_weight_only_quant_amd.quant_funcs import pseudo_quantize_tensor
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    x = torch.randn(4, 128).half()
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        pseudo_quantize_tensor(x, n_bits=4, q_group_size=128)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        QuantLinear.from_linear(torch.nn.Linear(128, 4).half(), w_bit=4, w_group_size=128)
+
+
+def test_geometry_errors_mirror_reference():
+    from iron_weight_only_quant_amd.kernels import group_geometry
+    assert group_geometry(4096, 11008, 128, 0) == (128, 4096 * 86)
+    assert group_geometry(4096, 11008, -2, 0) == (11008, 4096)
+    assert group_geometry(4096, 11008, -2, 1) == (4096, 11008)
+    assert group_geometry(64, 32, -1, 1) == (2048, 1)
+    with pytest.raises(AssertionError):
+        group_geometry(100, 64, 128, 0)
+    with pytest.raises(ValueError, match="Invalid w_group_size"):
+        group_geometry(100, 64, 0, 0)
+
+
+def test_quant_wrapper_noop_paths():
+    from types import SimpleNamespace
+
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+    m = torch.nn.Sequential(torch.nn.Linear(8, 8))
+    assert quantize_model(m, SimpleNamespace(w_bit=16, a_bit=16)) is m  # not weight-only
+    assert isinstance(m[0], torch.nn.Linear)
+    with pytest.raises(NotImplementedError):
+        quantize_model(m, SimpleNamespace(w_bit=4, a_bit=16, w_group_size=128, w_symmetric=False, gptq=True),
+                       verbose=False)
+
+
+def test_synth_generator_properties():
+    from oracle.synth import synth
+    x = synth(0, (512, 512), "float16").astype(np.float32)
+    assert abs(float(x.mean())) < 1e-3
+    assert 0.018 < float(x.std()) < 0.025
+    a = synth(5, (4, 1000), "float32")
+    b = synth(5, (4, 1000), "float32")
+    assert np.array_equal(a, b)
+    # counter-based: any sub-range can be regenerated from its offset
+    from oracle.synth import synth_f32
+    assert np.array_equal(synth_f32(5, 1500, 100), a.reshape(-1)[1500:1600])

@@ -1,0 +1,310 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) vs the golden fixtures the reference produced
+and vs the CPU oracle.  Bit-exact for dequantized values, scales, zero-points and integer codes."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import iwq_oracle as O
+from oracle.synth import synth
+
+from .golden_util import GOLD, bits_equal, load_edge, load_small, sha
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+TD = {"float16": torch.float16, "bfloat16": torch.bfloat16, "float32": torch.float32}
+
+
+def to_dev(a, dtype):
+    a = np.ascontiguousarray(a)
+    if dtype == "bfloat16":
+        return torch.from_numpy(a.view(np.int16)).view(torch.bfloat16).to(DEV)
+    return torch.from_numpy(a).to(DEV)
+
+
+def to_np(t):
+    t = t.detach().contiguous().cpu()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
+
+
+@pytest.fixture(scope="module")
+def K():
+    from iron_weight_only_quant_amd import kernels
+    return kernels
+
+
+def test_native_library_is_loaded(K):
+    from iron_weight_only_quant_amd import _lib
+    lib = _lib.load()
+    assert os.path.exists(_lib.LIB_PATH)
+    assert b"gfx950" in lib.iwq_build_info()
+
+
+def test_division_selftest(K):
+    bad32, bad16 = K.selftest_division(DEV)
+    assert bad16 == 0, bad16
+    assert bad32 == 0, bad32
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_synthetic_generator_matches_oracle(K, dtype):
+    shape = (333, 1000)
+    t = torch.empty(shape, dtype=TD[dtype], device=DEV)
+    K.fill_synthetic(t, 11)
+    exp = synth(11, shape, dtype)
+    assert bits_equal(to_np(t), exp)
+
+
+FLAG_SETS = [0, 1]  # 0: specialised kernels, 1: IWQ_FLAG_FORCE_GENERIC (universal path)
+
+
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_golden_small_quant_funcs(K, flags):
+    """Every pseudo_quantize_tensor case of the golden set; kernel called at C-ABI level."""
+    d = load_small()
+    n = 0
+    for key in d.files:
+        if not key.startswith("qf/"):
+            continue
+        _, tag, dtype, bits, zp, g, pt = key.split("/")
+        exp = d[key]
+        x = to_dev(d[f"in/{tag}/{dtype}"], dtype)
+        g, pt = int(g), bool(int(pt))
+        group = -1 if pt else (g if g > 0 else -2)
+        res = K.quantize_minmax(x, int(bits), group, not bool(int(zp)), 0, flags=flags)
+        if exp.size == 0:
+            assert res.has_nan(), key
+            continue
+        assert not res.has_nan(), key
+        assert bits_equal(to_np(res.out), exp), key
+        n += 1
+    assert n > 50
+
+
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_golden_small_quantlinear(K, flags):
+    d = load_small()
+    n = 0
+    for key in d.files:
+        if not (key.startswith("ql/") and key.endswith("/deq")):
+            continue
+        _, tag, dtype, bits, sym, g, qd, _ = key.split("/")
+        base = key[:-4]
+        x = to_dev(d[f"in/{tag}/{dtype}"], dtype)
+        res = K.quantize_minmax(x, int(bits), int(g), bool(int(sym)), int(qd), flags=flags)
+        assert bits_equal(to_np(res.out), d[key]), key
+        assert bits_equal(to_np(res.scales), d[base + "/scales"].reshape(-1)), key
+        if base + "/zeros" in d.files:
+            assert bits_equal(to_np(res.zeros), d[base + "/zeros"].reshape(-1)), key
+        n += 1
+    assert n > 50
+
+
+def test_golden_small_python_face():
+    """The drop-in Python API (quant_funcs / QuantLinear) reproduces the golden outputs."""
+    from iron_weight_only_quant_amd.quant_funcs import pseudo_quantize_tensor
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    d = load_small()
+    for key in d.files:
+        if key.startswith("qf/") and "/float16/" in key:
+            _, tag, dtype, bits, zp, g, pt = key.split("/")
+            x = to_dev(d[f"in/{tag}/{dtype}"], dtype)
+            kw = dict(n_bits=int(bits), zero_point=bool(int(zp)), q_group_size=int(g), per_tensor=bool(int(pt)))
+            if d[key].size == 0:
+                with pytest.raises(AssertionError):
+                    pseudo_quantize_tensor(x, **kw)
+                continue
+            assert bits_equal(to_np(pseudo_quantize_tensor(x, **kw)), d[key]), key
+            y = x.clone()
+            r = pseudo_quantize_tensor(y, inplace=True, **kw)
+            assert bits_equal(to_np(y), d[key]) and r.data_ptr() == y.data_ptr(), key
+        if key.startswith("ql/") and key.endswith("/deq"):
+            _, tag, dtype, bits, sym, g, qd, _ = key.split("/")
+            base = key[:-4]
+            x = to_dev(d[f"in/{tag}/{dtype}"], dtype)
+            lin = torch.nn.Linear(x.shape[1], x.shape[0], bias=False).to(DEV)
+            lin.weight.data = x
+            q = QuantLinear.from_linear(lin, w_bit=int(bits), w_group_size=int(g), symmetric=bool(int(sym)),
+                                        quant_dim=int(qd))
+            assert q.weight.data.data_ptr() == x.data_ptr()  # aliases the Linear's storage
+            assert bits_equal(to_np(x), d[key]), key
+            assert bits_equal(to_np(q.scales), d[base + "/scales"]), key
+            if base + "/zeros" in d.files:
+                assert bits_equal(to_np(q.zeros), d[base + "/zeros"]), key
+            else:
+                assert q.zeros is None
+
+
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_golden_edge_rows(K, flags):
+    d = load_edge()
+    e = d["in/edge"]
+    fin = d["in/edge_finite_rows"]
+    x_all = to_dev(e, "float16")
+    x_fin = to_dev(e[fin], "float16")
+    for bits in (2, 3, 4, 8):
+        for zp in (True, False):
+            r = K.quantize_minmax(x_fin, bits, 128, not zp, 0, flags=flags)
+            assert not r.has_nan()
+            assert bits_equal(to_np(r.out), d[f"qf/edge/{bits}/{int(zp)}"]), (bits, zp)
+            r = K.quantize_minmax(x_all, bits, 128, not zp, 0, flags=flags)
+            exp_all = d[f"qf/edge_all/{bits}/{int(zp)}"]
+            assert r.has_nan() == (exp_all.size == 0)
+            base = f"ql/edge_all/{bits}/{int(not zp)}"
+            assert bits_equal(to_np(r.out), d[base + "/deq"], nan_equal=True), (bits, zp)
+            assert bits_equal(to_np(r.scales), d[base + "/scales"].reshape(-1), nan_equal=True)
+            if zp:
+                zr = to_np(r.zeros)
+                ze = d[base + "/zeros"].reshape(-1)
+                ox = O.quantlinear_int(e, w_bit=bits, w_group_size=128, symmetric=False)
+                assert bits_equal(zr, ox.zeros.reshape(-1), nan_equal=True)  # oracle's -0 < +0 convention
+                assert np.array_equal(zr.astype(np.float32), ze.astype(np.float32), equal_nan=True)
+
+
+@pytest.mark.parametrize("flags", FLAG_SETS)
+def test_golden_nonfinite(K, flags):
+    d = load_edge()
+    x = to_dev(d["in/nonfinite"], "float16")
+    for zp in (True, False):
+        r = K.quantize_minmax(x, 4, 128, not zp, 0, flags=flags)
+        assert r.has_nan()  # quant_funcs.py:40 would assert
+        base = f"ql/nonfinite/{int(not zp)}"
+        assert bits_equal(to_np(r.out), d[base + "/deq"], nan_equal=True)
+        assert bits_equal(to_np(r.scales), d[base + "/scales"].reshape(-1), nan_equal=True)
+
+
+def _large_cases():
+    spec = json.load(open(os.path.join(GOLD, "int_large.json")))
+    return spec["cases"]
+
+
+@pytest.mark.parametrize("name", ["q_proj", "gate_proj", "down_proj"])
+def test_llama_shapes_vs_reference_sha(K, name):
+    """Full Llama-2-7B weight shapes: GPU-generated synthetic input -> kernels -> SHA-256 equal to
+    the reference's own outputs on the same input (tests/golden/int_large.json)."""
+    cases = [c for c in _large_cases() if c["name"] == name]
+    inp = cases[0]
+    x = torch.empty(tuple(inp["shape"]), dtype=torch.float16, device=DEV)
+    K.fill_synthetic(x, inp["seed"])
+    assert sha(to_np(x)) == inp["sha_input"]
+    for c in cases[1:]:
+        if c["kind"] == "qf":
+            g = c["q_group_size"]
+            r = K.quantize_minmax(x, c["n_bits"], g if g > 0 else -2, not c["zero_point"], 0)
+            assert not r.has_nan()
+            assert sha(to_np(r.out)) == c["sha_deq"], c
+        else:
+            r = K.quantize_minmax(x, c["w_bit"], c["w_group_size"], c["symmetric"], 0)
+            assert sha(to_np(r.out)) == c["sha_deq"], c
+            assert sha(to_np(r.scales).reshape(-1, 1)) == c["sha_scales"], c
+            if c["sha_zeros"] is not None:
+                assert sha(to_np(r.zeros).reshape(-1, 1)) == c["sha_zeros"], c
+
+
+@pytest.mark.parametrize("bits", [2, 3, 4, 8])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("mode", [(128, 0), (32, 0), (-2, 0), (-1, 0), (16, 1), (-2, 1)])
+def test_codes_match_oracle(K, bits, sym, mode):
+    g, qd = mode
+    x_np = synth(21, (96, 512), "float16")
+    x = to_dev(x_np, "float16")
+    ref = O.quantlinear_int(x_np, w_bit=bits, w_group_size=g, symmetric=sym, quant_dim=qd)
+    for flags in FLAG_SETS:
+        r = K.quantize_minmax(x, bits, g, sym, qd, want_codes=True, flags=flags)
+        assert bits_equal(to_np(r.out), ref.dequant)
+        assert np.array_equal(r.codes.cpu().numpy(), O.pack_codes(ref.codes, bits).reshape(-1)), (flags,)
+
+
+def test_batched_matches_single(K):
+    shapes = [(256, 512), (128, 1024), (384, 256), (64, 2048), (8, 128)]
+    ws = []
+    for i, s in enumerate(shapes):
+        t = torch.empty(s, dtype=torch.float16, device=DEV)
+        K.fill_synthetic(t, 40 + i)
+        ws.append(t)
+    for sym in (False, True):
+        plan = K.BatchPlan(ws, 4, 128, sym, want_codes=True)
+        plan.run()
+        torch.cuda.synchronize()
+        assert plan.nan_flag.item() == 0
+        for i, w in enumerate(ws):
+            r = K.quantize_minmax(w, 4, 128, sym, 0, want_codes=True)
+            assert torch.equal(plan.outs[i].view(torch.int16), r.out.view(torch.int16))
+            assert torch.equal(plan.scales[i].view(torch.int16), r.scales.view(torch.int16))
+            assert torch.equal(plan.codes[i], r.codes)
+            if not sym:
+                assert torch.equal(plan.zeros[i].view(torch.int16), r.zeros.view(torch.int16))
+
+
+def test_quantize_model_drop_in(K):
+    from types import SimpleNamespace
+
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+
+    torch.manual_seed(0)
+    specs = {"l0": (384, 256, True), "l1": (256, 384, False), "lm_head": (1000, 256, False)}
+    originals = {n: (torch.randn(o, i) * 0.02).half() for n, (o, i, _) in specs.items()}
+    for batched in (True, False):
+        m = torch.nn.Sequential()
+        for n, (o, i, b) in specs.items():
+            lin = torch.nn.Linear(i, o, bias=b).half().to(DEV)
+            lin.weight.data.copy_(originals[n])
+            m.add_module(n, lin)
+        args = SimpleNamespace(w_bit=4, a_bit=16, w_group_size=128, w_symmetric=False, w_format="int", quant_dim=0)
+        quantize_model(m, args, batched=batched, verbose=False)
+        assert isinstance(m.l0, QuantLinear) and isinstance(m.l1, QuantLinear)
+        assert isinstance(m.lm_head, torch.nn.Linear) and not isinstance(m.lm_head, QuantLinear)
+        for n in ("l0", "l1"):
+            ref = O.quantlinear_int(originals[n].numpy(), w_bit=4, w_group_size=128, symmetric=False)
+            q = getattr(m, n)
+            assert bits_equal(to_np(q.weight.data), ref.dequant), (n, batched)
+            assert bits_equal(to_np(q.scales), ref.scales), (n, batched)
+            assert bits_equal(to_np(q.zeros), ref.zeros), (n, batched)
+        assert torch.equal(m.lm_head.weight.data.cpu(), originals["lm_head"])
+        x = torch.randn(2, 5, 256, dtype=torch.float16, device=DEV)
+        y = m.l0(x)
+        torch.testing.assert_close(y, torch.nn.functional.linear(x, m.l0.weight, m.l0.bias))
+
+
+def test_errors_match_reference(K):
+    from iron_weight_only_quant_amd.quant_funcs import pseudo_quantize_tensor
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    x = torch.randn(8, 100, dtype=torch.float16, device=DEV)
+    with pytest.raises(AssertionError):
+        pseudo_quantize_tensor(x, n_bits=4, q_group_size=128)          # quant_funcs.py:11
+    with pytest.raises(AssertionError):
+        pseudo_quantize_tensor(torch.randn(2, 3, 4, device=DEV).half())  # quant_funcs.py:15
+    lin = torch.nn.Linear(100, 8).half().to(DEV)
+    with pytest.raises(ValueError):
+        QuantLinear.from_linear(lin, w_bit=4, w_group_size=-3)          # quant_linear.py:906
+    with pytest.raises(AssertionError):
+        QuantLinear.from_linear(torch.nn.Linear(100, 8).half().to(DEV), w_bit=4, w_group_size=64)  # :897
+    with pytest.raises(ValueError):
+        QuantLinear(4, 4, weight_format="int3")                          # :440-441
+
+
+def test_ragged_and_strided_inputs(K):
+    """Unaligned / strided / odd shapes take the universal path and still match the oracle."""
+    base_np = synth(77, (37, 262), "float16")
+    base = to_dev(base_np, "float16")
+    view = base[:, 3:259]            # row stride 262, 256 columns, not 16-B aligned
+    v_np = np.ascontiguousarray(base_np[:, 3:259])
+    for g in (128, 64, -2, -1):
+        r = K.quantize_minmax(view, 4, g, False, 0)
+        ref = O.quantlinear_int(v_np, w_bit=4, w_group_size=g, symmetric=False)
+        assert bits_equal(to_np(r.out), ref.dequant), g
+        assert bits_equal(to_np(r.scales), ref.scales.reshape(-1)), g
+    odd_np = synth(78, (13, 7), "float16")
+    r = K.quantize_minmax(to_dev(odd_np, "float16"), 3, -2, True, 0)
+    assert bits_equal(to_np(r.out), O.quantlinear_int(odd_np, w_bit=3, w_group_size=-2, symmetric=True).dequant)
+    for nb in (9, 12, 15):
+        x_np = synth(79, (16, 256), "float16")
+        r = K.quantize_minmax(to_dev(x_np, "float16"), nb, 128, False, 0)
+        ref = O.quantlinear_int(x_np, w_bit=nb, w_group_size=128, symmetric=False)
+        assert bits_equal(to_np(r.out), ref.dequant, nan_equal=True), nb

@@ -132,3 +132,24 @@ def test_large_llama_shapes_sha(case_idx):
             assert sha(r.dequant) == c["sha_deq"], c
             assert sha(r.scales) == c["sha_scales"], c
             assert sha(r.zeros) == c["sha_zeros"], c
+
+
+def test_torch_restatement_matches_golden():
+    """bench.py's CPU baseline (oracle/torch_ref.py) is pinned to the reference's outputs too."""
+    import torch
+
+    from oracle.torch_ref import minmax_fake_quant_cpu
+    d = load_small()
+    n = 0
+    for key in d.files:
+        if not (key.startswith("qf/") and "/float16/" in key):
+            continue
+        _, tag, dtype, bits, zp, g, pt = key.split("/")
+        x = torch.from_numpy(d[f"in/{tag}/{dtype}"].copy())
+        exp = d[key]
+        if exp.size == 0:
+            continue
+        out = minmax_fake_quant_cpu(x, int(bits), bool(int(zp)), int(g), bool(int(pt)))
+        assert bits_equal(out.numpy(), exp), key
+        n += 1
+    assert n > 30

@@ -1,0 +1,35 @@
+#!/bin/bash
+# One gpurun session: GPU tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/abort/timeout (status >= 2 other than pytest's
+# "tests failed" = 1) ends the session immediately.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 tmo=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+  local st=$?
+  echo "=== $name exit $st"
+  tail -n 5 "$OUT/$name.log"
+  if [ $st -ne 0 ] && [ $st -ne 1 ]; then echo "ABORT session after $name (status $st)"; exit $st; fi
+  return $st
+}
+WHAT=${1:-all}
+if [[ $WHAT == all || $WHAT == *tests* ]]; then
+  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider
+fi
+if [[ $WHAT == all || $WHAT == *smoke* ]]; then
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ $WHAT == all || $WHAT == *bench* ]]; then
+  step bench 600 python bench.py
+fi
+if [[ $WHAT == all || $WHAT == *prof* ]]; then
+  cd /tmp
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2
+  cd "$ROOT"
+fi
+echo "=== session done"
