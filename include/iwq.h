@@ -119,9 +119,10 @@ const char* iwq_status_string(int status);
 int iwq_last_hip_error(void);            /* last hipError_t seen by this thread (0 = none) */
 const char* iwq_build_info(void);        /* arch, compile flags, version */
 
-/* Test-only self check of the reciprocal-corrected fp32 division used in the hot loop against IEEE
- * division, over every finite fp16 numerator x every fp16 divisor in [2^-24, 65504].  Writes the
- * mismatch counts (fp32 bits, fp16-rounded) to d_counts[0..1]. */
+/* Test-only self check of the fast reciprocal and corrected fp32 division used in the hot loop
+ * against IEEE division, over every finite fp16 numerator x every fp16 divisor in [2^-24, 65504].
+ * Writes mismatch counts to d_counts[0..2]: quotient fp32 bits, quotient after fp16 rounding,
+ * reciprocal fp32 bits. */
 int iwq_selftest_division(uint64_t* d_counts, void* stream);
 
 #ifdef __cplusplus

@@ -3,7 +3,10 @@
 // Numerics contract (SURVEY.md §7 "Hard parts", §8a): the reference evaluates
 //   quant_funcs.py:16-38  /  quant_linear.py:909-947
 // as a chain of ATen ops on 16-bit tensors; each op computes in fp32 and rounds RNE to the
-// storage dtype.  Every function below that is marked "R()" reproduces one such rounding.
+// storage dtype.  The *exact* path below replays that chain literally (one rounding per op).
+// The *fast* path (fp16, finite groups) computes the same bits with fewer instructions; each
+// shortcut is justified next to it and the two non-obvious ones (reciprocal, corrected
+// division) are checked exhaustively over all fp16 operands by iwq_selftest_division.
 // Compiled with -ffp-contract=off and IEEE fp32 division (no fast-math).
 #pragma once
 
@@ -15,8 +18,28 @@ namespace iwq {
 enum : int { DT_F16 = 0, DT_BF16 = 1, DT_F32 = 2 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int WAVE = 64;
+
+// Global-address-space views: plain `T*` kernel pointers are generic (flat) to the compiler, and
+// flat loads are counted on both vmcnt and lgkmcnt, which forces full drains between them.
+#define IWQ_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ IWQ_GLOBAL T* gp(void* p) { return (IWQ_GLOBAL T*)(p); }
+template <typename T>
+__device__ __forceinline__ const IWQ_GLOBAL T* gp(const void* p) { return (const IWQ_GLOBAL T*)(p); }
+
+// Value barrier: forces x to exist as an fp32 register value.  Stops LLVM from folding
+// "fptrunc(fma(..))" into one v_fma_mixlo_f16 (a single rounding straight to fp16, which is NOT
+// RN16(RN32(.))) and "fptrunc(fdiv(fpext, fpext))" into an fp16 division.
+__device__ __forceinline__ float opaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
 // ---------------------------------------------------------------------------------------------
 // storage formats
@@ -34,7 +57,7 @@ struct Fmt<DT_F16> {
   __device__ __forceinline__ static uint32_t from_f(float x) {
     return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x);  // v_cvt_f16_f32, RNE
   }
-  __device__ __forceinline__ static float R(float x) { return (float)(_Float16)x; }
+  __device__ __forceinline__ static float R(float x) { return (float)(_Float16)opaque(x); }
 };
 
 template <>
@@ -45,7 +68,7 @@ struct Fmt<DT_BF16> {
   __device__ __forceinline__ static uint32_t from_f(float x) {
     return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x);  // v_cvt_pk_bf16_f32, RNE, NaN-preserving
   }
-  __device__ __forceinline__ static float R(float x) { return to_f(from_f(x)); }
+  __device__ __forceinline__ static float R(float x) { return to_f(from_f(opaque(x))); }
 };
 
 template <>
@@ -94,20 +117,39 @@ __device__ __forceinline__ float clamp_nan(float x, float lo, float hi) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// fast reciprocal / division for operands that are fp16 values (held in fp32)
+// ---------------------------------------------------------------------------------------------
+// RN32(1/s) for every positive finite fp16 s: v_rcp_f32 (<= 1 ulp) + one Newton step.
+// (exhaustively checked, iwq_selftest_division counter 2)
+__device__ __forceinline__ float rcp_f16val(float s) {
+  float r = __builtin_amdgcn_rcpf(s);
+  float e = __builtin_fmaf(-s, r, 1.0f);
+  return __builtin_fmaf(e, r, r);
+}
+// RN32(w/s) given rs = RN32(1/s) (Markstein: q0 = RN(w*rs), the residual w - q0*s is exact in one
+// fma, q1 = RN(q0 + e*rs) is the correctly rounded quotient).  Exhaustive over all finite fp16 w
+// and all positive fp16 s: iwq_selftest_division counters 0/1.
+__device__ __forceinline__ float div_f16vals(float w, float s, float rs) {
+  float q0 = w * rs;
+  float e = __builtin_fmaf(-q0, s, w);
+  return opaque(__builtin_fmaf(e, rs, q0));
+}
+
+// ---------------------------------------------------------------------------------------------
 // per-group parameters
 // ---------------------------------------------------------------------------------------------
 struct GroupParams {
   float s;    // scale (storage-rounded)
-  float rs;   // RN(1/s) (fp32), for the reciprocal-corrected division
-  float z;    // zero point (storage-rounded; 0 for symmetric)
+  float rs;   // RN(1/s) (fp32), for the corrected division
+  float z;    // zero point (storage-rounded; +0 for symmetric)
   float lo;   // min_int (storage-rounded)
   float hi;   // max_int (storage-rounded)
-  bool fast;  // the fast elementwise path is exact for this group (see quant_fast)
+  bool fast;  // the fast elementwise path is exact for this group
 };
 
-// zero_point=True branch: quant_funcs.py:17-22 == quant_linear.py:917-922
+// zero_point=True branch, literal op chain: quant_funcs.py:17-22 == quant_linear.py:917-922
 template <int DT>
-__device__ __forceinline__ GroupParams params_asym(float mn, float mx, int n_bits) {
+__device__ __forceinline__ GroupParams params_asym_exact(float mn, float mx, int n_bits) {
   using F = Fmt<DT>;
   GroupParams p;
   const float max_int = (float)((1u << n_bits) - 1u);
@@ -120,14 +162,13 @@ __device__ __forceinline__ GroupParams params_asym(float mn, float mx, int n_bit
   p.lo = 0.0f;
   p.z = clamp_nan(-__builtin_rintf(zq), 0.0f, p.hi);   // (-round(.)).clamp_(0, max_int); -0 kept
   p.rs = 1.0f / p.s;
-  p.fast = (DT == DT_F16) && (n_bits <= 10) && (p.s > 0.0f) && (p.s <= 3.0e38f) &&
-           (p.z == p.z) && (p.z <= 65504.0f);
+  p.fast = false;
   return p;
 }
 
-// zero_point=False branch: quant_funcs.py:24-29 == quant_linear.py:910-915
+// zero_point=False branch, literal op chain: quant_funcs.py:24-29 == quant_linear.py:910-915
 template <int DT>
-__device__ __forceinline__ GroupParams params_sym(float amax, int n_bits) {
+__device__ __forceinline__ GroupParams params_sym_exact(float amax, int n_bits) {
   using F = Fmt<DT>;
   GroupParams p;
   const float max_int = (float)((1u << (n_bits - 1)) - 1u);
@@ -138,15 +179,67 @@ __device__ __forceinline__ GroupParams params_sym(float amax, int n_bits) {
   p.hi = F::R(max_int);
   p.lo = F::R(-(float)(1u << (n_bits - 1)));
   p.rs = 1.0f / p.s;
-  p.fast = (DT == DT_F16) && (n_bits <= 10) && (p.s > 0.0f) && (p.s <= 3.0e38f);
+  p.fast = false;
   return p;
 }
 
+// Same values for fp16 groups with a finite range and a nonzero scale, n_bits <= 10, without
+// IEEE divisions: rng/max_int and mn/s are quotients of fp16 values -> div_f16vals.
+// rmax = RN32(1/max_int) (per-kernel constant).  Otherwise falls back to the exact chain.
+template <int DT>
+__device__ __forceinline__ GroupParams params_asym(float mn, float mx, int n_bits, float rmax) {
+  if constexpr (DT == DT_F16) {
+    if (n_bits <= 10) {
+      GroupParams p;
+      const float max_int = (float)((1u << n_bits) - 1u);
+      const float eps = (float)(_Float16)1e-5f;
+      float rng = (float)(_Float16)(mx - mn);  // exact-then-round == ATen's fp16 subtraction
+      rng = rng < eps ? eps : rng;
+      p.s = (float)(_Float16)div_f16vals(rng, max_int, rmax);
+      p.rs = rcp_f16val(p.s);
+      p.hi = max_int;                          // exact in fp16 for n_bits <= 10
+      p.lo = 0.0f;
+      float zq = (float)(_Float16)div_f16vals(mn, p.s, p.rs);
+      p.z = clamp_nan(-__builtin_rintf(zq), 0.0f, p.hi);
+      // rng finite (so mn, mx finite) and s > 0: every shortcut above is exact; z is finite
+      // because the clamp maps +-inf into [0, max_int].
+      p.fast = (rng <= 65504.0f) && (p.s > 0.0f);
+      if (p.fast) return p;
+    }
+  }
+  return params_asym_exact<DT>(mn, mx, n_bits);
+}
+
+template <int DT>
+__device__ __forceinline__ GroupParams params_sym(float amax, int n_bits, float rmax) {
+  if constexpr (DT == DT_F16) {
+    if (n_bits <= 10) {
+      GroupParams p;
+      const float max_int = (float)((1u << (n_bits - 1)) - 1u);
+      const float eps = (float)(_Float16)1e-5f;
+      float m = amax < eps ? eps : amax;
+      p.s = (float)(_Float16)div_f16vals(m, max_int, rmax);
+      p.rs = rcp_f16val(p.s);
+      p.z = 0.0f;
+      p.hi = max_int;
+      p.lo = -(float)(1u << (n_bits - 1));
+      p.fast = (m <= 65504.0f) && (p.s > 0.0f);
+      if (p.fast) return p;
+    }
+  }
+  return params_sym_exact<DT>(amax, n_bits);
+}
+
+// reciprocal of max_int used by the fast parameter path (IEEE division, once per thread)
+__device__ __forceinline__ float rmax_for(int n_bits, bool sym) {
+  const float max_int = sym ? (float)((1u << (n_bits - 1)) - 1u) : (float)((1u << n_bits) - 1u);
+  return 1.0f / max_int;
+}
+
 // ---------------------------------------------------------------------------------------------
-// elementwise quantize->dequantize
+// elementwise quantize->dequantize, exact path: literally the reference op chain, each op rounded
+// to the storage dtype.  Handles NaN/inf/zero scales exactly as ATen does.
 // ---------------------------------------------------------------------------------------------
-// Exact path: literally the reference op chain, each op rounded to the storage dtype.
-// Handles NaN/inf/zero scales exactly as ATen does.  c_out receives the clamped integer value.
 template <int DT, bool SYM>
 __device__ __forceinline__ float quant_exact(float w, const GroupParams& p, float& c_out) {
   using F = Fmt<DT>;
@@ -163,28 +256,82 @@ __device__ __forceinline__ float quant_exact(float w, const GroupParams& p, floa
   }
 }
 
-// Fast path (fp16 storage, finite positive scale, finite zero point, n_bits <= 10):
-//  * w/s via Markstein's reciprocal correction: q0 = RN(w*rs), e = fma(-q0, s, w) (exact),
-//    q1 = RN(e*rs + q0) == RN32(w/s) for rs = RN32(1/s).  Then RN16 of it equals RN16 of the IEEE
-//    fp32 quotient.  Verified exhaustively over all fp16 (w, s) pairs by iwq_selftest_division.
-//  * r + z needs no rounding: integers below 2^11 are exact in fp16 and anything larger is
-//    clamped to max_int <= 1023 either way; the clamp is a single v_med3_f32 (no NaN can occur).
-//  * (c - z) is exact (small integers).
-template <bool SYM>
-__device__ __forceinline__ float quant_fast_f16(float w, const GroupParams& p, float& c_out) {
-  float q0 = w * p.rs;
-  float e = __builtin_fmaf(-q0, p.s, w);
-  float q1 = __builtin_fmaf(e, p.rs, q0);
-  float t = (float)(_Float16)q1;
-  float r = __builtin_rintf(t);
-  float a = r + p.z;                       // symmetric: z == +0 -> normalises -0 like "+ 0"
-  float c = __builtin_amdgcn_fmed3f(a, p.lo, p.hi);
-  c_out = c;
-  if constexpr (SYM) {
-    return c * p.s;                        // caller rounds to fp16 on store
-  } else {
-    return (c - p.z) * p.s;
+// Per-element form of the fast path (used where neighbouring elements belong to different groups,
+// e.g. quant_dim = 1).  Same arguments as quant2_fast; r = rint(t) exactly here.
+template <int DT, bool SYM>
+__device__ __forceinline__ float quant_exact_or_fast(float w, const GroupParams& p, float& c_out) {
+  if constexpr (DT == DT_F16) {
+    if (p.fast) {
+      const float t = (float)(_Float16)div_f16vals(w, p.s, p.rs);
+      const float r = __builtin_rintf(t);
+      const float a = r + p.z;  // exact below 2^11; larger values clamp to the same bound
+      const float c = __builtin_amdgcn_fmed3f(a, p.lo, p.hi);
+      c_out = c;
+      return SYM ? c * p.s : (c - p.z) * p.s;  // exact fp32 product; rounded once on store
+    }
   }
+  return quant_exact<DT, SYM>(w, p, c_out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// elementwise fast path: fp16 pairs in packed math (p.fast groups only)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ uint32_t as_u32(h2 h) { return __builtin_bit_cast(uint32_t, h); }
+__device__ __forceinline__ h2 pk_max(h2 a, h2 b) {
+  h2 r;
+  asm("v_pk_max_f16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ h2 pk_min(h2 a, h2 b) {
+  h2 r;
+  asm("v_pk_min_f16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+struct FastPk {  // group constants broadcast to both halves
+  h2 z, lo, hi, s, codeoff;  // codeoff = code offset + 1024 (see codes below)
+};
+template <bool SYM>
+__device__ __forceinline__ FastPk fast_pk(const GroupParams& p, int n_bits) {
+  FastPk k;
+  k.z = h2{(_Float16)p.z, (_Float16)p.z};
+  k.lo = h2{(_Float16)p.lo, (_Float16)p.lo};
+  k.hi = h2{(_Float16)p.hi, (_Float16)p.hi};
+  k.s = h2{(_Float16)p.s, (_Float16)p.s};
+  const float off = (SYM ? (float)(1u << (n_bits - 1)) : 0.0f) + 1024.0f;
+  k.codeoff = h2{(_Float16)off, (_Float16)off};
+  return k;
+}
+
+// Two fp16 weights -> two dequantized fp16 (bit pattern) + two clamped integer values c (fp16).
+//  t = RN16(w/s)           corrected division in fp32 + v_cvt_pk_f16_f32 (RNE)
+//  r = rint(t)             (t + m) - m with m = copysign(1024, t): RNE to an integer for |t| < 1024;
+//                          for |t| >= 1024 it stays >= 1024 in magnitude with t's sign, and such
+//                          values clamp to the same bound as rint(t) (|bounds| <= 1023).  r is never
+//                          -0, which matches "round(.) + zeros" (-0 + z) for every z the clamp can
+//                          see (outputs and codes identical).
+//  a = r + z, c = clamp    v_pk_add_f16, v_pk_max_f16/v_pk_min_f16 (no NaN can occur here)
+//  y = (c - z) * s         exact difference, one correctly rounded fp16 product == RN16(RN32(.))
+template <bool SYM>
+__device__ __forceinline__ uint32_t quant2_fast(uint32_t wpair, const GroupParams& p, const FastPk& k,
+                                                uint32_t& cpair) {
+  const h2 w = as_h2(wpair);
+  const float q0 = div_f16vals((float)w.x, p.s, p.rs);
+  const float q1 = div_f16vals((float)w.y, p.s, p.rs);
+  const h2 t = __builtin_convertvector((f2){q0, q1}, h2);
+  const h2 m = as_h2((as_u32(t) & 0x80008000u) | 0x64006400u);
+  const h2 r = (t + m) - m;
+  const h2 c = pk_min(pk_max(r + k.z, k.lo), k.hi);
+  cpair = as_u32(c);
+  if constexpr (SYM) return as_u32(c * k.s);
+  else return as_u32((c - k.z) * k.s);
+}
+
+// integer codes of two clamped values: c + off + 1024 lies in [1024, 2048) where fp16 spacing is 1,
+// so its low 10 mantissa bits ARE the code.
+__device__ __forceinline__ uint32_t codes2_fast(uint32_t cpair, const FastPk& k) {
+  return as_u32(as_h2(cpair) + k.codeoff) & 0x03FF03FFu;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -197,7 +344,6 @@ __device__ __forceinline__ int32_t dpp(int32_t x) {
   return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
 }
 
-// All-reduce min and max over aligned groups of N lanes (N power of two, 1..64).
 template <int N>
 __device__ __forceinline__ void group_minmax(int32_t& mn, int32_t& mx) {
   if constexpr (N >= 2) { mn = min(mn, dpp<0xB1>(mn)); mx = max(mx, dpp<0xB1>(mx)); }
@@ -237,7 +383,7 @@ struct Vec8 {
     }
   }
   __device__ __forceinline__ void load(const void* p) {
-    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+    const IWQ_GLOBAL u32x4* q = gp<u32x4>(p);
 #pragma unroll
     for (int k = 0; k < WORDS / 4; ++k) {
       u32x4 v = __builtin_nontemporal_load(q + k);
@@ -249,7 +395,7 @@ struct Vec8 {
     for (int k = 0; k < WORDS; ++k) u[k] = 0;
   }
   __device__ __forceinline__ void store(void* p) const {
-    u32x4* q = reinterpret_cast<u32x4*>(p);
+    IWQ_GLOBAL u32x4* q = gp<u32x4>(p);
 #pragma unroll
     for (int k = 0; k < WORDS / 4; ++k) {
       u32x4 v = {u[4 * k + 0], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3]};
@@ -258,22 +404,109 @@ struct Vec8 {
   }
 };
 
-// pack 8 codes (0..255) of consecutive elements; CODES == 4: 4 B (low nibble = even element),
-// CODES == 8: 8 B.
+// min/max order keys of 8 elements (16-bit dtypes in packed int16 math)
+template <int DT, bool SYM>
+__device__ __forceinline__ void minmax8(const Vec8<DT>& v, int32_t& mn, int32_t& mx) {
+  if constexpr (Fmt<DT>::NB == 16) {
+    if constexpr (SYM) {
+      u16x2 m[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) m[i] = __builtin_bit_cast(u16x2, v.u[i] & 0x7FFF7FFFu);
+      u16x2 a = __builtin_elementwise_max(__builtin_elementwise_max(m[0], m[1]), __builtin_elementwise_max(m[2], m[3]));
+      mx = (int32_t)max(a.x, a.y);
+      mn = 0;
+    } else {
+      s16x2 k[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s16x2 x = __builtin_bit_cast(s16x2, v.u[i]);
+        k[i] = x ^ ((x >> (short)15) & (short)0x7FFF);
+      }
+      s16x2 a = __builtin_elementwise_min(__builtin_elementwise_min(k[0], k[1]), __builtin_elementwise_min(k[2], k[3]));
+      s16x2 b = __builtin_elementwise_max(__builtin_elementwise_max(k[0], k[1]), __builtin_elementwise_max(k[2], k[3]));
+      mn = min((int32_t)a.x, (int32_t)a.y);
+      mx = max((int32_t)b.x, (int32_t)b.y);
+    }
+  } else {
+    if constexpr (SYM) {
+      mn = 0;
+      mx = mag_key<DT>(v.get(0));
+#pragma unroll
+      for (int i = 1; i < 8; ++i) mx = max(mx, mag_key<DT>(v.get(i)));
+    } else {
+      mn = mx = key_of<DT>(v.get(0));
+#pragma unroll
+      for (int i = 1; i < 8; ++i) {
+        int32_t kk = key_of<DT>(v.get(i));
+        mn = min(mn, kk);
+        mx = max(mx, kk);
+      }
+    }
+  }
+}
+
+// store one storage-dtype value (scales / zeros)
+template <int DT>
+__device__ __forceinline__ void store_param(void* base, int64_t idx, float v) {
+  if constexpr (Fmt<DT>::NB == 16) gp<uint16_t>(base)[idx] = (uint16_t)Fmt<DT>::from_f(v);
+  else gp<uint32_t>(base)[idx] = Fmt<DT>::from_f(v);
+}
+
+template <int DT, bool SYM>
+__device__ __forceinline__ GroupParams params_from_keys(int32_t mn, int32_t mx, int n_bits, float rmax) {
+  using F = Fmt<DT>;
+  if constexpr (SYM) return params_sym<DT>(F::to_f(bits_of_key<DT>(mx)), n_bits, rmax);
+  else return params_asym<DT>(F::to_f(bits_of_key<DT>(mn)), F::to_f(bits_of_key<DT>(mx)), n_bits, rmax);
+}
+
+// Quantize 8 elements with one group's parameters.  codes[j] (j < 4) receives the integer codes of
+// elements 2j, 2j+1 in its two 16-bit halves.  Returns true if a dequantized value is NaN.
+template <int DT, bool SYM>
+__device__ __forceinline__ bool quant8(const Vec8<DT>& v, const GroupParams& p, int n_bits, Vec8<DT>& o,
+                                       uint32_t (&codes)[4]) {
+  if constexpr (DT == DT_F16) {
+    if (p.fast) {
+      const FastPk k = fast_pk<SYM>(p, n_bits);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t cp;
+        o.u[j] = quant2_fast<SYM>(v.u[j], p, k, cp);
+        codes[j] = codes2_fast(cp, k);
+      }
+      return false;
+    }
+  }
+  using F = Fmt<DT>;
+  bool any_nan = false;
+  const uint32_t off = SYM ? (1u << (n_bits - 1)) : 0u;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float cf;
+    const float y = quant_exact<DT, SYM>(F::to_f(v.get(i)), p, cf);
+    any_nan |= (y != y);
+    o.set(i, F::from_f(y));
+    const uint32_t c = (cf == cf) ? ((uint32_t)(int32_t)cf + off) & 0xFFFFu : 0u;
+    if (i & 1) codes[i >> 1] |= c << 16;
+    else codes[i >> 1] = c;
+  }
+  return any_nan;
+}
+
+// Store the codes of 8 consecutive elements (element index elem0, multiple of 8):
+// CODES == 4: 4 B (low nibble = even element), CODES == 8: 8 B.
 template <int CODES>
-__device__ __forceinline__ void store_codes8(uint8_t* base, int64_t elem0, const uint32_t (&c)[8]) {
+__device__ __forceinline__ void store_codes8(uint8_t* base, int64_t elem0, const uint32_t (&c)[4]) {
   if constexpr (CODES == 4) {
-    uint32_t v = 0;
+    uint32_t b[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v |= (c[i] & 0xFu) << (4 * i);
-    *reinterpret_cast<uint32_t*>(base + elem0 / 2) = v;
+    for (int j = 0; j < 4; ++j) b[j] = (c[j] | (c[j] >> 12)) & 0xFFu;  // lo | hi << 4
+    const uint32_t v = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    *gp<uint32_t>(base + elem0 / 2) = v;
   } else if constexpr (CODES == 8) {
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) lo |= (c[i] & 0xFFu) << (8 * i);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) hi |= (c[4 + i] & 0xFFu) << (8 * i);
-    *reinterpret_cast<uint2*>(base + elem0) = make_uint2(lo, hi);
+    const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x06040200u);
+    const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06040200u);
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    *gp<u32x2>(base + elem0) = (u32x2){lo, hi};
   }
 }
 

@@ -79,99 +79,88 @@ struct GroupArgs {
   uint32_t* nan_flag;
 };
 
+// Resolved target of one 512-element unit.
+struct UnitRef {
+  GroupTensor t;
+  int64_t e0;     // first element of this lane
+  bool valid;
+};
+
 template <int DT, int G, bool SYM, int CODES>
-__device__ __forceinline__ bool group_unit(const GroupTensor& t, int64_t unit_in_tensor, int lane, int n_bits) {
+__device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<DT>& v, int lane, int n_bits,
+                                                   float rmax) {
   using F = Fmt<DT>;
   constexpr int LPG = G / 8;  // lanes per group
-  const int64_t e0 = unit_in_tensor * UNIT + (int64_t)lane * 8;
-  const bool valid = e0 < t.numel;
-  Vec8<DT> v;
-  if (valid) v.load(static_cast<const char*>(t.w) + e0 * F::BYTES);
-  else v.zero();
-
-  // ---- per-lane 8-element reduction on order keys, then DPP all-reduce over the group's lanes
   int32_t mn, mx;
-  if constexpr (SYM) {
-    mx = mag_key<DT>(v.get(0));
-#pragma unroll
-    for (int i = 1; i < 8; ++i) mx = max(mx, mag_key<DT>(v.get(i)));
-    group_max<LPG>(mx);
-  } else {
-    mn = mx = key_of<DT>(v.get(0));
-#pragma unroll
-    for (int i = 1; i < 8; ++i) {
-      int32_t k = key_of<DT>(v.get(i));
-      mn = min(mn, k);
-      mx = max(mx, k);
-    }
-    group_minmax<LPG>(mn, mx);
-  }
-  GroupParams p;
-  if constexpr (SYM) p = params_sym<DT>(F::to_f(bits_of_key<DT>(mx)), n_bits);
-  else p = params_asym<DT>(F::to_f(bits_of_key<DT>(mn)), F::to_f(bits_of_key<DT>(mx)), n_bits);
-
-  // ---- quantize -> dequantize
+  minmax8<DT, SYM>(v, mn, mx);
+  if constexpr (SYM) group_max<LPG>(mx);
+  else group_minmax<LPG>(mn, mx);
+  const GroupParams p = params_from_keys<DT, SYM>(mn, mx, n_bits, rmax);
   Vec8<DT> o;
-  uint32_t c[8];
-  bool any_nan = false;
-  if (p.fast) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float cf;
-      float y = quant_fast_f16<SYM>(F::to_f(v.get(i)), p, cf);
-      o.set(i, F::from_f(y));
-      c[i] = (uint32_t)(int32_t)cf + (SYM ? (1u << (n_bits - 1)) : 0u);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float cf;
-      float y = quant_exact<DT, SYM>(F::to_f(v.get(i)), p, cf);
-      any_nan |= (y != y);
-      o.set(i, F::from_f(y));
-      c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (n_bits - 1)) : 0u) : 0u;
-    }
-  }
-  if (valid) {
-    if (t.out) o.store(static_cast<char*>(t.out) + e0 * F::BYTES);
-    if constexpr (CODES != 0) store_codes8<CODES>(static_cast<uint8_t*>(t.codes), e0, c);
+  uint32_t c[4];
+  const bool any_nan = quant8<DT, SYM>(v, p, n_bits, o, c);
+  if (r.valid) {
+    if (r.t.out) o.store(static_cast<char*>(r.t.out) + r.e0 * F::BYTES);
+    if constexpr (CODES != 0) store_codes8<CODES>(static_cast<uint8_t*>(r.t.codes), r.e0, c);
     if ((lane % LPG) == 0) {
-      const int64_t gidx = e0 / G;
-      if (t.scales) {
-        if constexpr (F::NB == 16) static_cast<uint16_t*>(t.scales)[gidx] = (uint16_t)F::from_f(p.s);
-        else static_cast<uint32_t*>(t.scales)[gidx] = F::from_f(p.s);
-      }
-      if (!SYM && t.zeros) {
-        if constexpr (F::NB == 16) static_cast<uint16_t*>(t.zeros)[gidx] = (uint16_t)F::from_f(p.z);
-        else static_cast<uint32_t*>(t.zeros)[gidx] = F::from_f(p.z);
-      }
+      const int64_t gidx = r.e0 / G;
+      if (r.t.scales) store_param<DT>(r.t.scales, gidx, p.s);
+      if (!SYM && r.t.zeros) store_param<DT>(r.t.zeros, gidx, p.z);
     }
   }
-  return valid && any_nan;
+  return r.valid && any_nan;
 }
 
+// Persistent launch; wave w owns the contiguous unit range [w*per, (w+1)*per) and walks it UNROLL
+// units at a time, issuing all UNROLL loads before any compute/store (the output may alias the
+// input, so the compiler cannot hoist later loads above earlier stores on its own).  Batched mode
+// keeps the current table entry in registers and re-reads the table only when the walk crosses
+// into the next tensor (a contiguous walk crosses at most a few boundaries per wave).
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
+  using F = Fmt<DT>;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+  const float rmax = rmax_for(a.n_bits, SYM);
+  int64_t per = (a.total_units + nwaves - 1) / nwaves;
+  per = (per + UNROLL - 1) / UNROLL * UNROLL;
+  const int64_t ubeg = wave * per;
+  const int64_t uend = min(ubeg + per, a.total_units);
   bool any_nan = false;
-  int32_t cur = 0;  // batched: monotone cursor into the entry table (wave-uniform)
-  for (int64_t u0 = wave * UNROLL; u0 < a.total_units; u0 += nwaves * UNROLL) {
+  GroupTensor cur_t = a.single;
+  int64_t cur_begin = 0, cur_next = INT64_MAX;
+  int32_t cur = 0;
+  if constexpr (BATCHED) cur_next = -1;  // force the first lookup
+  for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+    UnitRef r[UNROLL];
+    Vec8<DT> v[UNROLL];
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       const int64_t u = u0 + k;
-      if (u >= a.total_units) break;
       if constexpr (BATCHED) {
-        while (cur + 1 < a.n_entries && u >= a.entries[cur + 1].unit_begin) ++cur;
-        cur = __builtin_amdgcn_readfirstlane(cur);
-        const iwq_batch_entry& e = a.entries[cur];
-        GroupTensor t{e.w, e.out_deq, e.out_codes, e.out_scales, e.out_zeros, e.rows * e.cols};
-        any_nan |= group_unit<DT, G, SYM, CODES>(t, u - e.unit_begin, lane, a.n_bits);
-      } else {
-        any_nan |= group_unit<DT, G, SYM, CODES>(a.single, u, lane, a.n_bits);
+        if (u < uend && (u >= cur_next || cur_next < 0)) {
+          const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(a.entries);
+          while (cur + 1 < a.n_entries && u >= tab[cur + 1].unit_begin) ++cur;
+          cur = __builtin_amdgcn_readfirstlane(cur);
+          cur_t = GroupTensor{tab[cur].w, tab[cur].out_deq, tab[cur].out_codes, tab[cur].out_scales,
+                              tab[cur].out_zeros, tab[cur].rows * tab[cur].cols};
+          cur_begin = tab[cur].unit_begin;
+          cur_next = (cur + 1 < a.n_entries) ? tab[cur + 1].unit_begin : INT64_MAX;
+        }
       }
+      r[k].t = cur_t;
+      r[k].e0 = (u - cur_begin) * UNIT + (int64_t)lane * 8;
+      r[k].valid = (u < uend) && (r[k].e0 < r[k].t.numel);
     }
+    // unconditional loads (invalid lanes re-read the tensor's first 16 B and are never stored):
+    // no exec-masked branches around the loads, so the waits below are counted per unit
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k)
+      v[k].load(static_cast<const char*>(r[k].t.w) + (r[k].valid ? r[k].e0 : 0) * F::BYTES);
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k)
+      any_nan |= group_unit_compute<DT, G, SYM, CODES>(r[k], v[k], lane, a.n_bits, rmax);
   }
   flag_nan(a.nan_flag, any_nan);
 }
@@ -205,34 +194,26 @@ __global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
   const char* src = a.w + (row * a.ld_w + col0) * F::BYTES;
   Vec8<DT> v[CPL];
   const int64_t nchunks = a.L / 8;
+  const float rmax = rmax_for(a.n_bits, SYM);
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int64_t ch = (int64_t)k * WAVE + lane;
+    if (ch < nchunks) v[k].load(src + ch * 8 * F::BYTES);
+  }
   int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int64_t ch = (int64_t)k * WAVE + lane;
     if (ch < nchunks) {
-      v[k].load(src + ch * 8 * F::BYTES);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if constexpr (SYM) {
-          mx = max(mx, mag_key<DT>(v[k].get(i)));
-        } else {
-          int32_t kk = key_of<DT>(v[k].get(i));
-          mn = min(mn, kk);
-          mx = max(mx, kk);
-        }
-      }
-    } else {
-      v[k].zero();
+      int32_t a_mn, a_mx;
+      minmax8<DT, SYM>(v[k], a_mn, a_mx);
+      mn = min(mn, a_mn);
+      mx = max(mx, a_mx);
     }
   }
-  GroupParams p;
-  if constexpr (SYM) {
-    group_max<64>(mx);
-    p = params_sym<DT>(F::to_f(bits_of_key<DT>(mx)), a.n_bits);
-  } else {
-    group_minmax<64>(mn, mx);
-    p = params_asym<DT>(F::to_f(bits_of_key<DT>(mn)), F::to_f(bits_of_key<DT>(mx)), a.n_bits);
-  }
+  if constexpr (SYM) group_max<64>(mx);
+  else group_minmax<64>(mn, mx);
+  const GroupParams p = params_from_keys<DT, SYM>(mn, mx, a.n_bits, rmax);
   bool any_nan = false;
   char* dst = a.out ? a.out + (row * a.ld_out + col0) * F::BYTES : nullptr;
 #pragma unroll
@@ -240,29 +221,15 @@ __global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
     const int64_t ch = (int64_t)k * WAVE + lane;
     if (ch < nchunks) {
       Vec8<DT> o;
-      uint32_t c[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float cf, y;
-        if (p.fast) y = quant_fast_f16<SYM>(F::to_f(v[k].get(i)), p, cf);
-        else y = quant_exact<DT, SYM>(F::to_f(v[k].get(i)), p, cf);
-        any_nan |= (y != y);
-        o.set(i, F::from_f(y));
-        c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
-      }
+      uint32_t c[4];
+      any_nan |= quant8<DT, SYM>(v[k], p, a.n_bits, o, c);
       if (dst) o.store(dst + ch * 8 * F::BYTES);
       if constexpr (CODES != 0) store_codes8<CODES>(a.codes, row * a.cols + col0 + ch * 8, c);
     }
   }
   if (lane == 0) {
-    if (a.scales) {
-      if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[j] = (uint16_t)F::from_f(p.s);
-      else static_cast<uint32_t*>(a.scales)[j] = F::from_f(p.s);
-    }
-    if (!SYM && a.zeros) {
-      if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[j] = (uint16_t)F::from_f(p.z);
-      else static_cast<uint32_t*>(a.zeros)[j] = F::from_f(p.z);
-    }
+    if (a.scales) store_param<DT>(a.scales, j, p.s);
+    if (!SYM && a.zeros) store_param<DT>(a.zeros, j, p.z);
   }
   flag_nan(a.nan_flag, any_nan);
 }
@@ -295,6 +262,7 @@ __global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
   const int64_t jr = blockIdx.y;                               // group index along rows
   const int64_t r0 = jr * a.g;
   const bool cvalid = c0 < a.cols;
+  const float rmax = rmax_for(a.n_bits, SYM);
   int32_t mn[8], mx[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { mn[i] = 0x7FFFFFFF; mx[i] = (int32_t)0x80000000; }
@@ -322,8 +290,7 @@ __global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
   for (int i = 0; i < 8; ++i) {
     int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
     for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][tx * 8 + i]); a_mx = max(a_mx, s_mx[y][tx * 8 + i]); }
-    if constexpr (SYM) p[i] = params_sym<DT>(F::to_f(bits_of_key<DT>(a_mx)), a.n_bits);
-    else p[i] = params_asym<DT>(F::to_f(bits_of_key<DT>(a_mn)), F::to_f(bits_of_key<DT>(a_mx)), a.n_bits);
+    p[i] = params_from_keys<DT, SYM>(a_mn, a_mx, a.n_bits, rmax);
   }
   bool any_nan = false;
   if (cvalid) {
@@ -332,28 +299,23 @@ __global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int64_t gidx = (c0 + i) * ng + jr;
-        if (a.scales) {
-          if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[gidx] = (uint16_t)F::from_f(p[i].s);
-          else static_cast<uint32_t*>(a.scales)[gidx] = F::from_f(p[i].s);
-        }
-        if (!SYM && a.zeros) {
-          if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[gidx] = (uint16_t)F::from_f(p[i].z);
-          else static_cast<uint32_t*>(a.zeros)[gidx] = F::from_f(p[i].z);
-        }
+        if (a.scales) store_param<DT>(a.scales, gidx, p[i].s);
+        if (!SYM && a.zeros) store_param<DT>(a.zeros, gidx, p[i].z);
       }
     }
+    const uint32_t off = SYM ? (1u << (a.n_bits - 1)) : 0u;
     for (int64_t r = r0 + ty; r < r0 + a.g; r += TY) {
       Vec8<DT> v, o;
       v.load(a.w + (r * a.ld_w + c0) * F::BYTES);
-      uint32_t c[8];
+      uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float cf, y;
-        if (p[i].fast) y = quant_fast_f16<SYM>(F::to_f(v.get(i)), p[i], cf);
-        else y = quant_exact<DT, SYM>(F::to_f(v.get(i)), p[i], cf);
+        y = quant_exact_or_fast<DT, SYM>(F::to_f(v.get(i)), p[i], cf);
         any_nan |= (y != y);
         o.set(i, F::from_f(y));
-        c[i] = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
+        const uint32_t cc = (cf == cf) ? ((uint32_t)(int32_t)cf + off) & 0xFFFFu : 0u;
+        c[i >> 1] |= (i & 1) ? (cc << 16) : cc;
       }
       if (a.out) o.store(a.out + (r * a.ld_out + c0) * F::BYTES);
       if constexpr (CODES != 0) store_codes8<CODES>(a.codes, r * a.cols + c0, c);
@@ -424,8 +386,8 @@ __global__ __launch_bounds__(BLOCK) void k_seg_reduce(SegArgs a) {
       int64_t ow, oo, r, c;
       seg_locate(a, f, ow, oo, r, c);
       uint32_t b;
-      if constexpr (F::NB == 16) b = reinterpret_cast<const uint16_t*>(a.w)[ow];
-      else b = reinterpret_cast<const uint32_t*>(a.w)[ow];
+      if constexpr (F::NB == 16) b = gp<uint16_t>(a.w)[ow];
+      else b = gp<uint32_t>(a.w)[ow];
       if constexpr (SYM) {
         mx = max(mx, mag_key<DT>(b));
       } else {
@@ -467,37 +429,31 @@ __global__ __launch_bounds__(BLOCK) void k_seg_apply(SegArgs a) {
       const int64_t j = f / a.L;
       if (j != curj) {
         curj = j;
-        if constexpr (SYM) p = params_sym<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
-        else p = params_asym<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j])), F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
+        if constexpr (SYM) p = params_sym_exact<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
+        else p = params_asym_exact<DT>(F::to_f(bits_of_key<DT>(a.keys[2 * j])), F::to_f(bits_of_key<DT>(a.keys[2 * j + 1])), a.n_bits);
         if (f == j * a.L) {
-          if (a.scales) {
-            if constexpr (F::NB == 16) static_cast<uint16_t*>(a.scales)[j] = (uint16_t)F::from_f(p.s);
-            else static_cast<uint32_t*>(a.scales)[j] = F::from_f(p.s);
-          }
-          if (!SYM && a.zeros) {
-            if constexpr (F::NB == 16) static_cast<uint16_t*>(a.zeros)[j] = (uint16_t)F::from_f(p.z);
-            else static_cast<uint32_t*>(a.zeros)[j] = F::from_f(p.z);
-          }
+          if (a.scales) store_param<DT>(a.scales, j, p.s);
+          if (!SYM && a.zeros) store_param<DT>(a.zeros, j, p.z);
         }
       }
       int64_t ow, oo, r, c;
       seg_locate(a, f, ow, oo, r, c);
       uint32_t b;
-      if constexpr (F::NB == 16) b = reinterpret_cast<const uint16_t*>(a.w)[ow];
-      else b = reinterpret_cast<const uint32_t*>(a.w)[ow];
+      if constexpr (F::NB == 16) b = gp<uint16_t>(a.w)[ow];
+      else b = gp<uint32_t>(a.w)[ow];
       float cf;
       float y = quant_exact<DT, SYM>(F::to_f(b), p, cf);
       any_nan |= (y != y);
       const uint32_t yb = F::from_f(y);
       if (a.out) {
-        if constexpr (F::NB == 16) reinterpret_cast<uint16_t*>(a.out)[oo] = (uint16_t)yb;
-        else reinterpret_cast<uint32_t*>(a.out)[oo] = yb;
+        if constexpr (F::NB == 16) gp<uint16_t>(a.out)[oo] = (uint16_t)yb;
+        else gp<uint32_t>(a.out)[oo] = yb;
       }
       if (a.codes_bits) {
         const uint32_t code = (cf == cf) ? (uint32_t)(int32_t)cf + (SYM ? (1u << (a.n_bits - 1)) : 0u) : 0u;
         const int64_t e = r * a.cols + c;
         if (a.codes_bits == 8) {
-          a.codes[e] = (uint8_t)code;
+          gp<uint8_t>(a.codes)[e] = (uint8_t)code;
         } else {
           // nibbles: OR into the (pre-zeroed) 32-bit word; neighbours may belong to other threads
           const int64_t byte = e >> 1;
@@ -519,7 +475,7 @@ int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
 
 template <int DT, int G, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
-  constexpr int UNROLL = 2;
+  constexpr int UNROLL = 4;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * 8;

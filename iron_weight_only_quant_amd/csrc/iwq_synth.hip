@@ -28,24 +28,23 @@ __global__ __launch_bounds__(256) void k_synth(void* out, int64_t n, uint64_t se
   }
 }
 
-// Every finite fp16 numerator (63488 incl. +-0) against fp16 divisors d in [2^-24, 65504]:
-// reciprocal-corrected quotient (the hot loop's) vs IEEE fp32 division.
+// Every finite fp16 numerator (63488 incl. +-0) against fp16 divisors s in [2^-24, 65504]:
+// the hot loop's reciprocal (rcp_f16val) and corrected quotient (div_f16vals) vs IEEE fp32 division.
 __global__ __launch_bounds__(256) void k_selftest_div(unsigned long long* counts) {
   const uint32_t dbits = blockIdx.y + 1;  // 0x0001 .. 0x7BFF
   const float s = (float)__builtin_bit_cast(_Float16, (uint16_t)dbits);
-  const float rs = 1.0f / s;
+  const float rs_ref = opaque(1.0f / s);
+  const float rs = rcp_f16val(s);
   unsigned long long bad32 = 0, bad16 = 0;
   for (uint32_t wb = blockIdx.x * 256 + threadIdx.x; wb < 65536u; wb += gridDim.x * 256) {
     if ((wb & 0x7C00u) == 0x7C00u) continue;  // inf / NaN numerators never take the fast path
     const float w = (float)__builtin_bit_cast(_Float16, (uint16_t)wb);
-    const float q0 = w * rs;
-    const float e = __builtin_fmaf(-q0, s, w);
-    const float q1 = __builtin_fmaf(e, rs, q0);
-    const float ref = w / s;
-    const bool z1 = (q1 == 0.0f && ref == 0.0f);  // sign of a zero quotient is irrelevant (see quant_fast_f16)
+    const float q1 = div_f16vals(w, s, rs);
+    const float ref = opaque(w / s);
+    const bool z1 = (q1 == 0.0f && ref == 0.0f);  // sign of a zero quotient is irrelevant downstream
     bad32 += (!z1 && __builtin_bit_cast(uint32_t, q1) != __builtin_bit_cast(uint32_t, ref)) ? 1 : 0;
-    const uint16_t h1 = __builtin_bit_cast(uint16_t, (_Float16)q1), h2 = __builtin_bit_cast(uint16_t, (_Float16)ref);
-    bad16 += (!z1 && h1 != h2) ? 1 : 0;
+    const uint16_t h1 = __builtin_bit_cast(uint16_t, (_Float16)q1), h2v = __builtin_bit_cast(uint16_t, (_Float16)ref);
+    bad16 += (!z1 && h1 != h2v) ? 1 : 0;
   }
   for (int o = 32; o > 0; o >>= 1) {
     bad32 += __shfl_down(bad32, o);
@@ -55,6 +54,8 @@ __global__ __launch_bounds__(256) void k_selftest_div(unsigned long long* counts
     atomicAdd(&counts[0], bad32);
     atomicAdd(&counts[1], bad16);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && __builtin_bit_cast(uint32_t, rs) != __builtin_bit_cast(uint32_t, rs_ref))
+    atomicAdd(&counts[2], 1ull);
 }
 
 }  // namespace
@@ -77,7 +78,7 @@ int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t i
 int iwq_selftest_division(uint64_t* d_counts, void* stream) {
   if (!d_counts) return IWQ_ERR_ARG;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(d_counts, 0, 2 * sizeof(uint64_t), st) != hipSuccess) return IWQ_ERR_HIP;
+  if (hipMemsetAsync(d_counts, 0, 3 * sizeof(uint64_t), st) != hipSuccess) return IWQ_ERR_HIP;
   hipLaunchKernelGGL(k_selftest_div, dim3(64, 0x7BFF), dim3(256), 0, st,
                      reinterpret_cast<unsigned long long*>(d_counts));
   return hipGetLastError() == hipSuccess ? IWQ_OK : IWQ_ERR_HIP;

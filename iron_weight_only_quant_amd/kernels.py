@@ -170,9 +170,10 @@ def fill_synthetic(t: torch.Tensor, seed: int, index_offset: int = 0):
 
 
 def selftest_division(device="cuda"):
-    """(fp32 mismatches, fp16 mismatches) of the hot loop's corrected division vs IEEE division."""
+    """(quotient fp32 mismatches, quotient fp16 mismatches, reciprocal mismatches) of the hot loop's
+    fast division vs IEEE division, exhaustive over fp16 operands."""
     lib = L.load()
-    counts = torch.zeros(2, dtype=torch.int64, device=device)
+    counts = torch.zeros(3, dtype=torch.int64, device=device)
     with torch.cuda.device(counts.device):
         L.check(lib.iwq_selftest_division(L.ptr(counts), L.stream_handle(counts.device)), "iwq_selftest_division")
     return tuple(int(x) for x in counts.cpu())

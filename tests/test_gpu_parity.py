@@ -46,7 +46,8 @@ def test_native_library_is_loaded(K):
 
 
 def test_division_selftest(K):
-    bad32, bad16 = K.selftest_division(DEV)
+    bad32, bad16, badrcp = K.selftest_division(DEV)
+    assert badrcp == 0, badrcp
     assert bad16 == 0, bad16
     assert bad32 == 0, bad32
 

@@ -32,4 +32,12 @@ if [[ $WHAT == all || $WHAT == *prof* ]]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2
   cd "$ROOT"
 fi
+if [[ $WHAT == *pmc* ]]; then
+  cd /tmp
+  B="python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1"
+  step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
+  step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
+  step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- $B
+  cd "$ROOT"
+fi
 echo "=== session done"
