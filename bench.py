@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--variant", type=int, default=0, help="kernel tuning variant for the timed run")
+    ap.add_argument("--variants", default="", help="A/B: comma list of variants timed in interleaved rounds")
+    ap.add_argument("--rounds", type=int, default=5)
     return ap.parse_args()
 
 
@@ -111,6 +114,33 @@ def cpu_baseline(weights, bits, group, symmetric, budget_s):
                       f"{threads} threads), {spent:.1f} s"}
 
 
+def ab_variants(plan, variants, args):
+    """Interleaved in-process A/B of kernel variants (cdna_hip_programming.md §5.4 rule 24)."""
+    stream = torch.cuda.current_stream()
+    ref = [o.clone() for o in plan.outs[:3]]
+    times = {v: [] for v in variants}
+    for v in variants:  # warm + correctness vs variant of the first entry
+        plan.run(stream, variant=v)
+        torch.cuda.synchronize()
+        for o, r in zip(plan.outs[:3], ref):
+            assert torch.equal(o.view(torch.int16), r.view(torch.int16)), f"variant {v} differs"
+    for _ in range(args.rounds):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.steps):
+                plan.run(stream, variant=v)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.steps)
+    numel = plan.numel
+    for v in variants:
+        t = sorted(times[v])
+        med = t[len(t) // 2]
+        print(f"[ab] variant {v}: median {med:.4f} ms  min {t[0]:.4f} ms  -> {numel * 4 / med / 1e6:.1f} GB/s alg",
+              file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     ws_n, rank, _ = init_dist(args)
@@ -120,8 +150,10 @@ def main():
     numel = sum(w.numel() for w in weights)
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
     stream = torch.cuda.current_stream()
+    if args.variants:
+        ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
     for _ in range(args.warmup):
-        plan.run()
+        plan.run(variant=args.variant)
     torch.cuda.synchronize()
     assert plan.nan_flag.item() == 0
 
@@ -132,7 +164,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        plan.run(stream)
+        plan.run(stream, variant=args.variant)
     ev1.record(stream)
     torch.cuda.synchronize()
     barrier(ws_n)

@@ -66,6 +66,8 @@ enum iwq_status {
 /* flags */
 #define IWQ_FLAG_FORCE_GENERIC 0x1u  /* use the universal segmented path (testing / A-B)            */
 #define IWQ_FLAG_BATCH_CODES 0x100u  /* batched entry: every entry carries out_codes              */
+/* bits 16..23: kernel tuning variant of the batched fp16/g128/asym kernel (0 = default; A/B only) */
+#define IWQ_FLAG_VARIANT(v) (((unsigned)(v) & 0xFFu) << 16)
 
 /* Bytes of device workspace iwq_quantize_minmax needs for this problem (0 if none). */
 int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant_dim);

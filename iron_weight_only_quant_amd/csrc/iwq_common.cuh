@@ -134,6 +134,14 @@ __device__ __forceinline__ float div_f16vals(float w, float s, float rs) {
   float e = __builtin_fmaf(-q0, s, w);
   return opaque(__builtin_fmaf(e, rs, q0));
 }
+// Same, with IEEE's sign for a zero quotient (-0 / s = -0; the corrected form yields +0 there).
+// Needed where the sign of a zero is stored (the zero point of min_val = -0 groups); the
+// elementwise path does not need it (see quant2_fast).
+__device__ __forceinline__ float div_f16vals_signed(float w, float s, float rs) {
+  const float q0 = w * rs;
+  const float e = __builtin_fmaf(-q0, s, w);
+  return opaque(__builtin_copysignf(__builtin_fmaf(e, rs, q0), q0));
+}
 
 // ---------------------------------------------------------------------------------------------
 // per-group parameters
@@ -199,7 +207,7 @@ __device__ __forceinline__ GroupParams params_asym(float mn, float mx, int n_bit
       p.rs = rcp_f16val(p.s);
       p.hi = max_int;                          // exact in fp16 for n_bits <= 10
       p.lo = 0.0f;
-      float zq = (float)(_Float16)div_f16vals(mn, p.s, p.rs);
+      float zq = (float)(_Float16)div_f16vals_signed(mn, p.s, p.rs);
       p.z = clamp_nan(-__builtin_rintf(zq), 0.0f, p.hi);
       // rng finite (so mn, mx finite) and s > 0: every shortcut above is exact; z is finite
       // because the clamp maps +-inf into [0, max_int].
@@ -382,11 +390,14 @@ struct Vec8 {
       u[i] = b;
     }
   }
+  template <bool NT = true>
   __device__ __forceinline__ void load(const void* p) {
     const IWQ_GLOBAL u32x4* q = gp<u32x4>(p);
 #pragma unroll
     for (int k = 0; k < WORDS / 4; ++k) {
-      u32x4 v = __builtin_nontemporal_load(q + k);
+      u32x4 v;
+      if constexpr (NT) v = __builtin_nontemporal_load(q + k);
+      else v = q[k];
       u[4 * k + 0] = v.x; u[4 * k + 1] = v.y; u[4 * k + 2] = v.z; u[4 * k + 3] = v.w;
     }
   }
@@ -394,12 +405,14 @@ struct Vec8 {
 #pragma unroll
     for (int k = 0; k < WORDS; ++k) u[k] = 0;
   }
+  template <bool NT = true>
   __device__ __forceinline__ void store(void* p) const {
     IWQ_GLOBAL u32x4* q = gp<u32x4>(p);
 #pragma unroll
     for (int k = 0; k < WORDS / 4; ++k) {
       u32x4 v = {u[4 * k + 0], u[4 * k + 1], u[4 * k + 2], u[4 * k + 3]};
-      __builtin_nontemporal_store(v, q + k);
+      if constexpr (NT) __builtin_nontemporal_store(v, q + k);
+      else q[k] = v;
     }
   }
 };

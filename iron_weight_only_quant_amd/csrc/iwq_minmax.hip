@@ -86,7 +86,7 @@ struct UnitRef {
   bool valid;
 };
 
-template <int DT, int G, bool SYM, int CODES>
+template <int DT, int G, bool SYM, int CODES, bool NTS = true>
 __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<DT>& v, int lane, int n_bits,
                                                    float rmax) {
   using F = Fmt<DT>;
@@ -100,7 +100,7 @@ __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<
   uint32_t c[4];
   const bool any_nan = quant8<DT, SYM>(v, p, n_bits, o, c);
   if (r.valid) {
-    if (r.t.out) o.store(static_cast<char*>(r.t.out) + r.e0 * F::BYTES);
+    if (r.t.out) o.template store<NTS>(static_cast<char*>(r.t.out) + r.e0 * F::BYTES);
     if constexpr (CODES != 0) store_codes8<CODES>(static_cast<uint8_t*>(r.t.codes), r.e0, c);
     if ((lane % LPG) == 0) {
       const int64_t gidx = r.e0 / G;
@@ -112,29 +112,23 @@ __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<
 }
 
 // Persistent launch; wave w owns the contiguous unit range [w*per, (w+1)*per) and walks it UNROLL
-// units at a time, issuing all UNROLL loads before any compute/store (the output may alias the
-// input, so the compiler cannot hoist later loads above earlier stores on its own).  Batched mode
-// keeps the current table entry in registers and re-reads the table only when the walk crosses
-// into the next tensor (a contiguous walk crosses at most a few boundaries per wave).
-template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL>
-__global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
-  using F = Fmt<DT>;
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
-  const float rmax = rmax_for(a.n_bits, SYM);
-  int64_t per = (a.total_units + nwaves - 1) / nwaves;
-  per = (per + UNROLL - 1) / UNROLL * UNROLL;
-  const int64_t ubeg = wave * per;
-  const int64_t uend = min(ubeg + per, a.total_units);
-  bool any_nan = false;
-  GroupTensor cur_t = a.single;
+// units at a time.  All UNROLL loads of an iteration are issued before any compute/store (the
+// output may alias the input, so the compiler cannot hoist later loads above earlier stores on
+// its own); with PF the next iteration's loads are issued before this iteration's compute
+// (register double buffering; the prefetched units never overlap the ones being stored).
+// Batched mode keeps the current table entry in registers and re-reads the table only when the
+// walk crosses into the next tensor.
+template <int DT, int UNROLL, bool BATCHED>
+struct UnitWalker {
+  GroupTensor cur_t;
   int64_t cur_begin = 0, cur_next = INT64_MAX;
   int32_t cur = 0;
-  if constexpr (BATCHED) cur_next = -1;  // force the first lookup
-  for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
-    UnitRef r[UNROLL];
-    Vec8<DT> v[UNROLL];
+  __device__ __forceinline__ void init(const GroupArgs& a) {
+    cur_t = a.single;
+    if constexpr (BATCHED) cur_next = -1;
+  }
+  __device__ __forceinline__ void resolve(const GroupArgs& a, int64_t u0, int64_t uend, int lane,
+                                          UnitRef (&r)[UNROLL]) {
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       const int64_t u = u0 + k;
@@ -153,14 +147,62 @@ __global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
       r[k].e0 = (u - cur_begin) * UNIT + (int64_t)lane * 8;
       r[k].valid = (u < uend) && (r[k].e0 < r[k].t.numel);
     }
-    // unconditional loads (invalid lanes re-read the tensor's first 16 B and are never stored):
-    // no exec-masked branches around the loads, so the waits below are counted per unit
+  }
+};
+
+// unconditional loads (invalid lanes re-read the tensor's first 16 B and are never stored): no
+// exec-masked branches around the loads, so the waits are counted per unit
+template <int DT, int UNROLL, bool NTL>
+__device__ __forceinline__ void load_units(const UnitRef (&r)[UNROLL], Vec8<DT> (&v)[UNROLL]) {
 #pragma unroll
-    for (int k = 0; k < UNROLL; ++k)
-      v[k].load(static_cast<const char*>(r[k].t.w) + (r[k].valid ? r[k].e0 : 0) * F::BYTES);
+  for (int k = 0; k < UNROLL; ++k)
+    v[k].template load<NTL>(static_cast<const char*>(r[k].t.w) + (r[k].valid ? r[k].e0 : 0) * Fmt<DT>::BYTES);
+}
+
+template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
+          bool NTS = true>
+__global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+  const float rmax = rmax_for(a.n_bits, SYM);
+  int64_t per = (a.total_units + nwaves - 1) / nwaves;
+  per = (per + UNROLL - 1) / UNROLL * UNROLL;
+  const int64_t ubeg = wave * per;
+  const int64_t uend = min(ubeg + per, a.total_units);
+  bool any_nan = false;
+  UnitWalker<DT, UNROLL, BATCHED> walk;
+  walk.init(a);
+  if constexpr (PF) {
+    UnitRef rn[UNROLL];
+    Vec8<DT> vn[UNROLL];
+    if (ubeg < uend) {
+      walk.resolve(a, ubeg, uend, lane, rn);
+      load_units<DT, UNROLL, NTL>(rn, vn);
+    }
+    for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+      UnitRef r[UNROLL];
+      Vec8<DT> v[UNROLL];
 #pragma unroll
-    for (int k = 0; k < UNROLL; ++k)
-      any_nan |= group_unit_compute<DT, G, SYM, CODES>(r[k], v[k], lane, a.n_bits, rmax);
+      for (int k = 0; k < UNROLL; ++k) { r[k] = rn[k]; v[k] = vn[k]; }
+      if (u0 + UNROLL < uend) {
+        walk.resolve(a, u0 + UNROLL, uend, lane, rn);
+        load_units<DT, UNROLL, NTL>(rn, vn);
+      }
+#pragma unroll
+      for (int k = 0; k < UNROLL; ++k)
+        any_nan |= group_unit_compute<DT, G, SYM, CODES, NTS>(r[k], v[k], lane, a.n_bits, rmax);
+    }
+  } else {
+    for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+      UnitRef r[UNROLL];
+      Vec8<DT> v[UNROLL];
+      walk.resolve(a, u0, uend, lane, r);
+      load_units<DT, UNROLL, NTL>(r, v);
+#pragma unroll
+      for (int k = 0; k < UNROLL; ++k)
+        any_nan |= group_unit_compute<DT, G, SYM, CODES, NTS>(r[k], v[k], lane, a.n_bits, rmax);
+    }
   }
   flag_nan(a.nan_flag, any_nan);
 }
@@ -485,6 +527,33 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
+// selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
+template <int UNROLL, bool PF, bool NTL, bool NTS>
+hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
+  const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
+  int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  const int64_t cap = (int64_t)device_cu_count() * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS>), dim3((unsigned)blocks),
+                     dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
+  switch (v) {
+    case 1: return launch_variant_t<4, true, true, true>(a, st);
+    case 2: return launch_variant_t<4, true, false, true>(a, st);
+    case 3: return launch_variant_t<4, true, true, false>(a, st);
+    case 4: return launch_variant_t<4, true, false, false>(a, st);
+    case 5: return launch_variant_t<8, false, true, true>(a, st);
+    case 6: return launch_variant_t<2, true, true, true>(a, st);
+    case 7: return launch_variant_t<4, false, false, false>(a, st);
+    case 8: return launch_variant_t<8, true, true, true>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int DT, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_g(int64_t g, const GroupArgs& a, hipStream_t st) {
   switch (g) {
@@ -755,6 +824,11 @@ int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entr
   // the codes width is a template parameter and the entries are device-resident, so the caller
   // states with IWQ_FLAG_BATCH_CODES that every entry carries out_codes.
   const int codes = (flags & IWQ_FLAG_BATCH_CODES) ? (n_bits <= 4 ? 4 : 8) : 0;
+  const int variant = (int)((flags >> 16) & 0xFFu);
+  if (variant != 0 && dtype == IWQ_F16 && group == 128 && !symmetric && codes == 0) {
+    IWQ_HIP(launch_variant(variant, a, static_cast<hipStream_t>(stream)));
+    return IWQ_OK;
+  }
   IWQ_HIP(launch_group<true>(dtype, group, symmetric != 0, codes, a, static_cast<hipStream_t>(stream)));
   return IWQ_OK;
 }

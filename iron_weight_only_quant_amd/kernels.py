@@ -146,9 +146,9 @@ class BatchPlan:
         self.nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
         self.numel = sum(w.numel() for w in weights)
 
-    def run(self, stream=None):
+    def run(self, stream=None, variant=0):
         lib = L.load()
-        flags = L.IWQ_FLAG_BATCH_CODES if self.want_codes else 0
+        flags = (L.IWQ_FLAG_BATCH_CODES if self.want_codes else 0) | ((int(variant) & 0xFF) << 16)
         sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
         with torch.cuda.device(self.device):
             st = lib.iwq_quantize_minmax_batched(L.ptr(self.d_table), self.n, self.total_units,

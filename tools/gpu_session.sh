@@ -32,6 +32,9 @@ if [[ $WHAT == all || $WHAT == *prof* ]]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2
   cd "$ROOT"
 fi
+if [[ $WHAT == *ab* ]]; then
+  step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
+fi
 if [[ $WHAT == *pmc* ]]; then
   cd /tmp
   B="python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1"
