@@ -117,6 +117,8 @@ def cpu_baseline(weights, bits, group, symmetric, budget_s):
 def ab_variants(plan, variants, args):
     """Interleaved in-process A/B of kernel variants (cdna_hip_programming.md §5.4 rule 24)."""
     stream = torch.cuda.current_stream()
+    plan.run(stream, variant=0)
+    torch.cuda.synchronize()
     ref = [o.clone() for o in plan.outs[:3]]
     times = {v: [] for v in variants}
     for v in variants:  # warm + correctness vs variant of the first entry

@@ -52,6 +52,20 @@ int device_cu_count() {
   return cached[dev];
 }
 
+// Resident 256-thread blocks per CU for a kernel (occupancy API: VGPRs/LDS; SGPRs are capped at
+// 80 on the persistent kernels so the API answer is exact).  Cached per instantiation & device.
+template <typename Kern>
+int resident_blocks_per_cu(Kern kernel, int* cache) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, BLOCK, 0) != hipSuccess || n <= 0) n = 1;
+    cache[dev] = n > 8 ? 8 : n;
+  }
+  return cache[dev];
+}
+
 __device__ __forceinline__ void flag_nan(uint32_t* nan_flag, bool any_nan) {
   // one atomic per wave at most
   uint64_t m = __ballot(any_nan);
@@ -111,57 +125,78 @@ __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<
   return r.valid && any_nan;
 }
 
-// Persistent launch; wave w owns the contiguous unit range [w*per, (w+1)*per) and walks it UNROLL
-// units at a time.  All UNROLL loads of an iteration are issued before any compute/store (the
-// output may alias the input, so the compiler cannot hoist later loads above earlier stores on
-// its own); with PF the next iteration's loads are issued before this iteration's compute
-// (register double buffering; the prefetched units never overlap the ones being stored).
-// Batched mode keeps the current table entry in registers and re-reads the table only when the
-// walk crosses into the next tensor.
-template <int DT, int UNROLL, bool BATCHED>
-struct UnitWalker {
-  GroupTensor cur_t;
-  int64_t cur_begin = 0, cur_next = INT64_MAX;
+// Persistent launch; wave w owns the contiguous unit range [w*per, (w+1)*per) and walks it in
+// iterations of up to UNROLL units that never straddle two tensors, so one iteration has ONE
+// (wave-uniform, SGPR-resident) tensor descriptor and the lane offsets of its units differ by
+// immediates.  All loads of an iteration are issued before any compute/store (the output may
+// alias the input, so the compiler cannot hoist later loads above earlier stores on its own);
+// with PF the next iteration's loads are issued before this iteration's compute (register double
+// buffering; prefetched units never overlap the ones being stored).
+template <bool BATCHED>
+struct TensorCursor {
   int32_t cur = 0;
+  int64_t begin = 0, next = INT64_MAX;  // unit range [begin, next) of the current tensor
+  GroupTensor t;
   __device__ __forceinline__ void init(const GroupArgs& a) {
-    cur_t = a.single;
-    if constexpr (BATCHED) cur_next = -1;
-  }
-  __device__ __forceinline__ void resolve(const GroupArgs& a, int64_t u0, int64_t uend, int lane,
-                                          UnitRef (&r)[UNROLL]) {
-#pragma unroll
-    for (int k = 0; k < UNROLL; ++k) {
-      const int64_t u = u0 + k;
-      if constexpr (BATCHED) {
-        if (u < uend && (u >= cur_next || cur_next < 0)) {
-          const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(a.entries);
-          while (cur + 1 < a.n_entries && u >= tab[cur + 1].unit_begin) ++cur;
-          cur = __builtin_amdgcn_readfirstlane(cur);
-          cur_t = GroupTensor{tab[cur].w, tab[cur].out_deq, tab[cur].out_codes, tab[cur].out_scales,
-                              tab[cur].out_zeros, tab[cur].rows * tab[cur].cols};
-          cur_begin = tab[cur].unit_begin;
-          cur_next = (cur + 1 < a.n_entries) ? tab[cur + 1].unit_begin : INT64_MAX;
-        }
-      }
-      r[k].t = cur_t;
-      r[k].e0 = (u - cur_begin) * UNIT + (int64_t)lane * 8;
-      r[k].valid = (u < uend) && (r[k].e0 < r[k].t.numel);
+    t = a.single;
+    if constexpr (BATCHED) {
+      next = -1;
     }
+  }
+  // make u (< total) fall inside the current tensor; all values wave-uniform
+  __device__ __forceinline__ void seek(const GroupArgs& a, int64_t u) {
+    if constexpr (BATCHED) {
+      if (u >= next || next < 0) {
+        const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(a.entries);
+        while (cur + 1 < a.n_entries && u >= tab[cur + 1].unit_begin) ++cur;
+        cur = __builtin_amdgcn_readfirstlane(cur);
+        t.w = rfl_ptr(tab[cur].w);
+        t.out = rfl_ptr(tab[cur].out_deq);
+        t.codes = rfl_ptr(tab[cur].out_codes);
+        t.scales = rfl_ptr(tab[cur].out_scales);
+        t.zeros = rfl_ptr(tab[cur].out_zeros);
+        t.numel = rfl_i64(tab[cur].rows * tab[cur].cols);
+        begin = rfl_i64(tab[cur].unit_begin);
+        next = (cur + 1 < a.n_entries) ? rfl_i64(tab[cur + 1].unit_begin) : INT64_MAX;
+      }
+    }
+  }
+  __device__ __forceinline__ static int64_t rfl_i64(int64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }
+  template <typename P>
+  __device__ __forceinline__ static P rfl_ptr(P p) {
+    return (P)(uintptr_t)rfl_i64((int64_t)(uintptr_t)p);
   }
 };
 
-// unconditional loads (invalid lanes re-read the tensor's first 16 B and are never stored): no
-// exec-masked branches around the loads, so the waits are counted per unit
+struct Iter {
+  GroupTensor t;
+  int64_t e0;      // this lane's first element in unit 0 of the iteration
+  int32_t n;       // units in this iteration (1..UNROLL), wave-uniform
+};
+
 template <int DT, int UNROLL, bool NTL>
-__device__ __forceinline__ void load_units(const UnitRef (&r)[UNROLL], Vec8<DT> (&v)[UNROLL]) {
+__device__ __forceinline__ void load_iter(const Iter& it, Vec8<DT> (&v)[UNROLL]) {
+  // unconditional loads (units past it.n and lanes past numel re-read the tensor's first 16 B and
+  // are never stored): no exec-masked branches around the loads
+  const char* base = static_cast<const char*>(it.t.w);
 #pragma unroll
-  for (int k = 0; k < UNROLL; ++k)
-    v[k].template load<NTL>(static_cast<const char*>(r[k].t.w) + (r[k].valid ? r[k].e0 : 0) * Fmt<DT>::BYTES);
+  for (int k = 0; k < UNROLL; ++k) {
+    const int64_t e = it.e0 + (int64_t)k * UNIT;
+    const bool ok = (k < it.n) && (e < it.t.numel);
+    v[k].template load<NTL>(base + (ok ? e : 0) * Fmt<DT>::BYTES);
+  }
 }
 
+// SGPRs capped at 80: above that the hardware admits 7 (not 8) 256-thread blocks per CU while the
+// occupancy API still answers 8 (MI355X_MICROARCH.md "Residency"), and this persistent grid is
+// sized for full residency.
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
           bool NTS = true>
-__global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
@@ -171,37 +206,56 @@ __global__ __launch_bounds__(BLOCK) void k_group(GroupArgs a) {
   const int64_t ubeg = wave * per;
   const int64_t uend = min(ubeg + per, a.total_units);
   bool any_nan = false;
-  UnitWalker<DT, UNROLL, BATCHED> walk;
-  walk.init(a);
-  if constexpr (PF) {
-    UnitRef rn[UNROLL];
-    Vec8<DT> vn[UNROLL];
-    if (ubeg < uend) {
-      walk.resolve(a, ubeg, uend, lane, rn);
-      load_units<DT, UNROLL, NTL>(rn, vn);
+  TensorCursor<BATCHED> cursor;
+  cursor.init(a);
+  auto plan_iter = [&](int64_t u0, Iter& it) {
+    cursor.seek(a, u0);
+    const int64_t lim = min(uend, cursor.next);
+    it.t = cursor.t;
+    it.n = (int32_t)min((int64_t)UNROLL, lim - u0);
+    it.e0 = (u0 - cursor.begin) * UNIT + (int64_t)lane * 8;
+  };
+  auto compute_iter = [&](const Iter& it, const Vec8<DT> (&v)[UNROLL]) {
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      if (k < it.n) {
+        UnitRef r;
+        r.t = it.t;
+        r.e0 = it.e0 + (int64_t)k * UNIT;
+        r.valid = r.e0 < it.t.numel;
+        any_nan |= group_unit_compute<DT, G, SYM, CODES, NTS>(r, v[k], lane, a.n_bits, rmax);
+      }
     }
-    for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
-      UnitRef r[UNROLL];
+  };
+  if (ubeg >= uend) {
+    flag_nan(a.nan_flag, false);
+    return;
+  }
+  if constexpr (PF) {
+    Iter itn;
+    Vec8<DT> vn[UNROLL];
+    plan_iter(ubeg, itn);
+    load_iter<DT, UNROLL, NTL>(itn, vn);
+    for (int64_t u0 = ubeg; u0 < uend;) {
+      const Iter it = itn;
       Vec8<DT> v[UNROLL];
 #pragma unroll
-      for (int k = 0; k < UNROLL; ++k) { r[k] = rn[k]; v[k] = vn[k]; }
-      if (u0 + UNROLL < uend) {
-        walk.resolve(a, u0 + UNROLL, uend, lane, rn);
-        load_units<DT, UNROLL, NTL>(rn, vn);
+      for (int k = 0; k < UNROLL; ++k) v[k] = vn[k];
+      u0 += it.n;
+      if (u0 < uend) {
+        plan_iter(u0, itn);
+        load_iter<DT, UNROLL, NTL>(itn, vn);
       }
-#pragma unroll
-      for (int k = 0; k < UNROLL; ++k)
-        any_nan |= group_unit_compute<DT, G, SYM, CODES, NTS>(r[k], v[k], lane, a.n_bits, rmax);
+      compute_iter(it, v);
     }
   } else {
-    for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
-      UnitRef r[UNROLL];
+    for (int64_t u0 = ubeg; u0 < uend;) {
+      Iter it;
       Vec8<DT> v[UNROLL];
-      walk.resolve(a, u0, uend, lane, r);
-      load_units<DT, UNROLL, NTL>(r, v);
-#pragma unroll
-      for (int k = 0; k < UNROLL; ++k)
-        any_nan |= group_unit_compute<DT, G, SYM, CODES, NTS>(r[k], v[k], lane, a.n_bits, rmax);
+      plan_iter(u0, it);
+      load_iter<DT, UNROLL, NTL>(it, v);
+      compute_iter(it, v);
+      u0 += it.n;
     }
   }
   flag_nan(a.nan_flag, any_nan);
@@ -518,40 +572,15 @@ int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
 template <int DT, int G, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   constexpr int UNROLL = 4;
+  static int cache[64] = {0};
+  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-  const int64_t cap = (int64_t)device_cu_count() * 8;
+  const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((k_group<DT, G, SYM, CODES, BATCHED, UNROLL>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   return hipGetLastError();
-}
-
-// Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
-// selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
-template <int UNROLL, bool PF, bool NTL, bool NTS>
-hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
-  const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
-  int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-  const int64_t cap = (int64_t)device_cu_count() * 8;
-  if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS>), dim3((unsigned)blocks),
-                     dim3(BLOCK), 0, st, a);
-  return hipGetLastError();
-}
-hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
-  switch (v) {
-    case 1: return launch_variant_t<4, true, true, true>(a, st);
-    case 2: return launch_variant_t<4, true, false, true>(a, st);
-    case 3: return launch_variant_t<4, true, true, false>(a, st);
-    case 4: return launch_variant_t<4, true, false, false>(a, st);
-    case 5: return launch_variant_t<8, false, true, true>(a, st);
-    case 6: return launch_variant_t<2, true, true, true>(a, st);
-    case 7: return launch_variant_t<4, false, false, false>(a, st);
-    case 8: return launch_variant_t<8, true, true, true>(a, st);
-  }
-  return hipErrorInvalidValue;
 }
 
 template <int DT, bool SYM, int CODES, bool BATCHED>
