@@ -583,6 +583,34 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
+// selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
+template <int UNROLL, bool PF, bool NTL, bool NTS>
+hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
+  static int cache[64] = {0};
+  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS>;
+  const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
+  int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
+  switch (v) {
+    case 1: return launch_variant_t<4, true, true, true>(a, st);
+    case 2: return launch_variant_t<4, true, false, true>(a, st);
+    case 3: return launch_variant_t<4, true, true, false>(a, st);
+    case 4: return launch_variant_t<4, true, false, false>(a, st);
+    case 5: return launch_variant_t<8, false, true, true>(a, st);
+    case 6: return launch_variant_t<2, true, true, true>(a, st);
+    case 7: return launch_variant_t<4, false, false, false>(a, st);
+    case 8: return launch_variant_t<8, true, true, true>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int DT, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_g(int64_t g, const GroupArgs& a, hipStream_t st) {
   switch (g) {
