@@ -597,6 +597,43 @@ hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   return hipGetLastError();
 }
+// Roofline probes (variants >= 100): the same bytes moved without arithmetic, to measure the
+// achievable HBM rate of a given access style on the box at hand.  Timing reference only.
+//   MODE 0: copy, nt load + nt store     MODE 1: copy, plain       MODE 2: copy, 4 x 16 B in flight/lane (nt)
+//   MODE 3: read only (xor-reduce)       MODE 4: write only (nt)
+template <int MODE>
+__global__ __launch_bounds__(BLOCK) void k_probe(const iwq_batch_entry* entries, int32_t n, uint32_t* sink) {
+  uint32_t acc = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(entries);
+    const int64_t nvec = tab[i].rows * tab[i].cols / 8;
+    const IWQ_GLOBAL u32x4* src = gp<u32x4>(tab[i].w);
+    IWQ_GLOBAL u32x4* dst = gp<u32x4>(tab[i].out_deq);
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    const int64_t t0 = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if constexpr (MODE == 2) {
+      int64_t j = t0;
+      for (; j + 3 * stride < nvec; j += 4 * stride) {
+        u32x4 a0 = __builtin_nontemporal_load(src + j), a1 = __builtin_nontemporal_load(src + j + stride);
+        u32x4 a2 = __builtin_nontemporal_load(src + j + 2 * stride), a3 = __builtin_nontemporal_load(src + j + 3 * stride);
+        __builtin_nontemporal_store(a0, dst + j);
+        __builtin_nontemporal_store(a1, dst + j + stride);
+        __builtin_nontemporal_store(a2, dst + j + 2 * stride);
+        __builtin_nontemporal_store(a3, dst + j + 3 * stride);
+      }
+      for (; j < nvec; j += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + j), dst + j);
+    } else {
+      for (int64_t j = t0; j < nvec; j += stride) {
+        if constexpr (MODE == 0) __builtin_nontemporal_store(__builtin_nontemporal_load(src + j), dst + j);
+        if constexpr (MODE == 1) dst[j] = src[j];
+        if constexpr (MODE == 3) { u32x4 x = __builtin_nontemporal_load(src + j); acc ^= x.x ^ x.y ^ x.z ^ x.w; }
+        if constexpr (MODE == 4) __builtin_nontemporal_store((u32x4){(uint32_t)j, 0u, 0u, 0u}, dst + j);
+      }
+    }
+  }
+  if (MODE == 3 && acc == 0x12345678u) sink[0] = acc;
+}
+
 hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
   switch (v) {
     case 1: return launch_variant_t<4, true, true, true>(a, st);
@@ -607,6 +644,12 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 6: return launch_variant_t<2, true, true, true>(a, st);
     case 7: return launch_variant_t<4, false, false, false>(a, st);
     case 8: return launch_variant_t<8, true, true, true>(a, st);
+    case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 103: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 104: hipLaunchKernelGGL(k_probe<4>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 105: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 32)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
   }
   return hipErrorInvalidValue;
 }

@@ -32,6 +32,9 @@ if [[ $WHAT == all || $WHAT == *prof* ]]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 10 --warmup 2
   cd "$ROOT"
 fi
+if [[ $WHAT == *inplace* ]]; then
+  step bench_inplace 600 python bench.py --no-cpu-baseline --inplace
+fi
 if [[ $WHAT == *ab* ]]; then
   step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
 fi
@@ -40,6 +43,7 @@ if [[ $WHAT == *pmc* ]]; then
   B="python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1"
   step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
   step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
+  step traffic 60 python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" --numel 6476005376 -o "$OUT/traffic.json"
   step pmc_sq 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o run -- $B
   cd "$ROOT"
 fi
