@@ -31,10 +31,6 @@ sys.path.insert(0, ROOT)
 METRIC = "weights quantized GB/s + PPL delta, Llama-2-7B 4-bit g=128 at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
-LLAMA2_7B_LAYER = [("q_proj", 4096, 4096), ("k_proj", 4096, 4096), ("v_proj", 4096, 4096),
-                   ("o_proj", 4096, 4096), ("gate_proj", 11008, 4096), ("up_proj", 11008, 4096),
-                   ("down_proj", 4096, 11008)]
-N_LAYERS = 32
 
 
 def parse():
@@ -45,7 +41,11 @@ def parse():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--symmetric", action="store_true")
-    ap.add_argument("--layers", type=int, default=N_LAYERS)
+    ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-70b", "opt-125m"],
+                    help="llama2-7b: every rank quantizes a full 7B set (weak scaling, configs[1]); "
+                         "llama2-70b: the 560 weights are bin-packed over the ranks (strong scaling, configs[3])")
+    ap.add_argument("--gather", action="store_true",
+                    help="also time the all_gather of packed codes+scales to rank 0 (RCCL), reported separately")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -85,15 +85,25 @@ def max_over_ranks(x, ws):
     return float(t.item())
 
 
-def make_weights(rank, layers):
-    from iron_weight_only_quant_amd import kernels
-    ws = []
-    for li in range(layers):
-        for pi, (_, r, c) in enumerate(LLAMA2_7B_LAYER):
-            t = torch.empty((r, c), dtype=torch.float16, device="cuda")
-            kernels.fill_synthetic(t, seed=1_000_000 * rank + 16 * li + pi)
-            ws.append(t)
-    return ws
+def make_weights(model, rank, world):
+    """This rank's synthetic weights: the full model per rank (7B, weak scaling) or its bin-packed
+    shard (70B, strong scaling).  Seeds depend on the weight's global index (and rank for 7B)."""
+    from iron_weight_only_quant_amd import kernels, shard
+    shapes = shard.model_linear_shapes(model)
+    if model == "llama2-70b":
+        owned = shard.plan_shards(shapes, world)[rank]
+        seed_base = 0
+    else:
+        owned = list(range(len(shapes)))
+        seed_base = 1_000_000 * rank
+    ws, names = [], []
+    for i in owned:
+        name, (r, c) = shapes[i]
+        t = torch.empty((r, c), dtype=torch.float16, device="cuda")
+        kernels.fill_synthetic(t, seed=seed_base + i)
+        ws.append(t)
+        names.append(name)
+    return ws, names, shapes
 
 
 def cpu_baseline(weights, bits, group, symmetric, budget_s):
@@ -114,6 +124,24 @@ def cpu_baseline(weights, bits, group, symmetric, budget_s):
             "sample": f"{n} of the 224 Llama-2-7B weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
                       f"oracle/torch_ref.py (reference quant_funcs.py:16-38 op sequence, torch CPU, "
                       f"{threads} threads), {spent:.1f} s"}
+
+
+def time_gather(plan, names, all_shapes, args, ws_n):
+    """All_gather of the packed results (codes + scales/zeros) to rank 0 over RCCL, timed alone."""
+    from iron_weight_only_quant_amd import shard
+    import torch.distributed as dist
+    res = shard.ShardResult(names, plan.codes, plan.scales, plan.zeros)
+    bins = shard.plan_shards(all_shapes, ws_n)
+    names_per_rank = [[all_shapes[i][0] for i in b] for b in bins]
+    shp = dict(all_shapes)
+    shard.gather_to_rank0(res, shp, names_per_rank, args.bits, args.group, args.symmetric)  # warm
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    shard.gather_to_rank0(res, shp, names_per_rank, args.bits, args.group, args.symmetric)
+    torch.cuda.synchronize()
+    dist.barrier()
+    return round((time.perf_counter() - t0) * 1e3, 3)
 
 
 def ab_variants(plan, variants, args):
@@ -152,10 +180,13 @@ def main():
     ws_n, rank, _ = init_dist(args)
     from iron_weight_only_quant_amd import kernels
 
-    weights = make_weights(rank, args.layers)
+    strong = args.model == "llama2-70b"
+    if strong:
+        args.inplace = True  # 70B fp16 = 137 GB: in place (QuantLinear semantics) so N=1 fits in 288 GB
+    weights, names, all_shapes = make_weights(args.model, rank, ws_n)
     numel = sum(w.numel() for w in weights)
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric,
-                             outs=weights if args.inplace else None)
+                             outs=weights if args.inplace else None, want_codes=args.gather)
     stream = torch.cuda.current_stream()
     if args.variants:
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
@@ -180,10 +211,22 @@ def main():
     wall_max = max_over_ranks(wall, ws_n)
     ms_per_step = wall_max / args.steps * 1e3
 
+    gather_ms = None
+    if args.gather and ws_n > 1:
+        gather_ms = time_gather(plan, names, all_shapes, args, ws_n)
+
+    total_numel = numel
+    if ws_n > 1:
+        import torch.distributed as dist
+        t = torch.tensor([numel], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        total_numel = int(t.item())
     in_bytes = numel * 2
     groups = numel // args.group
     alg_bytes = numel * 2 + numel * 2 + groups * 2 * (1 if args.symmetric else 2)  # read w, write deq, s(,z)
-    value = ws_n * in_bytes / (ms_per_step / 1e3) / 1e9
+    if args.gather:
+        alg_bytes += numel // 2 if args.bits <= 4 else numel  # packed codes written too
+    value = total_numel * 2 / (ms_per_step / 1e3) / 1e9
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
 
     traffic = None
@@ -203,13 +246,14 @@ def main():
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ws_n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": f"Llama-2-7B all {len(weights)} Linear weights per GPU "
-                                   f"({numel} fp16 weights), INT{args.bits} g={args.group} "
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "config": {"workload": (f"Llama-2-70B 560 Linear weights bin-packed over {ws_n} GPU(s) "
+                                    if strong else f"Llama-2-7B all {len(weights)} Linear weights per GPU ")
+                                   + f"({total_numel} fp16 weights total), INT{args.bits} g={args.group} "
                                    f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
                                    f"{'in-place' if args.inplace else 'out-of-place'} dequant + scales/zeros, "
                                    f"one batched launch per step",
-                       "layers": args.layers, "bits": args.bits, "group": args.group,
+                       "model": args.model, "bits": args.bits, "group": args.group,
                        "parallelism": f"layer-shard x{ws_n} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -217,6 +261,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "ppl_delta": None,
+            "gather_ms": gather_ms,
         }
         print(json.dumps(rec), flush=True)
     if ws_n > 1:

@@ -1,0 +1,135 @@
+"""Layer sharding of a model's Linear weights across the GPUs of one node.
+
+The reference quantizes layer after layer on whichever GPU accelerate placed them
+(utils.py:43 device_map="balanced", quant_wrapper.py:52-82) — one GPU busy at a time.  Here
+every Linear weight is an independent unit of work, so the set is bin-packed by bytes over the
+ranks (one process per GPU) and each rank quantizes its shard with ONE batched launch; there is no
+exchange in the data path.  Optionally the packed results (int codes + fp16 scales/zeros, ~1/4 of
+the fp16 bytes) are gathered to rank 0 with a single torch.distributed collective (RCCL over xGMI
+on MI355X, gloo in the CPU tests).
+"""
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+# Linear shapes [out_features, in_features] per decoder layer (HF naming)
+LLAMA_LAYERS = {
+    "llama2-7b": (32, [("self_attn.q_proj", 4096, 4096), ("self_attn.k_proj", 4096, 4096),
+                       ("self_attn.v_proj", 4096, 4096), ("self_attn.o_proj", 4096, 4096),
+                       ("mlp.gate_proj", 11008, 4096), ("mlp.up_proj", 11008, 4096),
+                       ("mlp.down_proj", 4096, 11008)]),
+    "llama2-70b": (80, [("self_attn.q_proj", 8192, 8192), ("self_attn.k_proj", 1024, 8192),
+                        ("self_attn.v_proj", 1024, 8192), ("self_attn.o_proj", 8192, 8192),
+                        ("mlp.gate_proj", 28672, 8192), ("mlp.up_proj", 28672, 8192),
+                        ("mlp.down_proj", 8192, 28672)]),
+    "opt-125m": (12, [("self_attn.q_proj", 768, 768), ("self_attn.k_proj", 768, 768),
+                      ("self_attn.v_proj", 768, 768), ("self_attn.out_proj", 768, 768),
+                      ("fc1", 3072, 768), ("fc2", 768, 3072)]),
+}
+
+
+def model_linear_shapes(model: str) -> List[Tuple[str, Tuple[int, int]]]:
+    """All quantized Linear weights of a model (lm_head excluded, quant_wrapper.py:53)."""
+    n_layers, per = LLAMA_LAYERS[model]
+    prefix = "model.decoder.layers" if model.startswith("opt") else "model.layers"
+    return [(f"{prefix}.{i}.{n}", (r, c)) for i in range(n_layers) for n, r, c in per]
+
+
+def plan_shards(shapes: Sequence[Tuple[str, Tuple[int, int]]], world: int) -> List[List[int]]:
+    """Greedy longest-processing-time bin packing by element count; deterministic (ties by index).
+
+    Returns, per rank, the indices into `shapes` it owns (in ascending index order)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    order = sorted(range(len(shapes)), key=lambda i: (-shapes[i][1][0] * shapes[i][1][1], i))
+    loads = [0] * world
+    bins: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda k: (loads[k], k))
+        bins[r].append(i)
+        loads[r] += shapes[i][1][0] * shapes[i][1][1]
+    return [sorted(b) for b in bins]
+
+
+def shard_imbalance(shapes, bins) -> float:
+    loads = [sum(shapes[i][1][0] * shapes[i][1][1] for i in b) for b in bins]
+    return max(loads) / (sum(loads) / len(loads))
+
+
+@dataclass
+class ShardResult:
+    names: List[str]
+    codes: List[torch.Tensor]     # packed codes per owned tensor (uint8)
+    scales: List[torch.Tensor]
+    zeros: List[Optional[torch.Tensor]]
+
+
+def quantize_shard(named: Dict[str, torch.Tensor], n_bits: int, group: int, symmetric: bool,
+                   quantize_fn: Optional[Callable] = None) -> ShardResult:
+    """Quantize this rank's weights IN PLACE (dequantized values overwrite them, QuantLinear
+    semantics) and keep packed codes + scales/zeros.  `quantize_fn(list_of_weights) -> (codes,
+    scales, zeros)` may be injected by tests; the default is one batched gfx950 launch."""
+    names = sorted(named)
+    ws = [named[n] for n in names]
+    if quantize_fn is None:
+        from . import kernels
+        plan = kernels.BatchPlan(ws, n_bits, group, symmetric, outs=ws, want_codes=True)
+        plan.run()
+        codes, scales, zeros = plan.codes, plan.scales, plan.zeros
+    else:
+        codes, scales, zeros = quantize_fn(ws)
+    return ShardResult(names, list(codes), list(scales), list(zeros))
+
+
+def _flatten(res: ShardResult) -> torch.Tensor:
+    parts = []
+    for c, s, z in zip(res.codes, res.scales, res.zeros):
+        parts.append(c.reshape(-1).view(torch.uint8))
+        parts.append(s.reshape(-1).view(torch.uint8))
+        if z is not None:
+            parts.append(z.reshape(-1).view(torch.uint8))
+    if not parts:
+        return torch.zeros(0, dtype=torch.uint8)
+    return torch.cat([p.to(parts[0].device) for p in parts])
+
+
+def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bins_names: List[List[str]],
+                    n_bits: int, group: int, symmetric: bool, dtype=torch.float16, pg=None):
+    """Gather every rank's packed results to rank 0 with one padded all_gather (RCCL/gloo).
+
+    Returns {name: (codes, scales, zeros)} on rank 0, None elsewhere."""
+    import torch.distributed as dist
+    rank = dist.get_rank(pg)
+    world = dist.get_world_size(pg)
+    flat = _flatten(res)
+    dev = flat.device
+    n = torch.tensor([flat.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=pg)
+    mx = int(max(int(s.item()) for s in sizes))
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    buf[: flat.numel()] = flat
+    outs = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(outs, buf, group=pg)
+    if rank != 0:
+        return None
+    esz = torch.tensor([], dtype=dtype).element_size()
+    result = {}
+    for r in range(world):
+        off = 0
+        data = outs[r]
+        for name in sorted(all_bins_names[r]):
+            rows, cols = shapes[name]
+            ncode = rows * (cols // 2) if n_bits <= 4 else rows * cols
+            G = rows * cols // group
+            codes = data[off: off + ncode].clone()
+            off += ncode
+            scales = data[off: off + G * esz].clone().view(dtype)
+            off += G * esz
+            zeros = None
+            if not symmetric:
+                zeros = data[off: off + G * esz].clone().view(dtype)
+                off += G * esz
+            result[name] = (codes, scales, zeros)
+    return result
