@@ -57,7 +57,9 @@ enum iwq_status {
   IWQ_ERR_WORKSPACE = 6,  /* workspace missing or smaller than iwq_workspace_bytes()                 */
   IWQ_ERR_CODES = 7,      /* codes requested with n_bits > 8, or odd cols for nibble packing         */
   IWQ_ERR_HIP = 8,        /* a HIP runtime call failed (see iwq_last_hip_error)                      */
-  IWQ_ERR_ARG = 9         /* null pointer where one is required, bad flags, ...                      */
+  IWQ_ERR_ARG = 9,        /* null pointer where one is required, bad flags, ...                      */
+  IWQ_ERR_FORMAT = 10     /* FP format whose max value overflows fp16 (RuntimeError in the reference's
+                             torch.clamp, quant_linear.py:852)                                       */
 };
 
 #define IWQ_GROUP_PER_TENSOR (-1)
@@ -112,6 +114,28 @@ int iwq_batch_plan(iwq_batch_entry* h_entries, int32_t n_entries, int dtype, int
 int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units,
                                 int dtype, int n_bits, int64_t group, int symmetric, uint32_t* nan_flag,
                                 unsigned flags, void* stream);
+
+/*
+ * FP4/FP6/FP8 weight formats (QuantLinear FP branches, quant_linear.py:724-883), fp16 weights only.
+ * exp_bits/mant_bits as configure_fp_formats (quant_linear.py:84-110): E2M1 / E3M2 / E4M3 defaults.
+ * symmetric 1: absmax / fp_max scales, no zeros; 0: mid-point zeros and half-span scales.
+ * out_codes: the reference's code bytes (sign | exponent field | mantissa), nibble-packed
+ * (low nibble = even column) when 1 + exp_bits + mant_bits <= 4, else one byte per element.
+ */
+int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits, int mant_bits,
+                    int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out, void* out_codes,
+                    void* out_scales, void* out_zeros, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag,
+                    unsigned flags, void* stream);
+
+/*
+ * fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 (fp4_quantize_cpu.py:47-72): the E2M1 "grid" fake
+ * quantizer (per-group absmax scale S = absmax/6, AxCore two-step rounding), fp16 [rows, cols]
+ * contiguous -> fp16 out (same element order; the reference returns it viewed [-1, group]).
+ * out_scales: [G] fp16 S values, nullable.  group > 0 requires cols % group == 0 (ValueError).
+ */
+int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                 void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                 void* stream);
 
 /* Deterministic synthetic weights (oracle/synth.py bit-for-bit), written to [rows, cols] contiguous. */
 int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t index_offset, void* stream);

@@ -18,7 +18,7 @@ DTYPE_CODE = {torch.float16: IWQ_F16, torch.bfloat16: IWQ_BF16, torch.float32: I
 
 IWQ_OK = 0
 IWQ_ERR_SHAPE, IWQ_ERR_GROUP, IWQ_ERR_GROUP_MODE, IWQ_ERR_BITS, IWQ_ERR_DTYPE = 1, 2, 3, 4, 5
-IWQ_ERR_WORKSPACE, IWQ_ERR_CODES, IWQ_ERR_HIP, IWQ_ERR_ARG = 6, 7, 8, 9
+IWQ_ERR_WORKSPACE, IWQ_ERR_CODES, IWQ_ERR_HIP, IWQ_ERR_ARG, IWQ_ERR_FORMAT = 6, 7, 8, 9, 10
 
 IWQ_FLAG_FORCE_GENERIC = 0x1
 IWQ_FLAG_BATCH_CODES = 0x100
@@ -26,7 +26,7 @@ IWQ_FLAG_BATCH_CODES = 0x100
 EXPORTS = (
     "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",
     "iwq_fill_synthetic", "iwq_status_string", "iwq_last_hip_error", "iwq_build_info",
-    "iwq_selftest_division",
+    "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid",
 )
 
 
@@ -77,6 +77,11 @@ def load():
         lib.iwq_last_hip_error.restype = i32
         lib.iwq_build_info.argtypes = []
         lib.iwq_build_info.restype = ctypes.c_char_p
+        lib.iwq_quantize_fp.argtypes = [vp, i64, i64, i64, i32, i32, i32, i64, i32, i32, vp, i64, vp, vp, vp, vp,
+                                        i64, vp, u32, vp]
+        lib.iwq_quantize_fp.restype = i32
+        lib.iwq_fp4_grid.argtypes = [vp, i64, i64, i64, i32, vp, vp, vp, i64, vp, u32, vp]
+        lib.iwq_fp4_grid.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]
         lib.iwq_selftest_division.restype = i32
         _lib = lib

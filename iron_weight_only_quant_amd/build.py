@@ -6,8 +6,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
-SOURCES = ["iwq_minmax.hip", "iwq_synth.hip"]
-DEPS = SOURCES + ["iwq_common.cuh"]
+SOURCES = ["iwq_minmax.hip", "iwq_fp.hip", "iwq_synth.hip"]
+DEPS = SOURCES + ["iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Numerics: no FMA contraction, IEEE fp32 division, denormals preserved.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
@@ -28,11 +28,26 @@ def _stale():
 
 
 def build_library(force=False, verbose=True):
+    """Compile each translation unit in parallel (-fgpu-rdc not needed: no cross-TU device calls),
+    then link the shared library."""
     if not force and not _stale():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(OUT_DIR, exist_ok=True)
+    objs = [os.path.join(OUT_DIR, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+
+    def cc(src_obj):
+        src, obj = src_obj
+        cmd = [HIPCC] + compile_flags + ["-c", "-o", obj, os.path.join(CSRC, src)]
+        if verbose:
+            print("[iwq build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True, cwd=CSRC)
+
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
+        list(ex.map(cc, zip(SOURCES, objs)))
     tmp = LIB + ".tmp"
-    cmd = [HIPCC] + FLAGS + ["-o", tmp] + [os.path.join(CSRC, s) for s in SOURCES]
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print("[iwq build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)

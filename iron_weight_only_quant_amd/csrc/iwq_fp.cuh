@@ -1,0 +1,147 @@
+// iwq_fp.cuh — FP weight formats of the reference, bit-exact on gfx950 (fp16 storage).
+//
+//   encode  quant_linear._float_to_fp   quant_linear.py:126-163
+//   decode  quant_linear._fp_to_float   quant_linear.py:213-235
+//   FP4/FP6/FP8 branches of QuantLinear.quantize_weight   quant_linear.py:724-883
+//   E2M1 "grid" quantizer  fp4_quantize_cpu.py:37-72
+//
+// The reference codec is neither IEEE nor OCP (E4M3 max is 480; a mantissa that rounds past the
+// top of its binade is clamped, not carried; the exponent comes from an fp16 torch.log2, which
+// rounds up for the top few mantissas of 40 binades).  CDNA4's v_cvt_*fp8/fp4 therefore cannot be
+// used for the encode: it is integer/ALU code here, with the log2 behaviour as per-binade
+// thresholds (iwq_fp_tables.h) and every arithmetic step exact in fp32.
+#pragma once
+#include "iwq_common.cuh"
+#include "iwq_fp_tables.h"
+
+namespace iwq {
+
+struct FpSpec {
+  int E, M, bias;    // exponent / mantissa bits, bias = 2^(E-1) - 1
+  int emin, emax;    // min normal unbiased exponent (1 - bias), max ((2^E - 1) - bias)
+  float fp_max;      // (1 + (2^M - 1)/2^M) * 2^emax  (python float in the reference)
+  float fp_max16;    // RN16(fp_max): torch.clamp converts its bounds to half
+  float rmax;        // RN32(1/fp_max): corrected division when fp_max is an fp16 value
+  int fpmax_is_f16;  // fp_max exactly representable in fp16
+};
+
+// floor(RN16(log2 x)) for a positive fp16 magnitude (bit pattern, 1..0x7BFF)
+__device__ __forceinline__ int fp16_floor_log2_torch(uint32_t mag, const uint16_t* thresh) {
+  const int ef = (int)(mag >> 10);
+  const int e_true = ef > 0 ? ef - 15 : (31 - __builtin_clz(mag)) - 24;
+  return e_true + (mag >= (uint32_t)thresh[e_true + 24] ? 1 : 0);
+}
+
+// _float_to_fp on an fp16 value (bit pattern).  NaN inputs (only reachable when the group's scale
+// is NaN, where every output is NaN anyway) encode as 0.
+__device__ __forceinline__ uint32_t fp_encode(uint32_t b, const FpSpec& f) {
+  const uint32_t mag = b & 0x7FFFu;
+  if (mag == 0 || mag > 0x7C00u) return 0;                // zero_mask (:132,:161); NaN
+  const uint32_t sign = b >> 15;                          // x < 0 (:130)
+  const int e = fp16_floor_log2_torch(mag < 0x7C00u ? mag : 0x7BFFu, kLog2UpThresh);
+  const float xa = (float)__builtin_bit_cast(_Float16, (uint16_t)mag);
+  const float ms = (float)(1u << f.M);
+  uint32_t exp_field, mant;
+  if (e >= f.emin) {                                      // normal path (:145-149)
+    const int ec = e < f.emax ? e : f.emax;
+    float m = __builtin_rintf((__builtin_ldexpf(xa, -ec) - 1.0f) * ms);   // exact in fp32
+    m = m < 0.0f ? 0.0f : (m > ms - 1.0f ? ms - 1.0f : m);               // no carry
+    exp_field = (uint32_t)(ec + f.bias);
+    mant = (uint32_t)m;
+  } else {                                                // subnormal path (:152-154), fp16 ops exact
+    float m = __builtin_rintf(__builtin_ldexpf(xa, -f.emin) * ms);
+    m = m > ms - 1.0f ? ms - 1.0f : m;
+    exp_field = 0;
+    mant = (uint32_t)m;
+  }
+  return ((sign << (f.E + f.M)) | (exp_field << f.M) | mant) & 0xFFu;
+}
+
+// _fp_to_float: exact value in fp32 (code 0 -> +0; sign-only code -> -0)
+__device__ __forceinline__ float fp_decode(uint32_t code, const FpSpec& f) {
+  if (code == 0) return 0.0f;
+  const uint32_t sign = (code >> (f.E + f.M)) & 1u;
+  const int raw_exp = (int)((code >> f.M) & ((1u << f.E) - 1u));
+  const int mant = (int)(code & ((1u << f.M) - 1u));
+  const float v = raw_exp == 0 ? __builtin_ldexpf((float)mant, f.emin - f.M)
+                               : __builtin_ldexpf((float)((1 << f.M) + mant), raw_exp - f.bias - f.M);
+  return sign ? -v : v;
+}
+
+struct FpParams {
+  float s;    // scales (fp16 value)
+  float rs;   // RN32(1/s)
+  float z;    // zeros = mid point (asymmetric) / 0
+  bool fast;  // finite group: corrected divisions are exact
+};
+
+__device__ __forceinline__ float f16r(float x) { return (float)(_Float16)opaque(x); }
+
+// quotient of fp16 values x / y rounded to fp16: corrected division when allowed, else IEEE
+__device__ __forceinline__ float div16(float x, float y, float ry, bool fast) {
+  return fast ? (float)(_Float16)div_f16vals(x, y, ry) : f16r(x / y);
+}
+
+// sym (:744-747 etc.): max_val = absmax.clamp(1e-5); scales = (max_val / fp_max).clamp(1e-5)
+__device__ __forceinline__ FpParams fp_params_sym(float am, const FpSpec& f) {
+  FpParams p;
+  const float eps = (float)(_Float16)1e-5f;
+  const bool fin = am <= 65504.0f;  // false for NaN / inf
+  float m = am < eps ? eps : am;
+  float s = div16(m, f.fp_max, f.rmax, fin && f.fpmax_is_f16);
+  s = s < eps ? eps : s;
+  p.s = s;
+  p.z = 0.0f;
+  p.rs = rcp_f16val(s);
+  p.fast = fin;
+  return p;
+}
+
+// asym (:749-755): mid = (max + min) * 0.5; span = ((max - min) * 0.5).clamp(1e-5);
+// scales = (span / fp_max).clamp(1e-5); zeros = mid
+__device__ __forceinline__ FpParams fp_params_asym(float mn, float mx, const FpSpec& f) {
+  FpParams p;
+  const float eps = (float)(_Float16)1e-5f;
+  const float mid = f16r(f16r(mx + mn) * 0.5f);
+  float span = f16r(f16r(mx - mn) * 0.5f);
+  const bool fin = span <= 65504.0f && mid == mid && mid <= 65504.0f && mid >= -65504.0f;
+  span = span < eps ? eps : span;
+  float s = div16(span, f.fp_max, f.rmax, fin && f.fpmax_is_f16);
+  s = s < eps ? eps : s;
+  p.s = s;
+  p.z = mid;
+  p.rs = rcp_f16val(s);
+  p.fast = fin;
+  return p;
+}
+
+// one element of the FP branches: returns the dequantized value (fp32 holding an fp16 value)
+template <bool SYM>
+__device__ __forceinline__ float fp_quant_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+  float t;
+  if constexpr (SYM) t = div16(w, p.s, p.rs, p.fast);                    // W / scales
+  else t = div16(f16r(w - p.z), p.s, p.rs, p.fast);                      // (W - zeros) / scales
+  t = clamp_nan(t, -f.fp_max16, f.fp_max16);                             // clamp(-fp_max, fp_max)
+  const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
+  code = fp_encode(tb, f);
+  float y = f16r(f16r(fp_decode(code, f)) * p.s);                        // .to(fp16) * scales
+  if constexpr (!SYM) y = f16r(y + p.z);                                  // + zeros
+  if (t != t) y = t;                                                      // NaN scale: NaN out
+  return y;
+}
+
+// fp4_quantize_cpu._fp_scale element (:37-44) with S = RN16(max(absmax, fp16(1e-8)) / 6)
+__device__ __forceinline__ float grid_elem(float x, float S, float rS, bool fast) {
+  float u = (fast && S > 0.0f) ? (float)(_Float16)div_f16vals(x, S, rS) : f16r(x / S);
+  u = clamp_nan(u, -6.0f, 6.0f);
+  if (u != u) return u;
+  const uint32_t mag = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)u) & 0x7FFFu;
+  // ls = clamp(floor(log2|u| + 1), 1): |u| == 0 -> -inf -> 1
+  int ls = mag == 0 ? 1 : fp16_floor_log2_torch(mag, kLog2P1UpThresh) + 1;
+  ls = ls < 1 ? 1 : ls;
+  const float sc = __builtin_ldexpf(1.0f, ls - 2);                        // 2^(ls - M - bias)
+  const float q = __builtin_rintf(u / sc) * sc;                           // exact (power-of-two scale)
+  return f16r(f16r(q) * S);
+}
+
+}  // namespace iwq

@@ -1,0 +1,384 @@
+// iwq_fp.hip — gfx950 kernels + C-ABI for the reference's FP weight formats (fp16 storage).
+//
+// Replaces (reference, /root/reference):
+//   QuantLinear.quantize_weight FP4/FP6/FP8 branches   quant_linear.py:724-883 (+ _float_to_fp :126,
+//                                                       _fp_to_float :213, configure_fp_formats :84)
+//   fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2         fp4_quantize_cpu.py:37-72
+//
+// Kernels:
+//   k_fp_group  contiguous groups 8..512 (power of two), quant_dim 0: persistent, 8 elements per
+//               lane, group min/max (or absmax) by DPP, ALU encode/decode per element.
+//   k_fp_apply  universal apply after iwq::seg's atomic key reduction (per-tensor, per-channel,
+//               quant_dim 1, odd shapes).
+#include "iwq_common.cuh"
+#include "iwq_fp.cuh"
+#include "iwq_seg.cuh"
+#include "../../include/iwq.h"
+
+using namespace iwq;
+using iwq::seg::SegArgs;
+using iwq::seg::SEG_RUN;
+using iwq::seg::seg_locate;
+
+namespace {
+
+thread_local int g_last_hip_error_fp = 0;
+
+#define IWQ_HIP_FP(call)                \
+  do {                                  \
+    hipError_t e_ = (call);             \
+    if (e_ != hipSuccess) {             \
+      g_last_hip_error_fp = (int)e_;    \
+      return IWQ_ERR_HIP;               \
+    }                                   \
+  } while (0)
+
+constexpr int BLOCK = 256;
+constexpr int WPB = BLOCK / WAVE;
+constexpr int UNIT = WAVE * 8;
+
+enum : int { CODEC_FP = 0, CODEC_GRID = 1 };
+
+struct FpArgs {
+  const char* w;
+  char* out;
+  uint8_t* codes;
+  void* scales;
+  void* zeros;
+  int64_t numel;
+  int64_t total_units;
+  FpSpec f;
+  uint32_t* nan_flag;
+};
+
+__device__ __forceinline__ void fp_flag_nan(uint32_t* nan_flag, bool any_nan) {
+  uint64_t m = __ballot(any_nan);
+  if (m != 0 && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(m) && nan_flag) atomicOr(nan_flag, 1u);
+}
+
+template <int CODEC, bool SYM>
+__device__ __forceinline__ FpParams fp_group_params(int32_t mn, int32_t mx, const FpSpec& f) {
+  using F = Fmt<DT_F16>;
+  if constexpr (CODEC == CODEC_GRID) {
+    // fp4_quantize_cpu.py:61-66: S = absmax.clamp(min=1e-8) / 6  (fp16(1e-8) == 0)
+    const float am = F::to_f(bits_of_key<DT_F16>(mx));
+    FpParams p;
+    const bool fin = am <= 65504.0f;
+    const float amc = am < 1e-8f ? 0.0f : am;
+    p.s = fin ? (float)(_Float16)div_f16vals(amc, 6.0f, 1.0f / 6.0f) : f16r(amc / 6.0f);
+    p.rs = p.s > 0.0f ? rcp_f16val(p.s) : 0.0f;
+    p.z = 0.0f;
+    p.fast = fin;
+    return p;
+  } else if constexpr (SYM) {
+    return fp_params_sym(F::to_f(bits_of_key<DT_F16>(mx)), f);
+  } else {
+    return fp_params_asym(F::to_f(bits_of_key<DT_F16>(mn)), F::to_f(bits_of_key<DT_F16>(mx)), f);
+  }
+}
+
+template <int CODEC, bool SYM>
+__device__ __forceinline__ float fp_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+  if constexpr (CODEC == CODEC_GRID) {
+    code = 0;
+    return grid_elem(w, p.s, p.rs, p.fast);
+  } else {
+    return fp_quant_elem<SYM>(w, p, f, code);
+  }
+}
+
+// pack 8 one-byte codes of consecutive elements: CODES 4 -> nibbles (4 B), 8 -> bytes (8 B)
+template <int CODES>
+__device__ __forceinline__ void store_fp_codes8(uint8_t* base, int64_t elem0, const uint32_t (&c)[8]) {
+  if constexpr (CODES == 4) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= (c[i] & 0xFu) << (4 * i);
+    *gp<uint32_t>(base + elem0 / 2) = v;
+  } else if constexpr (CODES == 8) {
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { lo |= (c[i] & 0xFFu) << (8 * i); hi |= (c[4 + i] & 0xFFu) << (8 * i); }
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    *gp<u32x2>(base + elem0) = (u32x2){lo, hi};
+  }
+}
+
+template <int CODEC, int G, bool SYM, int CODES>
+__global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
+  using F = Fmt<DT_F16>;
+  constexpr int UNROLL = 4;
+  constexpr int LPG = G / 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * WPB;
+  int64_t per = (a.total_units + nwaves - 1) / nwaves;
+  per = (per + UNROLL - 1) / UNROLL * UNROLL;
+  const int64_t ubeg = wave * per;
+  const int64_t uend = min(ubeg + per, a.total_units);
+  bool any_nan = false;
+  for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+    Vec8<DT_F16> v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
+      const bool ok = (u0 + k < uend) && e < a.numel;
+      v[k].load(a.w + (ok ? e : 0) * F::BYTES);
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      if (u0 + k >= uend) break;
+      const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
+      const bool valid = e0 < a.numel;
+      int32_t mn, mx;
+      minmax8<DT_F16, SYM || CODEC == CODEC_GRID>(v[k], mn, mx);
+      if constexpr (SYM || CODEC == CODEC_GRID) group_max<LPG>(mx);
+      else group_minmax<LPG>(mn, mx);
+      const FpParams p = fp_group_params<CODEC, SYM>(mn, mx, a.f);
+      Vec8<DT_F16> o;
+      uint32_t c[8];
+      bool nan8 = false;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float y = fp_elem<CODEC, SYM>(F::to_f(v[k].get(i)), p, a.f, c[i]);
+        nan8 |= (y != y);
+        o.set(i, F::from_f(y));
+      }
+      if (valid) {
+        any_nan |= nan8;
+        if (a.out) o.store(a.out + e0 * F::BYTES);
+        if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
+        if ((lane % LPG) == 0) {
+          if (a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
+          if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, e0 / G, p.z);
+        }
+      }
+    }
+  }
+  fp_flag_nan(a.nan_flag, any_nan);
+}
+
+template <int CODEC, bool SYM>
+__global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
+  using F = Fmt<DT_F16>;
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  int64_t curj = -1;
+  FpParams p{};
+  bool any_nan = false;
+  for (int64_t f0 = tid * SEG_RUN; f0 < a.total; f0 += nthreads * SEG_RUN) {
+    const int64_t fend = min(f0 + SEG_RUN, a.total);
+    for (int64_t fi = f0; fi < fend; ++fi) {
+      const int64_t j = fi / a.L;
+      if (j != curj) {
+        curj = j;
+        p = fp_group_params<CODEC, SYM>(a.keys[2 * j], a.keys[2 * j + 1], f);
+        if (fi == j * a.L) {
+          if (a.scales) store_param<DT_F16>(a.scales, j, p.s);
+          if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, j, p.z);
+        }
+      }
+      int64_t ow, oo, r, c;
+      seg_locate(a, fi, ow, oo, r, c);
+      uint32_t code;
+      const float y = fp_elem<CODEC, SYM>(F::to_f(gp<uint16_t>(a.w)[ow]), p, f, code);
+      any_nan |= (y != y);
+      if (a.out) gp<uint16_t>(a.out)[oo] = (uint16_t)F::from_f(y);
+      if (a.codes_bits) {
+        const int64_t e = r * a.cols + c;
+        if (a.codes_bits == 8) {
+          gp<uint8_t>(a.codes)[e] = (uint8_t)code;
+        } else {
+          const int64_t byte = e >> 1;
+          const int shift = (int)((byte & 3) * 8 + (e & 1) * 4);
+          atomicOr(reinterpret_cast<uint32_t*>(a.codes + (byte & ~(int64_t)3)), (code & 0xFu) << shift);
+        }
+      }
+    }
+  }
+  fp_flag_nan(a.nan_flag, any_nan);
+}
+
+int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 256;
+  return n;
+}
+
+template <int CODEC, int G, bool SYM, int CODES>
+hipError_t launch_fp_group_t(const FpArgs& a, hipStream_t st) {
+  auto kern = k_fp_group<CODEC, G, SYM, CODES>;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, BLOCK, 0) != hipSuccess || occ <= 0) occ = 1;
+  if (occ > 8) occ = 8;
+  int64_t blocks = (a.total_units + 4 * WPB - 1) / (4 * WPB);
+  const int64_t cap = (int64_t)cu_count() * occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int CODEC, bool SYM, int CODES>
+hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
+  switch (g) {
+    case 8: return launch_fp_group_t<CODEC, 8, SYM, CODES>(a, st);
+    case 16: return launch_fp_group_t<CODEC, 16, SYM, CODES>(a, st);
+    case 32: return launch_fp_group_t<CODEC, 32, SYM, CODES>(a, st);
+    case 64: return launch_fp_group_t<CODEC, 64, SYM, CODES>(a, st);
+    case 128: return launch_fp_group_t<CODEC, 128, SYM, CODES>(a, st);
+    case 256: return launch_fp_group_t<CODEC, 256, SYM, CODES>(a, st);
+    case 512: return launch_fp_group_t<CODEC, 512, SYM, CODES>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpArgs& a, hipStream_t st) {
+  if (codec == CODEC_GRID) return launch_fp_group_g<CODEC_GRID, true, 0>(g, a, st);
+  if (sym) {
+    if (codes == 0) return launch_fp_group_g<CODEC_FP, true, 0>(g, a, st);
+    if (codes == 4) return launch_fp_group_g<CODEC_FP, true, 4>(g, a, st);
+    return launch_fp_group_g<CODEC_FP, true, 8>(g, a, st);
+  }
+  if (codes == 0) return launch_fp_group_g<CODEC_FP, false, 0>(g, a, st);
+  if (codes == 4) return launch_fp_group_g<CODEC_FP, false, 4>(g, a, st);
+  return launch_fp_group_g<CODEC_FP, false, 8>(g, a, st);
+}
+
+hipError_t launch_fp_seg(int codec, bool sym, const SegArgs& a, const FpSpec& f, hipStream_t st) {
+  const int64_t cap = (int64_t)cu_count() * 8;
+  int64_t ib = (a.G + BLOCK - 1) / BLOCK;
+  if (ib > cap) ib = cap;
+  hipLaunchKernelGGL(iwq::seg::k_seg_init, dim3((unsigned)ib), dim3(BLOCK), 0, st, a.keys, a.G);
+  int64_t blocks = (a.total + (int64_t)BLOCK * SEG_RUN - 1) / ((int64_t)BLOCK * SEG_RUN);
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  const bool red_sym = sym || codec == CODEC_GRID;
+  if (red_sym) hipLaunchKernelGGL((iwq::seg::k_seg_reduce<DT_F16, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  else hipLaunchKernelGGL((iwq::seg::k_seg_reduce<DT_F16, false>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  if (codec == CODEC_GRID) hipLaunchKernelGGL((k_fp_apply<CODEC_GRID, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
+  else if (sym) hipLaunchKernelGGL((k_fp_apply<CODEC_FP, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
+  else hipLaunchKernelGGL((k_fp_apply<CODEC_FP, false>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
+  return hipGetLastError();
+}
+
+bool aligned16p(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int fp_spec(int exp_bits, int mant_bits, FpSpec& f) {
+  if (exp_bits < 1 || mant_bits < 0 || exp_bits + mant_bits > 7) return IWQ_ERR_BITS;
+  f.E = exp_bits;
+  f.M = mant_bits;
+  f.bias = (1 << (exp_bits - 1)) - 1;
+  f.emin = 1 - f.bias;
+  f.emax = ((1 << exp_bits) - 1) - f.bias;
+  const double fm = (1.0 + (double)((1 << mant_bits) - 1) / (double)(1 << mant_bits)) * __builtin_ldexp(1.0, f.emax);
+  f.fp_max = (float)fm;
+  if (fm >= 65520.0) return IWQ_ERR_FORMAT;  // RN16(fp_max) overflows: torch.clamp raises (E5M2)
+  const float r16 = (float)(_Float16)f.fp_max;
+  f.fp_max16 = r16;
+  f.fpmax_is_f16 = r16 == f.fp_max ? 1 : 0;
+  f.rmax = 1.0f / f.fp_max;
+  return IWQ_OK;
+}
+
+int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+           int mant_bits, int64_t group, int symmetric, int quant_dim, void* out, int64_t ld_out, void* codes_out,
+           void* scales, void* zeros, void* ws, int64_t ws_bytes, uint32_t* nan_flag, unsigned flags,
+           void* stream) {
+  if (dtype != IWQ_F16) return IWQ_ERR_DTYPE;
+  if (!w) return IWQ_ERR_ARG;
+  if (rows <= 0 || cols <= 0 || ld_w < cols || (out && ld_out < cols)) return IWQ_ERR_SHAPE;
+  if (quant_dim != 0 && quant_dim != 1) return IWQ_ERR_ARG;
+  FpSpec f{};
+  int st = fp_spec(exp_bits, mant_bits, f);
+  if (st != IWQ_OK) return st;
+  const int64_t vr = quant_dim == 1 ? cols : rows;
+  const int64_t vc = quant_dim == 1 ? rows : cols;
+  int64_t L, G;
+  if (group > 0) {
+    if (vc % group != 0) return IWQ_ERR_GROUP;
+    L = group;
+    G = vr * vc / group;
+  } else if (group == IWQ_GROUP_PER_TENSOR) {
+    L = vr * vc;
+    G = 1;
+  } else if (group == IWQ_GROUP_PER_CHANNEL) {
+    L = vc;
+    G = vr;
+  } else {
+    return IWQ_ERR_GROUP_MODE;
+  }
+  int codes = 0;
+  if (codes_out) {
+    if (codec == CODEC_GRID) return IWQ_ERR_CODES;
+    codes = (exp_bits + mant_bits + 1) <= 4 ? 4 : 8;
+    if (codes == 4 && (cols & 1)) return IWQ_ERR_CODES;
+  }
+  const bool sym = codec == CODEC_GRID ? true : symmetric != 0;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool al = aligned16p(w) && (!out || aligned16p(out)) && (!codes_out || aligned16p(codes_out));
+  if (!(flags & IWQ_FLAG_FORCE_GENERIC) && quant_dim == 0 && group >= 8 && group <= 512 &&
+      (group & (group - 1)) == 0 && al && ld_w == cols && (!out || ld_out == cols)) {
+    FpArgs a{};
+    a.w = static_cast<const char*>(w);
+    a.out = static_cast<char*>(out);
+    a.codes = static_cast<uint8_t*>(codes_out);
+    a.scales = scales;
+    a.zeros = sym ? nullptr : zeros;
+    a.numel = rows * cols;
+    a.total_units = (a.numel + UNIT - 1) / UNIT;
+    a.f = f;
+    a.nan_flag = nan_flag;
+    IWQ_HIP_FP(launch_fp_group(codec, group, sym, codes, a, s));
+    return IWQ_OK;
+  }
+  const int64_t need = ((8 * G + 255) / 256) * 256;
+  if (!ws || ws_bytes < need || !aligned16p(ws)) return IWQ_ERR_WORKSPACE;
+  if (codes == 4) IWQ_HIP_FP(hipMemsetAsync(codes_out, 0, (size_t)(rows * (cols / 2)), s));
+  SegArgs a{};
+  a.w = static_cast<const char*>(w);
+  a.out = static_cast<char*>(out);
+  a.codes = static_cast<uint8_t*>(codes_out);
+  a.scales = scales;
+  a.zeros = sym ? nullptr : zeros;
+  a.keys = static_cast<int32_t*>(ws);
+  a.rows = rows;
+  a.cols = cols;
+  a.ld_w = ld_w;
+  a.ld_out = out ? ld_out : cols;
+  a.vc = vc;
+  a.L = L;
+  a.G = G;
+  a.total = rows * cols;
+  a.quant_dim = quant_dim;
+  a.n_bits = 8;
+  a.codes_bits = codes;
+  a.nan_flag = nan_flag;
+  IWQ_HIP_FP(launch_fp_seg(codec, sym, a, f, s));
+  return IWQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits, int mant_bits,
+                    int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out, void* out_codes,
+                    void* out_scales, void* out_zeros, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag,
+                    unsigned flags, void* stream) {
+  return run_fp(CODEC_FP, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, symmetric, quant_dim, out_deq,
+                ld_out, out_codes, out_scales, out_zeros, workspace, workspace_bytes, nan_flag, flags, stream);
+}
+
+int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                 void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                 void* stream) {
+  // grouping of fp4_quantize_cpu.py:55-60: reshape(-1, g) when g > 0, then (1, -1) when per_tensor,
+  // else rows of the 2-D input
+  const int64_t g = per_tensor ? IWQ_GROUP_PER_TENSOR : (group > 0 ? group : IWQ_GROUP_PER_CHANNEL);
+  return run_fp(CODEC_GRID, w, rows, cols, cols, IWQ_F16, 2, 1, g, 1, 0, out, cols, nullptr, out_scales, nullptr,
+                workspace, workspace_bytes, nan_flag, flags, stream);
+}
+
+}  // extern "C"

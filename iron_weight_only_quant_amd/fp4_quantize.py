@@ -1,0 +1,29 @@
+"""Drop-in for the reference's fp4_quantize_cpu.py (`quantize_fp16_to_fp4_e1m2`, :47-72) on the GPU.
+
+Same signature, grouping and errors; like the reference it returns the GROUPED view
+([-1, group_size], or [1, numel] per tensor) of the fake-quantized fp16 values, and
+`return_scales=True` (accepted but ignored by the reference) additionally returns the per-group
+scales S = absmax / 6."""
+import torch
+
+from . import kernels
+
+
+@torch.no_grad()
+def quantize_fp16_to_fp4_e1m2(tensor, group_size=128, per_tensor=False, return_scales=False):
+    if tensor.dtype != torch.float16:
+        tensor = tensor.to(torch.float16)
+    if tensor.dim() != 2:
+        raise ValueError("Expected a 2D tensor of shape [out_features, in_features].")
+    rows, cols = tensor.shape
+    if group_size > 0 and cols % group_size != 0:
+        raise ValueError("in_features must be divisible by group_size.")
+    res = kernels.fp4_grid(tensor, group_size, per_tensor)
+    out = res.out
+    if group_size > 0:
+        out = out.reshape(-1, group_size)
+    if per_tensor:
+        out = out.reshape(1, -1)
+    if return_scales:
+        return out, res.scales.view(-1, 1)
+    return out

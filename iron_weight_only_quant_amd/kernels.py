@@ -49,6 +49,8 @@ def _raise_for(status, what):
         raise AssertionError(f"{what}: last dimension not divisible by the group size")
     if status == L.IWQ_ERR_GROUP_MODE:
         raise ValueError("Invalid w_group_size")
+    if status == L.IWQ_ERR_FORMAT:
+        raise RuntimeError("value cannot be converted to type c10::Half without overflow")
     L.check(status, what)
 
 
@@ -94,6 +96,69 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
             L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev))
     _raise_for(st, "iwq_quantize_minmax")
     return QuantResult(out, scales, zeros, codes, nan_flag)
+
+
+def fp_code_nbytes(rows, cols, exp_bits, mant_bits):
+    return rows * (cols // 2) if (1 + exp_bits + mant_bits) <= 4 else rows * cols
+
+
+def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symmetric: bool, quant_dim: int = 0,
+                out: Optional[torch.Tensor] = None, want_codes: bool = False, flags: int = 0) -> QuantResult:
+    """FP4/FP6/FP8 fake quantization of an fp16 2-D weight (QuantLinear FP branches) on the GPU."""
+    L.require_device(w)
+    if w.dim() != 2:
+        raise AssertionError("weight must be 2-D")
+    if w.dtype != torch.float16:
+        raise TypeError("FP weight formats are implemented for fp16 weights")
+    lib = L.load()
+    if w.stride(1) != 1 or w.stride(0) < w.shape[1]:
+        w = w.contiguous()
+    rows, cols = w.shape
+    _, G = group_geometry(rows, cols, group, quant_dim)
+    dev = w.device
+    if out is None:
+        out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
+    scales = torch.empty(G, dtype=w.dtype, device=dev)
+    zeros = None if symmetric else torch.empty(G, dtype=w.dtype, device=dev)
+    codes = torch.empty(fp_code_nbytes(rows, cols, exp_bits, mant_bits), dtype=torch.uint8, device=dev) \
+        if want_codes else None
+    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    wsb = ((8 * G + 255) // 256) * 256
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        st = lib.iwq_quantize_fp(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
+                                 int(group), int(bool(symmetric)), int(quant_dim), L.ptr(out), out.stride(0),
+                                 L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag),
+                                 int(flags), L.stream_handle(dev))
+    _raise_for(st, "iwq_quantize_fp")
+    return QuantResult(out, scales, zeros, codes, nan_flag)
+
+
+def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int = 0) -> QuantResult:
+    """fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 arithmetic on the GPU; output in w's element order."""
+    L.require_device(w)
+    lib = L.load()
+    w = w.contiguous()
+    rows, cols = w.shape
+    if per_tensor:
+        G = 1
+    elif group > 0:
+        if cols % group != 0:
+            raise ValueError("in_features must be divisible by group_size.")
+        G = rows * cols // group
+    else:
+        G = rows
+    dev = w.device
+    out = torch.empty_like(w)
+    scales = torch.empty(G, dtype=w.dtype, device=dev)
+    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    wsb = ((8 * G + 255) // 256) * 256
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        st = lib.iwq_fp4_grid(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out), L.ptr(scales),
+                              L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev))
+    _raise_for(st, "iwq_fp4_grid")
+    return QuantResult(out, scales, None, None, nan_flag)
 
 
 class BatchPlan:

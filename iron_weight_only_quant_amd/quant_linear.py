@@ -13,8 +13,9 @@ Differences by design (documented in DESIGN.md):
   * quantization runs in the gfx950 kernels (no CPU path);
   * `keep_codes=True` additionally keeps the packed integer codes (`qweight`, include/iwq.h layout)
     for the fused dequant->GEMM forward.
-The FP4/FP6/FP8/BFP and "approximate" research formats (:470-883) are not part of this round's
-hot path and raise NotImplementedError.
+FP4/FP6/FP8 (quant_linear.py:724-883) run the gfx950 FP codec (fp16 weights), with the formats set
+by the same module-level `configure_fp_formats` (:84-110).  The BFP and "approximate"/double-
+approximate research decodes (:470-723) are out of scope and raise NotImplementedError.
 """
 import torch
 import torch.nn as nn
@@ -23,6 +24,35 @@ import torch.nn.functional as F
 from . import kernels
 
 _FORMATS = {"int", "fp4", "fp6", "fp8", "bfp"}
+
+# FP format configuration, module globals exactly like the reference (quant_linear.py:7-16, :84-110)
+FP4_EXP_BITS = 2
+FP4_MANTISSA_BITS = 1
+FP4_EXP_BIAS = 2 ** (FP4_EXP_BITS - 1) - 1
+FP6_EXP_BITS = 3
+FP6_MANTISSA_BITS = 2
+FP6_EXP_BIAS = 2 ** (FP6_EXP_BITS - 1) - 1
+FP8_EXP_BITS = 4
+FP8_MANTISSA_BITS = 3
+FP8_EXP_BIAS = 2 ** (FP8_EXP_BITS - 1) - 1
+
+
+def configure_fp_formats(fp4_exp_bits: int = 2, fp4_mantissa_bits: int = 1, fp6_exp_bits: int = 3,
+                         fp6_mantissa_bits: int = 2, fp8_exp_bits: int = 4, fp8_mantissa_bits: int = 3):
+    """quant_linear.py:84-110: set exponent/mantissa widths of FP4/FP6/FP8 (bias follows)."""
+    global FP4_EXP_BITS, FP4_MANTISSA_BITS, FP4_EXP_BIAS, FP6_EXP_BITS, FP6_MANTISSA_BITS, FP6_EXP_BIAS
+    global FP8_EXP_BITS, FP8_MANTISSA_BITS, FP8_EXP_BIAS
+    FP4_EXP_BITS, FP4_MANTISSA_BITS = int(fp4_exp_bits), int(fp4_mantissa_bits)
+    FP4_EXP_BIAS = 2 ** (FP4_EXP_BITS - 1) - 1
+    FP6_EXP_BITS, FP6_MANTISSA_BITS = int(fp6_exp_bits), int(fp6_mantissa_bits)
+    FP6_EXP_BIAS = 2 ** (FP6_EXP_BITS - 1) - 1
+    FP8_EXP_BITS, FP8_MANTISSA_BITS = int(fp8_exp_bits), int(fp8_mantissa_bits)
+    FP8_EXP_BIAS = 2 ** (FP8_EXP_BITS - 1) - 1
+
+
+def _fp_bits(fmt):
+    return {"fp4": (FP4_EXP_BITS, FP4_MANTISSA_BITS), "fp6": (FP6_EXP_BITS, FP6_MANTISSA_BITS),
+            "fp8": (FP8_EXP_BITS, FP8_MANTISSA_BITS)}[fmt]
 
 
 class QuantLinear(nn.Module):
@@ -93,10 +123,12 @@ class QuantLinear(nn.Module):
     def quantize_weight(self):
         """quant_linear.py:635-958 — INT branch on the GPU; in-place on self.weight."""
         with torch.no_grad():
-            if self.approximate or self.weight_format != "int":
+            if self.approximate or self.weight_format == "bfp":
                 raise NotImplementedError(
-                    f"weight_format={self.weight_format!r} approximate={self.approximate}: only the INT "
-                    "min-max format is on this build's hot path (SURVEY.md §8f lists the FP codec next)")
+                    f"weight_format={self.weight_format!r} approximate={self.approximate}: the BFP and "
+                    "approximate FIGLUT decode simulations are outside this build's hot path")
+            if self.weight_format in ("fp4", "fp6", "fp8"):
+                return self._quantize_weight_fp()
             if self.w_bit >= 16:
                 self.quantized.fill_(False)
                 self.weight_fp4 = None
@@ -118,6 +150,25 @@ class QuantLinear(nn.Module):
             self.weight_fp6 = None
             self.weight_fp8 = None
             self.quantized.fill_(True)
+
+    def _quantize_weight_fp(self):
+        """FP4/FP6/FP8 branches (quant_linear.py:724-883) on the GPU, in place on self.weight."""
+        if self.w_group_size not in (-1, -2) and not self.w_group_size > 0:
+            raise ValueError("Invalid w_group_size")
+        e, m = _fp_bits(self.weight_format)
+        w = self.weight.data
+        res = kernels.quantize_fp(w, e, m, self.w_group_size, bool(self.symmetric), self.quant_dim,
+                                  out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None,
+                                  want_codes=self.keep_codes)
+        if res.out is not w:
+            w.copy_(res.out)
+        self.scales = res.scales.view(-1, 1)
+        self.zeros = res.zeros.view(-1, 1) if res.zeros is not None else None
+        self.qweight = res.codes
+        for other in ("fp4", "fp6", "fp8"):
+            if other != self.weight_format:
+                setattr(self, f"weight_{other}", None)
+        self.quantized.fill_(True)
 
     def forward(self, input):
         """quant_linear.py:960-972: the dequantized weight already sits in self.weight."""
