@@ -137,6 +137,19 @@ int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int p
                  void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
                  void* stream);
 
+/*
+ * Fused dequant -> GEMM forward (QuantLinear.forward, quant_linear.py:960-972, on packed weights):
+ *   y[M, N] = x[M, K] . W_deq[N, K]^T (+ bias[N]),  W_deq = RN16((q - z) * s) per element
+ * x, bias, y fp16 row-major (lda, ldy elements); codes = packed 2..4-bit weights in the include/iwq.h
+ * layout ([N, K/2] bytes, low nibble = even k); scales/zeros [N * K/group] fp16 in the reference's
+ * group order (zeros NULL = symmetric, code offset 2^(n_bits-1)).  group: IWQ_GROUP_PER_CHANNEL or a
+ * multiple of 32 dividing K.  Requires N % 128 == 0, K % 128 == 0, 16-B aligned x / codes.
+ * fp32 accumulation on v_mfma_f32_16x16x32_f16.
+ */
+int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                   const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
+                   unsigned flags, void* stream);
+
 /* Deterministic synthetic weights (oracle/synth.py bit-for-bit), written to [rows, cols] contiguous. */
 int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t index_offset, void* stream);
 

@@ -26,7 +26,7 @@ IWQ_FLAG_BATCH_CODES = 0x100
 EXPORTS = (
     "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",
     "iwq_fill_synthetic", "iwq_status_string", "iwq_last_hip_error", "iwq_build_info",
-    "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid",
+    "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
 )
 
 
@@ -82,6 +82,8 @@ def load():
         lib.iwq_quantize_fp.restype = i32
         lib.iwq_fp4_grid.argtypes = [vp, i64, i64, i64, i32, vp, vp, vp, i64, vp, u32, vp]
         lib.iwq_fp4_grid.restype = i32
+        lib.iwq_w4a16_gemm.argtypes = [vp, i64, i64, i64, vp, vp, vp, i32, i64, i64, vp, vp, i64, u32, vp]
+        lib.iwq_w4a16_gemm.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]
         lib.iwq_selftest_division.restype = i32
         _lib = lib

@@ -1,0 +1,221 @@
+// iwq_gemm.hip — fused dequant -> GEMM forward for packed INT4 weights on gfx950 MFMA.
+//
+// Replaces the fake-quant forward of the reference, QuantLinear.forward = F.linear(x, W_deq, b)
+// (quant_linear.py:960-972), where W_deq is the fp16 dequantized weight written by
+// quantize_weight (:935-949).  Here the weight stays packed (4 bits + per-channel / per-group fp16
+// scale and zero point, include/iwq.h layout, 4x fewer weight bytes than fp16) and is dequantized
+// in registers inside the GEMM: each fp16 weight element is exactly the reference's
+// RN16((q - z) * s), so the result differs from F.linear on the dequantized weight only in fp32
+// accumulation order.
+//
+// Structure (k_w4a16): 128x128 output tile per 256-thread workgroup, 4 waves as 2 (M) x 2 (N),
+// each wave 64x64 = 4x4 v_mfma_f32_16x16x32_f16 tiles; K in steps of 128.
+//   X tile [128 x 128] fp16: global -> registers -> LDS (double-buffered, XOR-swizzled 16-B slots,
+//     halves permuted (0,4,1,5,2,6,3,7) inside each 8-element chunk), read with ds_read_b128.
+//   W: each lane streams 16 B of packed codes = 32 consecutive k of one output column per 128-k
+//     step straight into registers (no LDS), and per MFMA step dequantizes one dword: 8 nibbles ->
+//     (1024+q) fp16 pairs by one and-or each -> minus (1024+z) (exact) -> times s (RN16).  The
+//     nibble pairs come out as (k, k+4), which is why X is permuted the same way when staged: the
+//     MFMA's 32-wide k slice of lane group q is the logical k range [32q+8s, 32q+8s+8) of the tile.
+//   XCD-aware tile order: consecutive tiles of one X row panel are dealt to one XCD (L2 reuse).
+#include "iwq_common.cuh"
+#include "../../include/iwq.h"
+
+using namespace iwq;
+
+namespace {
+
+thread_local int g_last_hip_error_gemm = 0;
+
+constexpr int BM = 128, BN = 128, BK = 128, NTHR = 256;
+constexpr int LDS_TILE = BM * BK * 2;  // bytes of one X tile
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+struct GemmArgs {
+  const _Float16* x;    // [M, K], row stride lda
+  int64_t lda;
+  const uint8_t* codes; // [N, K/2] (two 4-bit codes per byte, low nibble = even k)
+  const _Float16* scales;
+  const _Float16* zeros;  // nullable: symmetric (z = 2^(b-1) offset folded in zoff)
+  const _Float16* bias;   // nullable
+  _Float16* y;          // [M, N], row stride ldy
+  int64_t ldy;
+  int M, N, K;
+  int gpr;              // scale groups per row = K / group
+  int group;            // group length along K (K for per-channel)
+  float zsym;           // symmetric code offset 2^(b-1)
+};
+
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+__device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
+  const int64_t xcd = bid % 8, i = bid / 8;
+  const int64_t q = nblocks / 8, r = nblocks % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+}
+
+__global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * LDS_TILE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int tiles_n = a.N / BN;
+  const int64_t nblocks = (int64_t)gridDim.x;
+  const int64_t t = swizzled_block(blockIdx.x, nblocks);
+  const int tm = (int)(t / tiles_n), tn = (int)(t % tiles_n);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = a.K / BK;
+
+  // ---- X staging: 2048 16-B chunks per tile, 8 per thread (row = c >> 4, slot = c & 15)
+  u32x4 xr[8];
+  auto load_x = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = tid + NTHR * i;
+      const int row = c >> 4, slot = c & 15;
+      const int gm = m0 + row;
+      const int64_t off = (int64_t)(gm < a.M ? gm : a.M - 1) * a.lda + (int64_t)kt * BK + slot * 8;
+      xr[i] = *gp<u32x4>(a.x + off);
+      if (gm >= a.M) xr[i] = (u32x4){0u, 0u, 0u, 0u};
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = tid + NTHR * i;
+      const int row = c >> 4, slot = c & 15;
+      const u32x4 d = xr[i];
+      const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                        perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+      *reinterpret_cast<u32x4*>(smem + buf * LDS_TILE + row * 256 + ((slot ^ (row & 15)) << 4)) = pd;
+    }
+  };
+
+  // ---- per-lane weight columns (one per 16-wide n subtile)
+  int ncol[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) ncol[nt] = n0 + wn * 64 + nt * 16 + r16;
+
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
+
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+
+  const int64_t crow = a.K / 2;  // bytes per packed row
+  for (int kt = 0; kt < nk; ++kt) {
+    const int k0 = kt * BK;
+    // packed codes of this lane: k in [k0 + 32q, k0 + 32q + 32) of 4 columns
+    u32x4 bc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+      bc[nt] = __builtin_nontemporal_load(gp<u32x4>(a.codes + (int64_t)ncol[nt] * crow + (k0 >> 1) + q * 16));
+    // scale / zero point of the group holding k0 + 32q (groups are >= 32 wide and aligned)
+    h2 sv[4], zv[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int64_t gi = (int64_t)ncol[nt] * a.gpr + (k0 + 32 * q) / a.group;
+      const _Float16 s = gp<_Float16>(a.scales)[gi];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
+      const _Float16 zz = (_Float16)(1024.0f + zf);  // exact: z is a small integer
+      sv[nt] = h2{s, s};
+      zv[nt] = h2{zz, zz};
+    }
+    if (kt + 1 < nk) load_x(kt + 1);
+    const uint8_t* xb = smem + (kt & 1) * LDS_TILE;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      h8 af[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int row = wm * 64 + mt * 16 + r16;
+        const int slot = 4 * q + s;
+        af[mt] = *reinterpret_cast<const h8*>(xb + row * 256 + ((slot ^ (row & 15)) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const uint32_t w = bc[nt][s];
+        h8 bf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const h2 c = as_h2(((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u);  // (1024+q_i, 1024+q_{i+4})
+          const h2 d = (c - zv[nt]) * sv[nt];                                 // RN16((q - z) * s)
+          bf[2 * i] = d.x;
+          bf[2 * i + 1] = d.y;
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt], bf, acc[mt][nt], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) store_x((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + reg
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = ncol[nt];
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + mt * 16 + 4 * q + r;
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(acc[mt][nt][r] + b);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                   const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
+                   unsigned flags, void* stream) {
+  (void)flags;
+  if (!x || !codes || !scales || !y) return IWQ_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldy < N) return IWQ_ERR_SHAPE;
+  if (N % BN != 0 || K % BK != 0 || (lda % 8) != 0) return IWQ_ERR_SHAPE;
+  if (n_bits < 2 || n_bits > 4) return IWQ_ERR_BITS;
+  const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
+  if (g <= 0 || g % 32 != 0 || K % g != 0) return IWQ_ERR_GROUP;
+  if ((reinterpret_cast<uintptr_t>(x) & 15u) || (reinterpret_cast<uintptr_t>(codes) & 15u)) return IWQ_ERR_ARG;
+  if (M > 0x7FFFFFFF || N > 0x7FFFFFFF || K > 0x7FFFFFFF) return IWQ_ERR_SHAPE;
+  GemmArgs a{};
+  a.x = static_cast<const _Float16*>(x);
+  a.lda = lda;
+  a.codes = static_cast<const uint8_t*>(codes);
+  a.scales = static_cast<const _Float16*>(scales);
+  a.zeros = static_cast<const _Float16*>(zeros);
+  a.bias = static_cast<const _Float16*>(bias);
+  a.y = static_cast<_Float16*>(y);
+  a.ldy = ldy;
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.group = (int)g;
+  a.gpr = (int)(K / g);
+  a.zsym = (float)(1 << (n_bits - 1));
+  const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
+  hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, static_cast<hipStream_t>(stream), a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_last_hip_error_gemm = (int)e;
+    return IWQ_ERR_HIP;
+  }
+  return IWQ_OK;
+}
+
+}  // extern "C"

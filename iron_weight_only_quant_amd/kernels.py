@@ -161,6 +161,30 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     return QuantResult(out, scales, None, None, nan_flag)
 
 
+def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
+    g = K if group == -2 else group
+    return (x.is_cuda and x.dtype == torch.float16 and 2 <= n_bits <= 4 and N % 128 == 0 and K % 128 == 0
+            and g > 0 and g % 32 == 0 and K % g == 0)
+
+
+def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
+               n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA)."""
+    L.require_device(x)
+    lib = L.load()
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    if x2.stride(-1) != 1 or x2.data_ptr() % 16 or x2.stride(0) % 8:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    y = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    with torch.cuda.device(x.device):
+        st = lib.iwq_w4a16_gemm(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
+                                int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, 0, L.stream_handle(x.device))
+    _raise_for(st, "iwq_w4a16_gemm")
+    return y.reshape(*x.shape[:-1], N)
+
+
 class BatchPlan:
     """Device-resident work table for quantizing many weights in one launch (quant_wrapper.py:52-82).
 

@@ -61,7 +61,8 @@ class QuantLinear(nn.Module):
                  fp8_hi_align_start: int = 12, fp8_hi_align_exp_field: int = 15, fp8_tail_pad_bits: int = 1,
                  double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
                  fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
-                 fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, _init_weight: bool = True):
+                 fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, fused_forward: bool = False,
+                 _init_weight: bool = True):
         super().__init__()
         self.in_features = in_features
         self.out_features = out_features
@@ -83,7 +84,8 @@ class QuantLinear(nn.Module):
         self.fp4_hi_align_start = fp4_hi_align_start
         self.fp4_hi_align_exp_field = fp4_hi_align_exp_field
         self.fp4_tail_pad_bits = fp4_tail_pad_bits
-        self.keep_codes = keep_codes
+        self.fused_forward = fused_forward
+        self.keep_codes = keep_codes or fused_forward
         if self.weight_format not in _FORMATS:
             raise ValueError(f"Unsupported weight_format: {weight_format}")
 
@@ -171,9 +173,19 @@ class QuantLinear(nn.Module):
         self.quantized.fill_(True)
 
     def forward(self, input):
-        """quant_linear.py:960-972: the dequantized weight already sits in self.weight."""
+        """quant_linear.py:960-972: the dequantized weight already sits in self.weight.
+
+        With fused_forward=True (INT, 2-4 bits, quant_dim 0) the GEMM reads the packed codes instead
+        (kernels.w4a16_gemm, MFMA): same weights, fp32 accumulation in a different order."""
         if not self.quantized:
             return F.linear(input, self.weight, self.bias)
+        if (self.fused_forward and self.weight_format == "int" and self.quant_dim == 0 and self.qweight is not None
+                and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
+                                                 self.w_group_size)
+                and (self.bias is None or self.bias.dtype == torch.float16)):
+            return kernels.w4a16_gemm(input, self.qweight, self.scales.view(-1),
+                                      None if self.zeros is None else self.zeros.view(-1), self.w_bit,
+                                      self.w_group_size, self.out_features, self.bias)
         original_input_shape = input.shape
         weight = self.weight.to(input.dtype)
         out = F.linear(input, weight, self.bias)
@@ -187,7 +199,8 @@ class QuantLinear(nn.Module):
                     fp8_hi_align_start: int = 12, fp8_hi_align_exp_field: int = 15, fp8_tail_pad_bits: int = 1,
                     double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
                     fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
-                    fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, quantize: bool = True):
+                    fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, fused_forward: bool = False,
+                    quantize: bool = True):
         """quant_linear.py:974-1033.  `quantize=False` is used by the batched model transform,
         which has already quantized the weight in one multi-tensor launch."""
         assert isinstance(linear_layer, nn.Linear), "Input layer must be nn.Linear"
@@ -199,7 +212,7 @@ class QuantLinear(nn.Module):
                 fp6_hi_align_start=fp6_hi_align_start, fp6_hi_align_exp_field=fp6_hi_align_exp_field,
                 fp6_tail_pad_bits=fp6_tail_pad_bits, fp4_hi_align_start=fp4_hi_align_start,
                 fp4_hi_align_exp_field=fp4_hi_align_exp_field, fp4_tail_pad_bits=fp4_tail_pad_bits,
-                keep_codes=keep_codes, _init_weight=False)
+                keep_codes=keep_codes, fused_forward=fused_forward, _init_weight=False)
         q.weight = nn.Parameter(linear_layer.weight.data.detach(), requires_grad=False)
         if linear_layer.bias is not None:
             q.bias = nn.Parameter(linear_layer.bias.data.detach(), requires_grad=False)

@@ -422,3 +422,51 @@ def test_fp_large_sha(K, FPD):
         assert hashlib.sha256(to_np(r.out).tobytes()).digest() == FPD[f"sha/{which}/{fmt}/{int(sym)}"].tobytes()
     r = K.fp4_grid(x, 128)
     assert hashlib.sha256(to_np(r.out).tobytes()).digest() == FPD["sha/grid/128"].tobytes()
+
+
+# ----------------------------------------------------------------------------------------------
+# fused dequant -> GEMM forward (config 3)
+# ----------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M", [1, 7, 128, 300])
+@pytest.mark.parametrize("group,sym,bits", [(-2, False, 4), (-2, True, 4), (128, False, 4), (32, True, 4),
+                                            (64, False, 3)])
+def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
+    """y = x W_deq^T + b with W_deq = the bit-exact fake-quant weight: compared with an fp32 GEMM on the
+    same dequantized weight (tolerance: fp16 output rounding + fp32 accumulation-order error)."""
+    N, Kd = 384, 512
+    torch.manual_seed(0)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 90)
+    r = K.quantize_minmax(w, bits, group, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b)
+    ref = x.float() @ r.out.float().t() + b.float()
+    err = (y.float() - ref).abs()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool((err <= tol).all()), float(err.max())
+    # and against the reference forward semantics: F.linear on the dequantized fp16 weight
+    y2 = torch.nn.functional.linear(x, r.out, b)
+    assert float((y.float() - y2.float()).abs().max()) <= 4 * float(err.max()) + 2e-3
+
+
+def test_w4a16_gemm_identity_layout(K):
+    """A = I with an asymmetric weight: catches any transposed or permuted output/operand mapping."""
+    N, Kd = 128, 128
+    w = (torch.arange(N * Kd, device=DEV, dtype=torch.float32).reshape(N, Kd) % 13 - 6).half()
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = torch.eye(Kd, device=DEV, dtype=torch.float16)
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
+    assert torch.equal(y, r.out.t().contiguous())
+
+
+def test_quantlinear_fused_forward(K):
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    lin = torch.nn.Linear(512, 256, bias=True).half().to(DEV)
+    q = QuantLinear.from_linear(lin, w_bit=4, w_group_size=-2, symmetric=False, fused_forward=True)
+    assert q.qweight is not None
+    x = torch.randn(3, 5, 512, device=DEV).half()
+    y = q(x)
+    ref = torch.nn.functional.linear(x, q.weight, q.bias)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
