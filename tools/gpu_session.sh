@@ -38,6 +38,9 @@ fi
 if [[ $WHAT == *b70* ]]; then
   step bench70b 900 python bench.py --model llama2-70b --steps 5 --warmup 2 --cpu-seconds 8
 fi
+if [[ $WHAT == *gemm* ]]; then
+  step bench_gemm 600 python tools/bench_gemm.py
+fi
 if [[ $WHAT == *ab* ]]; then
   step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
 fi
