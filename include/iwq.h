@@ -144,7 +144,8 @@ int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int p
  * layout ([N, K/2] bytes, low nibble = even k); scales/zeros [N * K/group] fp16 in the reference's
  * group order (zeros NULL = symmetric, code offset 2^(n_bits-1)).  group: IWQ_GROUP_PER_CHANNEL or a
  * multiple of 32 dividing K.  Requires N % 128 == 0, K % 128 == 0, 16-B aligned x / codes.
- * fp32 accumulation on v_mfma_f32_16x16x32_f16.
+ * fp32 accumulation on v_mfma_f32_16x16x32_f16.  M <= 16 takes the weight-streaming decode kernel
+ * (IWQ_FLAG_FORCE_GENERIC forces the tiled prefill kernel).
  */
 int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,

@@ -113,25 +113,34 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
   __syncthreads();
 
   const int64_t crow = a.K / 2;  // bytes per packed row
-  for (int kt = 0; kt < nk; ++kt) {
+  // packed codes of this lane for one 128-k step: k in [k0 + 32q, k0 + 32q + 32) of 4 columns, and
+  // the scale / zero point of the group holding k0 + 32q (groups are >= 32 wide and aligned)
+  auto load_b = [&](int kt, u32x4 (&bc)[4], h2 (&sv)[4], h2 (&zv)[4]) {
     const int k0 = kt * BK;
-    // packed codes of this lane: k in [k0 + 32q, k0 + 32q + 32) of 4 columns
-    u32x4 bc[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
       bc[nt] = __builtin_nontemporal_load(gp<u32x4>(a.codes + (int64_t)ncol[nt] * crow + (k0 >> 1) + q * 16));
-    // scale / zero point of the group holding k0 + 32q (groups are >= 32 wide and aligned)
-    h2 sv[4], zv[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int64_t gi = (int64_t)ncol[nt] * a.gpr + (k0 + 32 * q) / a.group;
-      const _Float16 s = gp<_Float16>(a.scales)[gi];
+      const _Float16 sc = gp<_Float16>(a.scales)[gi];
       const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
       const _Float16 zz = (_Float16)(1024.0f + zf);  // exact: z is a small integer
-      sv[nt] = h2{s, s};
+      sv[nt] = h2{sc, sc};
       zv[nt] = h2{zz, zz};
     }
-    if (kt + 1 < nk) load_x(kt + 1);
+  };
+  u32x4 bc[4];
+  h2 sv[4], zv[4];
+  load_b(0, bc, sv, zv);
+  for (int kt = 0; kt < nk; ++kt) {
+    // next step's weights and X tile are in flight during this step's MFMAs
+    u32x4 bcn[4];
+    h2 svn[4], zvn[4];
+    if (kt + 1 < nk) {
+      load_b(kt + 1, bcn, svn, zvn);
+      load_x(kt + 1);
+    }
     const uint8_t* xb = smem + (kt & 1) * LDS_TILE;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -157,7 +166,15 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
         for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt], bf, acc[mt][nt], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store_x((kt + 1) & 1);
+    if (kt + 1 < nk) {
+      store_x((kt + 1) & 1);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        bc[nt] = bcn[nt];
+        sv[nt] = svn[nt];
+        zv[nt] = zvn[nt];
+      }
+    }
     __syncthreads();
   }
 
@@ -177,6 +194,86 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_decode: M <= 16 (token decode).  HBM-bound on the packed weight bytes (0.5 B/weight +
+// scales), so the work is laid out for streaming, not for MFMA throughput: one workgroup per 16
+// output columns, its WAVES waves split K and each issues ALL its 16-B code loads (one per 128-k
+// step) before computing; the 16x16x32 MFMA (rows >= M zero) does the dot products, the waves'
+// partial tiles are summed through LDS.  X rows are read from L2 (16 B per lane per MFMA step,
+// permuted like the prefill kernel's LDS image).
+// ---------------------------------------------------------------------------------------------
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
+  constexpr int MAXSTEPS = 8;  // 128-k steps whose loads are in flight together
+  __shared__ __attribute__((aligned(16))) float red[WAVES][64 * 4];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int n = blockIdx.x * 16 + r16;
+  const int nk = a.K / BK;
+  const int per = (nk + WAVES - 1) / WAVES;
+  const int kb = wid * per, ke = min(kb + per, nk);
+  const int64_t crow = a.K / 2;
+  const int m = r16;  // A row of this lane
+  const bool mvalid = m < a.M;
+  const _Float16* xrow = a.x + (int64_t)(mvalid ? m : 0) * a.lda;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0s = kb; k0s < ke; k0s += MAXSTEPS) {
+    const int ns = min(MAXSTEPS, ke - k0s);
+    u32x4 bc[MAXSTEPS];
+#pragma unroll
+    for (int i = 0; i < MAXSTEPS; ++i) {
+      const int kt = k0s + (i < ns ? i : 0);
+      bc[i] = __builtin_nontemporal_load(gp<u32x4>(a.codes + (int64_t)n * crow + kt * (BK / 2) + q * 16));
+    }
+#pragma unroll
+    for (int i = 0; i < MAXSTEPS; ++i) {
+      if (i >= ns) break;
+      const int k0 = (k0s + i) * BK;
+      const int64_t gi = (int64_t)n * a.gpr + (k0 + 32 * q) / a.group;
+      const _Float16 sc = gp<_Float16>(a.scales)[gi];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
+      const h2 sv = h2{sc, sc};
+      const _Float16 zz = (_Float16)(1024.0f + zf);
+      const h2 zv = h2{zz, zz};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        u32x4 xa = {0u, 0u, 0u, 0u};
+        if (mvalid) xa = *gp<u32x4>(xrow + k0 + 32 * q + 8 * s);
+        const u32x4 pa = {perm(xa.z, xa.x, 0x05040100u), perm(xa.z, xa.x, 0x07060302u),
+                          perm(xa.w, xa.y, 0x05040100u), perm(xa.w, xa.y, 0x07060302u)};
+        const h8 af = __builtin_bit_cast(h8, pa);
+        const uint32_t w = bc[i][s];
+        h8 bf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const h2 c = as_h2(((w >> (4 * j)) & 0x000F000Fu) | 0x64006400u);
+          const h2 d = (c - zv) * sv;
+          bf[2 * j] = d.x;
+          bf[2 * j + 1] = d.y;
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][lane * 4 + r] = acc[r];
+  __syncthreads();
+  if (wid == 0) {
+    f4 t = acc;
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[r] += red[w][lane * 4 + r];
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[n] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 4 * q + r;  // C layout: col = lane & 15, row = 4 * (lane >> 4) + reg
+      if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + n] = (_Float16)(t[r] + b);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -184,7 +281,6 @@ extern "C" {
 int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
                    unsigned flags, void* stream) {
-  (void)flags;
   if (!x || !codes || !scales || !y) return IWQ_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldy < N) return IWQ_ERR_SHAPE;
   if (N % BN != 0 || K % BK != 0 || (lda % 8) != 0) return IWQ_ERR_SHAPE;
@@ -208,8 +304,14 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
   a.group = (int)g;
   a.gpr = (int)(K / g);
   a.zsym = (float)(1 << (n_bits - 1));
-  const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, static_cast<hipStream_t>(stream), a);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+    if (K >= 4096) hipLaunchKernelGGL(k_w4a16_decode<8>, dim3((unsigned)(N / 16)), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(k_w4a16_decode<4>, dim3((unsigned)(N / 16)), dim3(256), 0, st, a);
+  } else {
+    const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
+    hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, st, a);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_last_hip_error_gemm = (int)e;

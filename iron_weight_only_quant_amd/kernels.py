@@ -168,7 +168,7 @@ def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: in
 
 
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
-               n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+               n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0) -> torch.Tensor:
     """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA)."""
     L.require_device(x)
     lib = L.load()
@@ -180,7 +180,8 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     y = torch.empty((M, N), dtype=torch.float16, device=x.device)
     with torch.cuda.device(x.device):
         st = lib.iwq_w4a16_gemm(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
-                                int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, 0, L.stream_handle(x.device))
+                                int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, int(flags),
+                                L.stream_handle(x.device))
     _raise_for(st, "iwq_w4a16_gemm")
     return y.reshape(*x.shape[:-1], N)
 

@@ -427,24 +427,25 @@ def test_fp_large_sha(K, FPD):
 # ----------------------------------------------------------------------------------------------
 # fused dequant -> GEMM forward (config 3)
 # ----------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("M", [1, 7, 128, 300])
+@pytest.mark.parametrize("M", [1, 7, 16, 128, 300])
 @pytest.mark.parametrize("group,sym,bits", [(-2, False, 4), (-2, True, 4), (128, False, 4), (32, True, 4),
                                             (64, False, 3)])
 def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     """y = x W_deq^T + b with W_deq = the bit-exact fake-quant weight: compared with an fp32 GEMM on the
     same dequantized weight (tolerance: fp16 output rounding + fp32 accumulation-order error)."""
-    N, Kd = 384, 512
+    N, Kd = 384, 4352
     torch.manual_seed(0)
     w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
     K.fill_synthetic(w, 90)
     r = K.quantize_minmax(w, bits, group, sym, 0, want_codes=True)
     x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
     b = (torch.randn(N, device=DEV) * 0.1).half()
-    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b)
     ref = x.float() @ r.out.float().t() + b.float()
-    err = (y.float() - ref).abs()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    assert bool((err <= tol).all()), float(err.max())
+    for flags in (0, 1):  # decode kernel (M <= 16) and the tiled prefill kernel
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b, flags=flags)
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (flags, float(err.max()))
     # and against the reference forward semantics: F.linear on the dequantized fp16 weight
     y2 = torch.nn.functional.linear(x, r.out, b)
     assert float((y.float() - y2.float()).abs().max()) <= 4 * float(err.max()) + 2e-3
