@@ -204,7 +204,7 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
-  constexpr int MAXSTEPS = 8;  // 128-k steps whose loads are in flight together
+  constexpr int CH = 4;  // 128-k steps per chunk: all their code, scale and X loads are in flight together
   __shared__ __attribute__((aligned(16))) float red[WAVES][64 * 4];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -214,34 +214,38 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
   const int per = (nk + WAVES - 1) / WAVES;
   const int kb = wid * per, ke = min(kb + per, nk);
   const int64_t crow = a.K / 2;
-  const int m = r16;  // A row of this lane
-  const bool mvalid = m < a.M;
-  const _Float16* xrow = a.x + (int64_t)(mvalid ? m : 0) * a.lda;
+  const bool mvalid = r16 < a.M;  // A row of this lane = r16
+  const _Float16* xrow = a.x + (int64_t)(mvalid ? r16 : 0) * a.lda;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k0s = kb; k0s < ke; k0s += MAXSTEPS) {
-    const int ns = min(MAXSTEPS, ke - k0s);
-    u32x4 bc[MAXSTEPS];
+  for (int c0 = kb; c0 < ke; c0 += CH) {
+    const int ns = min(CH, ke - c0);
+    u32x4 bc[CH];
+    u32x4 xa[CH][4];
+    _Float16 sc[CH];
+    float zf[CH];
 #pragma unroll
-    for (int i = 0; i < MAXSTEPS; ++i) {
-      const int kt = k0s + (i < ns ? i : 0);
+    for (int i = 0; i < CH; ++i) {
+      const int kt = c0 + (i < ns ? i : 0);
+      const int k0 = kt * BK;
       bc[i] = __builtin_nontemporal_load(gp<u32x4>(a.codes + (int64_t)n * crow + kt * (BK / 2) + q * 16));
+      const int64_t gi = (int64_t)n * a.gpr + (k0 + 32 * q) / a.group;
+      sc[i] = gp<_Float16>(a.scales)[gi];
+      zf[i] = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        xa[i][s] = *gp<u32x4>(xrow + k0 + 32 * q + 8 * s);  // unconditional (row 0 for padding lanes)
     }
 #pragma unroll
-    for (int i = 0; i < MAXSTEPS; ++i) {
+    for (int i = 0; i < CH; ++i) {
       if (i >= ns) break;
-      const int k0 = (k0s + i) * BK;
-      const int64_t gi = (int64_t)n * a.gpr + (k0 + 32 * q) / a.group;
-      const _Float16 sc = gp<_Float16>(a.scales)[gi];
-      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
-      const h2 sv = h2{sc, sc};
-      const _Float16 zz = (_Float16)(1024.0f + zf);
+      const h2 sv = h2{sc[i], sc[i]};
+      const _Float16 zz = (_Float16)(1024.0f + zf[i]);
       const h2 zv = h2{zz, zz};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        u32x4 xa = {0u, 0u, 0u, 0u};
-        if (mvalid) xa = *gp<u32x4>(xrow + k0 + 32 * q + 8 * s);
-        const u32x4 pa = {perm(xa.z, xa.x, 0x05040100u), perm(xa.z, xa.x, 0x07060302u),
-                          perm(xa.w, xa.y, 0x05040100u), perm(xa.w, xa.y, 0x07060302u)};
+        const u32x4 x4 = mvalid ? xa[i][s] : (u32x4){0u, 0u, 0u, 0u};
+        const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
+                          perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
         const h8 af = __builtin_bit_cast(h8, pa);
         const uint32_t w = bc[i][s];
         h8 bf;
