@@ -53,3 +53,8 @@ def build_library(force=False, verbose=True):
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(tmp, LIB)
     return LIB
+
+
+if __name__ == "__main__":
+    import sys
+    build_library(force="--force" in sys.argv)

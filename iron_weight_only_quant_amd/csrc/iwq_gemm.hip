@@ -45,11 +45,26 @@ struct GemmArgs {
   int M, N, K;
   int gpr;              // scale groups per row = K / group
   int group;            // group length along K (K for per-channel)
+  int gshift;           // log2(group) when group is a power of two, else -1
   float zsym;           // symmetric code offset 2^(b-1)
 };
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
   return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// 8 packed 4-bit codes (nibble p of w = k offset p) -> 8 dequantized fp16 RN16((q - z) * s) in the
+// MFMA k order (0,4,1,5,2,6,3,7).  Nibbles 0/4 and 2/6 become (1024 + q) by one and-or with 0x6400
+// (fp16 mantissa ulp 1 at 1024); nibbles 1/5 and 3/7 sit at mantissa bits 4..7, so or-ing 0x5400
+// (64, ulp 1/16) gives (64 + q) with no shift.  (q - z) is then one exact subtraction and the only
+// rounding is the multiply by s — the reference's fp16 dequant, element for element.
+__device__ __forceinline__ h8 dequant8(uint32_t w, h2 z1024, h2 z64, h2 s) {
+  const uint32_t w8 = w >> 8;
+  const h2 d0 = (as_h2((w & 0x000F000Fu) | 0x64006400u) - z1024) * s;
+  const h2 d1 = (as_h2((w & 0x00F000F0u) | 0x54005400u) - z64) * s;
+  const h2 d2 = (as_h2((w8 & 0x000F000Fu) | 0x64006400u) - z1024) * s;
+  const h2 d3 = (as_h2((w8 & 0x00F000F0u) | 0x54005400u) - z64) * s;
+  return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
 }
 
 __device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
@@ -125,11 +140,12 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
       const int64_t gi = (int64_t)ncol[nt] * a.gpr + (k0 + 32 * q) / a.group;
       const _Float16 sc = gp<_Float16>(a.scales)[gi];
       const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
-      const _Float16 zz = (_Float16)(1024.0f + zf);  // exact: z is a small integer
+      const _Float16 zz = (_Float16)zf;  // exact: z is a small integer
       sv[nt] = h2{sc, sc};
       zv[nt] = h2{zz, zz};
     }
   };
+  const h2 k1024 = h2{(_Float16)1024.0f, (_Float16)1024.0f}, k64 = h2{(_Float16)64.0f, (_Float16)64.0f};
   u32x4 bc[4];
   h2 sv[4], zv[4];
   load_b(0, bc, sv, zv);
@@ -153,15 +169,7 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
       }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const uint32_t w = bc[nt][s];
-        h8 bf;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const h2 c = as_h2(((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u);  // (1024+q_i, 1024+q_{i+4})
-          const h2 d = (c - zv[nt]) * sv[nt];                                 // RN16((q - z) * s)
-          bf[2 * i] = d.x;
-          bf[2 * i + 1] = d.y;
-        }
+        const h8 bf = dequant8(bc[nt][s], zv[nt] + k1024, zv[nt] + k64, sv[nt]);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt], bf, acc[mt][nt], 0, 0, 0);
       }
@@ -239,23 +247,15 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
     for (int i = 0; i < CH; ++i) {
       if (i >= ns) break;
       const h2 sv = h2{sc[i], sc[i]};
-      const _Float16 zz = (_Float16)(1024.0f + zf[i]);
-      const h2 zv = h2{zz, zz};
+      const _Float16 zz = (_Float16)(1024.0f + zf[i]), z6 = (_Float16)(64.0f + zf[i]);
+      const h2 zv = h2{zz, zz}, zv64 = h2{z6, z6};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const u32x4 x4 = mvalid ? xa[i][s] : (u32x4){0u, 0u, 0u, 0u};
         const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
                           perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
         const h8 af = __builtin_bit_cast(h8, pa);
-        const uint32_t w = bc[i][s];
-        h8 bf;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const h2 c = as_h2(((w >> (4 * j)) & 0x000F000Fu) | 0x64006400u);
-          const h2 d = (c - zv) * sv;
-          bf[2 * j] = d.x;
-          bf[2 * j + 1] = d.y;
-        }
+        const h8 bf = dequant8(bc[i][s], zv, zv64, sv);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
       }
     }
@@ -275,6 +275,148 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
       const int row = 4 * q + r;  // C layout: col = lane & 15, row = 4 * (lane >> 4) + reg
       if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + n] = (_Float16)(t[r] + b);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_gemv: M <= 16 (token decode), the weight-streaming kernel.  HBM-bound on the packed
+// weight bytes, so it is organised around bytes in flight:
+//   - a workgroup of T*S waves owns T tiles of 16 output columns; wave (tile, ks) takes the 128-k
+//     steps ks, ks+S, ks+2S, ... of its tile (consecutive steps of one column row are loaded by
+//     neighbouring waves at the same time);
+//   - each wave keeps a ring of PF steps of packed-code loads (1 KiB each) in flight: step j is
+//     dequantized + MFMA'd, then its slot is refilled with step j+PF;
+//   - X (M x K fp16, L2-resident, shared by all workgroups) is staged once per workgroup into LDS,
+//     pre-permuted to the nibble-pair order, when it fits (XLDS); then the A operand is an LDS read
+//     (lgkmcnt) that never makes a wave wait behind its own code prefetches on the in-order
+//     vmcnt.  Otherwise the X fragments of a step ride in the same ring slot as its codes.
+//   - lanes whose A row is >= M read row M-1 (their C rows are discarded); the S partial tiles of a
+//     column tile are summed through LDS in k-split order (deterministic).
+// ---------------------------------------------------------------------------------------------
+constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X image (2+ workgroups per CU)
+
+template <int PF, int S, int T, bool XLDS, int PROBE = 0>
+__global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
+  constexpr int WPB = S * T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = wid % T, ks = wid / T;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int n = (blockIdx.x * T + tile) * 16 + r16;
+  const int nks = a.K / BK;
+  const int nj = nks > ks ? (nks - ks + S - 1) / S : 0;  // steps of this wave: kt = ks + j*S
+  const int64_t crow = a.K / 2;
+  const int arow = r16 < a.M ? r16 : a.M - 1;
+  const int xpitch = a.K * 2 + 16;                       // LDS row pitch (bytes), +16 vs bank conflicts
+  const uint8_t* cbase = a.codes + (int64_t)n * crow + q * 16;
+  const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
+  const bool perch = a.gpr == 1;                          // one scale/zero per column: hoisted
+
+  _Float16 sc0 = (_Float16)0.f, zz0 = (_Float16)0.f;
+  if (perch) {
+    sc0 = gp<_Float16>(a.scales)[n];
+    zz0 = a.zeros ? gp<_Float16>(a.zeros)[n] : (_Float16)a.zsym;
+  }
+  const h2 k1024 = h2{(_Float16)1024.0f, (_Float16)1024.0f}, k64 = h2{(_Float16)64.0f, (_Float16)64.0f};
+  u32x4 bc[PF];
+  _Float16 sv[PF], zv[PF];
+  u32x4 xa[XLDS ? 1 : PF][4];
+  auto load = [&](int j, int u) {
+    const int kt = ks + j * S;
+    bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * (BK / 2)));
+    if (!perch) {
+      const int kk = kt * BK + 32 * q;
+      const int64_t gi = (int64_t)n * a.gpr + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group);
+      sv[u] = gp<_Float16>(a.scales)[gi];
+      zv[u] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
+    }
+    if constexpr (!XLDS) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nj) load(u, u);
+
+  if constexpr (XLDS) {
+    // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c
+    const int cpr = a.K / 8;
+    for (int m = 0; m < a.M; ++m) {
+      const _Float16* xr = a.x + (int64_t)m * a.lda;
+      for (int c = threadIdx.x; c < cpr; c += WPB * 64) {
+        const u32x4 d = *gp<u32x4>(xr + 8 * c);
+        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+      }
+    }
+    __syncthreads();
+  }
+  const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nj; j0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int j = j0 + u;
+      if (j >= nj) break;
+      const int kt = ks + j * S;
+      const h2 s2 = perch ? h2{sc0, sc0} : h2{sv[u], sv[u]};
+      const h2 z2 = perch ? h2{zz0, zz0} : h2{zv[u], zv[u]};
+      const h2 z1024 = z2 + k1024, z64 = z2 + k64;  // exact: z is a small integer
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        h8 af;
+        if constexpr (XLDS) {
+          af = *reinterpret_cast<const h8*>(xsrow + kt * (BK * 2) + 16 * s);
+        } else {
+          const u32x4 x4 = xa[u][s];
+          const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
+                            perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
+          af = __builtin_bit_cast(h8, pa);
+        }
+        h8 bf;
+        if constexpr (PROBE == 1) {  // A/B probe only: no dequantization (wrong results)
+          const uint32_t w = bc[u][s];
+          bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
+        } else {
+          bf = dequant8(bc[u][s], z1024, z64, s2);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
+      }
+      if (j + PF < nj) load(j + PF, u);
+    }
+  }
+  if constexpr (XLDS) __syncthreads();  // X image dead: its LDS now holds the partial tiles
+  float* red = reinterpret_cast<float*>(dsm);  // [WPB][256], wave (tile, ks) at index ks*T + tile
+  *reinterpret_cast<f4*>(red + wid * 256 + lane * 4) = acc;
+  __syncthreads();
+  for (int o = threadIdx.x; o < T * 256; o += WPB * 64) {
+    const int t = o >> 8, e = o & 255;                    // e = lane' * 4 + reg of the C layout
+    const int ln = e >> 2, reg = e & 3;
+    const int row = 4 * (ln >> 4) + reg, col = (blockIdx.x * T + t) * 16 + (ln & 15);
+    if (row < a.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) v += red[(k * T + t) * 256 + e];
+      if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
+      gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+    }
+  }
+}
+
+template <int PF, int S, int T, int PROBE = 0>
+void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
+  const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
+  const unsigned blocks = (unsigned)(a.N / (16 * T));
+  const size_t red = (size_t)S * T * 256 * 4;
+  if (allow_lds && xbytes <= XLDS_MAX) {
+    const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+  } else {
+    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE>), dim3(blocks), dim3(S * T * 64), red, st, a);
   }
 }
 
@@ -308,10 +450,29 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
   a.group = (int)g;
   a.gpr = (int)(K / g);
   a.zsym = (float)(1 << (n_bits - 1));
+  a.gshift = (g & (g - 1)) == 0 ? __builtin_ctzll((unsigned long long)g) : -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned variant = (flags >> 16) & 0xFFu;
   if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
-    if (K >= 4096) hipLaunchKernelGGL(k_w4a16_decode<8>, dim3((unsigned)(N / 16)), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(k_w4a16_decode<4>, dim3((unsigned)(N / 16)), dim3(256), 0, st, a);
+    switch (variant) {
+      case 1:  // previous decode kernel (A/B reference)
+        if (K >= 4096) hipLaunchKernelGGL(k_w4a16_decode<8>, dim3((unsigned)(N / 16)), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(k_w4a16_decode<4>, dim3((unsigned)(N / 16)), dim3(256), 0, st, a);
+        break;
+      case 2: launch_gemv<4, 8, 1>(a, st, true); break;
+      case 3: launch_gemv<4, 8, 1>(a, st, false); break;
+      case 4: launch_gemv<4, 4, 2>(a, st, true); break;
+      case 5: launch_gemv<4, 4, 4>(a, st, true); break;
+      case 6: launch_gemv<2, 8, 1>(a, st, true); break;
+      case 7: launch_gemv<6, 4, 2>(a, st, true); break;
+      case 8: launch_gemv<4, 16, 1>(a, st, true); break;
+      case 9: launch_gemv<8, 4, 1>(a, st, true); break;
+      case 10: launch_gemv<4, 2, 4>(a, st, true); break;
+      case 11: launch_gemv<2, 4, 2>(a, st, false); break;
+      case 100: launch_gemv<2, 8, 1, 1>(a, st, true); break;  // probes: no dequant
+      case 101: launch_gemv<4, 8, 1, 1>(a, st, true); break;
+      default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 3 % of best at M in {1, 4, 16}
+    }
   } else {
     const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, st, a);

@@ -161,6 +161,11 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     return QuantResult(out, scales, None, None, nan_flag)
 
 
+def gemm_variant_flags(v: int) -> int:
+    """IWQ_FLAG_VARIANT(v) for iwq_w4a16_gemm's decode path (0 = default; A/B and tests only)."""
+    return (int(v) & 0xFF) << 16
+
+
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
     g = K if group == -2 else group
     return (x.is_cuda and x.dtype == torch.float16 and 2 <= n_bits <= 4 and N % 128 == 0 and K % 128 == 0

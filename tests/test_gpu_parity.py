@@ -429,7 +429,7 @@ def test_fp_large_sha(K, FPD):
 # ----------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("M", [1, 7, 16, 128, 300])
 @pytest.mark.parametrize("group,sym,bits", [(-2, False, 4), (-2, True, 4), (128, False, 4), (32, True, 4),
-                                            (64, False, 3)])
+                                            (64, False, 3), (544, False, 4)])
 def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     """y = x W_deq^T + b with W_deq = the bit-exact fake-quant weight: compared with an fp32 GEMM on the
     same dequantized weight (tolerance: fp16 output rounding + fp32 accumulation-order error)."""
@@ -442,7 +442,8 @@ def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    for flags in (0, 1):  # decode kernel (M <= 16) and the tiled prefill kernel
+    # default (decode kernel for M <= 16), the tiled prefill kernel, and every decode variant
+    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 12) if M <= 16):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b, flags=flags)
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (flags, float(err.max()))
@@ -459,6 +460,10 @@ def test_w4a16_gemm_identity_layout(K):
     x = torch.eye(Kd, device=DEV, dtype=torch.float16)
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
+    for m in (1, 5, 16):  # decode kernels: rows of the identity pick weight columns exactly
+        for v in range(0, 12):
+            y = K.w4a16_gemm(x[:m].contiguous(), r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
+            assert torch.equal(y, r.out.t()[:m].contiguous()), (m, v)
 
 
 def test_quantlinear_fused_forward(K):

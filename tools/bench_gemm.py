@@ -65,34 +65,38 @@ def main():
     ap.add_argument("--m", default="8192,16,1")
     ap.add_argument("--group", type=int, default=-2)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="0", help="decode-kernel variants to time for M <= 16 (IWQ_FLAG_VARIANT)")
+    ap.add_argument("--shapes", default="q_proj,gate_proj,down_proj")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels
-    for name, N, K in SHAPES:
+    shapes = SHAPES + [("70b_gate", 28672, 8192), ("70b_down", 8192, 28672)]
+    for name, N, K in [t for t in shapes if t[0] in a.shapes.split(",")]:
         w = torch.empty(N, K, dtype=torch.float16, device="cuda")
         kernels.fill_synthetic(w, 7)
         r = kernels.quantize_minmax(w, 4, a.group, False, 0, want_codes=True)
         for M in [int(m) for m in a.m.split(",")]:
             x = (torch.randn(M, K, device="cuda") * 0.5).half()
-            fused = lambda: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N)
             ref = lambda: torch.nn.functional.linear(x, r.out)
-            fused(); ref(); torch.cuda.synchronize()
-            err = float((fused().float() - ref().float()).abs().max())
-            reps = a.reps if M >= 1024 else a.reps * 20
-            if M >= 1024:
-                t_f = timed(fused, reps)
-                t_r = timed(ref, reps)
-            else:  # decode: launch-bound from Python, so time device work via hipGraph replay
-                t_f = timed_graph(fused, 50)
-                t_r = timed_graph(ref, 50)
-            flops = 2.0 * M * N * K
-            rec = {"shape": name, "M": M, "N": N, "K": K, "group": a.group,
-                   "fused_ms": round(t_f, 4), "fused_tflops": round(flops / t_f / 1e9, 1),
-                   "fused_frac_peak": round(flops / t_f / 1e9 / PEAK_TFLOPS, 4),
-                   "hipblaslt_fp16_ms": round(t_r, 4), "hipblaslt_tflops": round(flops / t_r / 1e9, 1),
-                   "speedup_vs_F_linear": round(t_r / t_f, 3),
-                   "weight_bytes_fused": int(r.codes.numel() + r.scales.numel() * 4),
-                   "weight_bytes_fp16": int(N * K * 2), "max_abs_diff_vs_F_linear": err}
-            print(json.dumps(rec), flush=True)
+            ref()
+            t_r = timed(ref, a.reps) if M >= 1024 else timed_graph(ref, 50)
+            for v in ([0] if M >= 1024 else [int(t) for t in a.variants.split(",")]):
+                fl = kernels.gemm_variant_flags(v)
+                fused = lambda: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N, flags=fl)
+                fused(); torch.cuda.synchronize()
+                err = float((fused().float() - ref().float()).abs().max())
+                # decode: launch-bound from Python, so time device work via hipGraph replay
+                t_f = timed(fused, a.reps) if M >= 1024 else timed_graph(fused, 50)
+                flops = 2.0 * M * N * K
+                wbytes = int(r.codes.numel() + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0))
+                rec = {"shape": name, "M": M, "N": N, "K": K, "group": a.group, "variant": v,
+                       "fused_ms": round(t_f, 4), "fused_tflops": round(flops / t_f / 1e9, 1),
+                       "fused_frac_peak": round(flops / t_f / 1e9 / PEAK_TFLOPS, 4),
+                       "fused_weight_GBps": round(wbytes / t_f / 1e6, 1),
+                       "hipblaslt_fp16_ms": round(t_r, 4), "hipblaslt_tflops": round(flops / t_r / 1e9, 1),
+                       "speedup_vs_F_linear": round(t_r / t_f, 3),
+                       "weight_bytes_fused": wbytes,
+                       "weight_bytes_fp16": int(N * K * 2), "max_abs_diff_vs_F_linear": err}
+                print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -39,7 +39,7 @@ if [[ $WHAT == *b70* ]]; then
   step bench70b 900 python bench.py --model llama2-70b --steps 5 --warmup 2 --cpu-seconds 8
 fi
 if [[ $WHAT == *gemm* ]]; then
-  step bench_gemm 600 python tools/bench_gemm.py
+  step bench_gemm 600 python tools/bench_gemm.py ${GEMM_ARGS:-}
 fi
 if [[ $WHAT == *ppl* ]]; then
   step ppl_opt125m 600 python tools/ppl_delta.py --random opt-125m --synthetic_tokens 65536 --w_bits 8 4 --w_group_size -2
