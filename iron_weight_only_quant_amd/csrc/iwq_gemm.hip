@@ -471,7 +471,9 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 11: launch_gemv<2, 4, 2>(a, st, false); break;
       case 100: launch_gemv<2, 8, 1, 1>(a, st, true); break;  // probes: no dequant
       case 101: launch_gemv<4, 8, 1, 1>(a, st, true); break;
-      default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 3 % of best at M in {1, 4, 16}
+      case 12: launch_gemv<2, 4, 1>(a, st, true); break;
+      case 13: launch_gemv<2, 16, 1>(a, st, true); break;
+      default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
     }
   } else {
     const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);

@@ -443,7 +443,7 @@ def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     # default (decode kernel for M <= 16), the tiled prefill kernel, and every decode variant
-    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 12) if M <= 16):
+    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 14) if M <= 16):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b, flags=flags)
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (flags, float(err.max()))
@@ -461,7 +461,7 @@ def test_w4a16_gemm_identity_layout(K):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
     for m in (1, 5, 16):  # decode kernels: rows of the identity pick weight columns exactly
-        for v in range(0, 12):
+        for v in range(0, 14):
             y = K.w4a16_gemm(x[:m].contiguous(), r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
             assert torch.equal(y, r.out.t()[:m].contiguous()), (m, v)
 
