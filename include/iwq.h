@@ -128,6 +128,34 @@ int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int
                     unsigned flags, void* stream);
 
 /*
+ * QuantLinear.quantize_weight_approximate (quant_linear.py:470-632), fp16 weights: symmetric absmax
+ * FP codes exactly as iwq_quantize_fp (symmetric=1), decoded by the "aligned" decoder
+ * _fp_decode_aligned (:237-285) or, with double_approx, fp_decode_aligned_double_approx (:288-363:
+ * quads = 4 consecutive groups at one in-group position), then out = RN16(decoded * scale).
+ * hi_align_start / hi_align_exp_field / tail_pad_bits: the fpN_* arguments of QuantLinear.
+ * group > 0 only (IWQ_ERR_GROUP_MODE); out_scales [G] fp16 required.  workspace: at least
+ * iwq_approx_workspace_bytes(...) bytes, 16-B aligned (codes of the double-approximate pass and the
+ * generic path's group keys).
+ */
+int64_t iwq_approx_workspace_bytes(int64_t rows, int64_t cols, int exp_bits, int mant_bits, int64_t group,
+                                   int quant_dim, int double_approx);
+int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                           int mant_bits, int64_t group, int quant_dim, int hi_align_start, int hi_align_exp_field,
+                           int tail_pad_bits, int double_approx, void* out_deq, int64_t ld_out, void* out_scales,
+                           void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                           void* stream);
+
+/*
+ * QuantLinear.quantize_weight, weight_format "bfp" (quant_linear.py:648-723): block floating point
+ * with a shared per-group exponent (max fp16 exponent field of the group) and min(w_bit-1, 11)
+ * mantissa bits incl. the leading one (round-half-up, saturating).  dtype F16 / BF16 / F32 (taken to
+ * fp16 first, like the reference); out may equal w (in place).  group > 0 (IWQ_ERR_GROUP_MODE),
+ * grouped dimension % group == 0 (IWQ_ERR_GROUP), w_bit >= 1 (IWQ_ERR_BITS).  No scales / zeros.
+ */
+int iwq_quantize_bfp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int w_bit, int64_t group,
+                     int quant_dim, void* out, int64_t ld_out, unsigned flags, void* stream);
+
+/*
  * fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 (fp4_quantize_cpu.py:47-72): the E2M1 "grid" fake
  * quantizer (per-group absmax scale S = absmax/6, AxCore two-step rounding), fp16 [rows, cols]
  * contiguous -> fp16 out (same element order; the reference returns it viewed [-1, group]).

@@ -27,6 +27,7 @@ EXPORTS = (
     "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",
     "iwq_fill_synthetic", "iwq_status_string", "iwq_last_hip_error", "iwq_build_info",
     "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
+    "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
 )
 
 
@@ -84,6 +85,13 @@ def load():
         lib.iwq_fp4_grid.restype = i32
         lib.iwq_w4a16_gemm.argtypes = [vp, i64, i64, i64, vp, vp, vp, i32, i64, i64, vp, vp, i64, u32, vp]
         lib.iwq_w4a16_gemm.restype = i32
+        lib.iwq_approx_workspace_bytes.argtypes = [i64, i64, i32, i32, i64, i32, i32]
+        lib.iwq_approx_workspace_bytes.restype = i64
+        lib.iwq_quantize_fp_approx.argtypes = [vp, i64, i64, i64, i32, i32, i32, i64, i32, i32, i32, i32, i32, vp,
+                                               i64, vp, vp, i64, vp, u32, vp]
+        lib.iwq_quantize_fp_approx.restype = i32
+        lib.iwq_quantize_bfp.argtypes = [vp, i64, i64, i64, i32, i32, i64, i32, vp, i64, u32, vp]
+        lib.iwq_quantize_bfp.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]
         lib.iwq_selftest_division.restype = i32
         _lib = lib

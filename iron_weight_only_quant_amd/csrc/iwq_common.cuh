@@ -15,6 +15,10 @@
 
 namespace iwq {
 
+// last HIP error of this host thread, shared by every translation unit (iwq_last_hip_error)
+int& last_hip_error();
+
+
 enum : int { DT_F16 = 0, DT_BF16 = 1, DT_F32 = 2 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

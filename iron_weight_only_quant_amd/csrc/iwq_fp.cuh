@@ -23,6 +23,7 @@ struct FpSpec {
   float fp_max16;    // RN16(fp_max): torch.clamp converts its bounds to half
   float rmax;        // RN32(1/fp_max): corrected division when fp_max is an fp16 value
   int fpmax_is_f16;  // fp_max exactly representable in fp16
+  int hs, hf, tp;    // approximate decodes: hi_align_start, hi_align_exp_field, tail_pad_bits
 };
 
 // floor(RN16(log2 x)) for a positive fp16 magnitude (bit pattern, 1..0x7BFF)
@@ -128,6 +129,99 @@ __device__ __forceinline__ float fp_quant_elem(float w, const FpParams& p, const
   if constexpr (!SYM) y = f16r(y + p.z);                                  // + zeros
   if (t != t) y = t;                                                      // NaN scale: NaN out
   return y;
+}
+
+// ---------------------------------------------------------------------------------------------
+// "approximate" decodes (quant_linear.py:112-123, :237-363).  Integer steps follow ATen's shift
+// semantics: x << b == 0 and x >> b == x >> (width-1) once b >= width; the double-approximate
+// decoder's tensors are int8, so its adds and shifts wrap at 8 bits (w8).
+__device__ __forceinline__ int w8(int x) { return (int)(int8_t)(uint8_t)(x & 0xFF); }
+__device__ __forceinline__ int lsh8(int a, int b) { return (b < 0 || b >= 8) ? 0 : w8(a << b); }
+__device__ __forceinline__ int rsh8(int a, int b) { return (b < 0 || b >= 8) ? (a >> 7) : (a >> b); }
+__device__ __forceinline__ int rrsh8(int v, int s) { return rsh8(w8(v + (s > 0 ? lsh8(1, s - 1) : 0)), s); }
+__device__ __forceinline__ int lsh32(int a, int b) { return (b < 0 || b >= 32) ? 0 : (int)((uint32_t)a << b); }
+__device__ __forceinline__ int rsh32(int a, int b) { return (b < 0 || b >= 32) ? (a >> 31) : (a >> b); }
+__device__ __forceinline__ int rrsh32(int v, int s) {
+  return rsh32((int)((uint32_t)v + (uint32_t)(s > 0 ? lsh32(1, s - 1) : 0)), s);
+}
+
+// _fp_decode_aligned (quant_linear.py:237-285) as every caller uses it (align_subnorm_exp_as_one,
+// limit_align_exp_to_field, decode_dtype fp16): codes whose aligned exponent is in [hs, hf] are
+// re-expressed at exponent hf (mantissa padded by tp bits, rounding right shift by hf - exp), the
+// others decode normally.  Exact value in fp32; code 0 -> +0, sign-only code -> -0.
+__device__ __forceinline__ float fp_decode_aligned(uint32_t code, const FpSpec& f) {
+  code &= 0xFFu;
+  if (code == 0) return 0.0f;
+  const uint32_t sign = (code >> (f.E + f.M)) & 1u;
+  const int ef = (int)((code >> f.M) & ((1u << f.E) - 1u));
+  const int mf = (int)(code & ((1u << f.M) - 1u));
+  const int ae = ef == 0 ? 1 : ef;
+  const int mfull = ((ef != 0 ? 1 : 0) << f.M) | mf;
+  float v;
+  if (ae >= f.hs && ae <= f.hf) {
+    const int mpad = f.tp >= 0 ? lsh32(mfull, f.tp) : rrsh32(mfull, -f.tp);
+    const int mal = rrsh32(mpad, f.hf - ae);                 // hf - ae >= 0 here
+    v = __builtin_ldexpf((float)mal, (f.hf - f.bias) - f.M - f.tp);
+  } else {
+    // fp16 ops RN16(mant / 2^M) * RN16(2^e): exact for every format that passes fp_spec
+    v = __builtin_ldexpf((float)mfull, (ef == 0 ? 1 - f.bias : ef - f.bias) - f.M);
+  }
+  return sign ? -v : v;
+}
+
+// one element of quantize_weight_approximate (:470-632), single-aligned decode: symmetric absmax
+// codes exactly as the FP branch, then RN16(RN16(decode_aligned(code)) * scales)
+__device__ __forceinline__ float fp_apx_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+  float t = div16(w, p.s, p.rs, p.fast);
+  t = clamp_nan(t, -f.fp_max16, f.fp_max16);
+  code = fp_encode((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t), f);
+  const float y = f16r(f16r(fp_decode_aligned(code, f)) * p.s);
+  return t != t ? t : y;
+}
+
+// fp_decode_aligned_double_approx (quant_linear.py:288-363) on one quad of codes (4 consecutive
+// elements of the transposed grouped code matrix), int8 arithmetic; fp16 values out.
+__device__ __forceinline__ void fp_decode_double4(const uint32_t (&code)[4], const FpSpec& f, float (&out)[4]) {
+  int ae[4], mpad[4], sg[4];
+  bool zero[4];
+  int cnt = 0, gmax = -128;
+  bool has_max = false;
+  const int maxv = (1 << f.E) - 1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t c = code[k] & 0xFFu;
+    zero[k] = c == 0;
+    sg[k] = w8((int)((c >> (f.E + f.M)) & 1u));
+    const int ef = w8((int)((c >> f.M) & ((1u << f.E) - 1u)));
+    const int mf = w8((int)(c & ((1u << f.M) - 1u)));
+    ae[k] = ef == 0 ? 1 : ef;
+    const int mfull = w8(lsh8(ef == 0 ? 0 : 1, f.M) | mf);
+    mpad[k] = f.tp >= 0 ? lsh8(mfull, f.tp) : rrsh8(mfull, -f.tp);
+    const bool outl = ae[k] < f.hs || ae[k] > f.hf;
+    cnt += outl ? 1 : 0;
+    gmax = ae[k] > gmax ? ae[k] : gmax;
+    has_max |= outl && ae[k] == maxv;
+  }
+  int tgt = cnt <= 1 ? w8(f.hf) : gmax;
+  if (has_max) tgt = w8(maxv);
+  const int capr = ((1 << (f.M + 1)) - 1);
+  const int cap = w8(f.tp >= 0 ? (capr << f.tp) : (capr >> (-f.tp)));
+  const float scale_m = (float)(_Float16)__builtin_ldexpf(1.0f, -(f.M + f.tp));
+  const float p2 = (float)(_Float16)__builtin_ldexpf(1.0f, w8(tgt - f.bias));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int sh = w8(tgt - ae[k]);
+    const int shr = sh > 0 ? sh : 0;
+    const int nsh = w8(-sh);
+    const int shl = nsh > 0 ? nsh : 0;
+    const int mr = rrsh8(mpad[k], shr);
+    int ml = lsh8(mpad[k], shl);
+    ml = ml > cap ? cap : ml;
+    const int mal = sh >= 0 ? mr : ml;
+    float v = f16r(f16r((float)mal * scale_m) * p2);   // fp16 ops: mant / 2^(M+tail) * 2^(tgt-bias)
+    v = sg[k] == 1 ? -v : v;
+    out[k] = zero[k] ? 0.0f : v;
+  }
 }
 
 // fp4_quantize_cpu._fp_scale element (:37-44) with S = RN16(max(absmax, fp16(1e-8)) / 6)

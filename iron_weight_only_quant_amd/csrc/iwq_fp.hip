@@ -10,6 +10,10 @@
 //               lane, group min/max (or absmax) by DPP, ALU encode/decode per element.
 //   k_fp_apply  universal apply after iwq::seg's atomic key reduction (per-tensor, per-channel,
 //               quant_dim 1, odd shapes).
+//   CODEC_APX   quantize_weight_approximate (quant_linear.py:470-632), single-aligned decode: the
+//               same two kernels with the aligned decoder in the element step (one pass).
+//   k_apx_double  double-approximate decode (:288-363): codes + scales from a symmetric FP pass
+//               (into the workspace), then one thread per quad of codes (4 groups, same position).
 #include "iwq_common.cuh"
 #include "iwq_fp.cuh"
 #include "iwq_seg.cuh"
@@ -22,13 +26,11 @@ using iwq::seg::seg_locate;
 
 namespace {
 
-thread_local int g_last_hip_error_fp = 0;
-
 #define IWQ_HIP_FP(call)                \
   do {                                  \
     hipError_t e_ = (call);             \
     if (e_ != hipSuccess) {             \
-      g_last_hip_error_fp = (int)e_;    \
+      iwq::last_hip_error() = (int)e_;    \
       return IWQ_ERR_HIP;               \
     }                                   \
   } while (0)
@@ -37,7 +39,7 @@ constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
 constexpr int UNIT = WAVE * 8;
 
-enum : int { CODEC_FP = 0, CODEC_GRID = 1 };
+enum : int { CODEC_FP = 0, CODEC_GRID = 1, CODEC_APX = 2 };
 
 struct FpArgs {
   const char* w;
@@ -82,6 +84,8 @@ __device__ __forceinline__ float fp_elem(float w, const FpParams& p, const FpSpe
   if constexpr (CODEC == CODEC_GRID) {
     code = 0;
     return grid_elem(w, p.s, p.rs, p.fast);
+  } else if constexpr (CODEC == CODEC_APX) {
+    return fp_apx_elem(w, p, f, code);
   } else {
     return fp_quant_elem<SYM>(w, p, f, code);
   }
@@ -236,6 +240,7 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
 
 hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpArgs& a, hipStream_t st) {
   if (codec == CODEC_GRID) return launch_fp_group_g<CODEC_GRID, true, 0>(g, a, st);
+  if (codec == CODEC_APX) return launch_fp_group_g<CODEC_APX, true, 0>(g, a, st);
   if (sym) {
     if (codes == 0) return launch_fp_group_g<CODEC_FP, true, 0>(g, a, st);
     if (codes == 4) return launch_fp_group_g<CODEC_FP, true, 4>(g, a, st);
@@ -254,10 +259,11 @@ hipError_t launch_fp_seg(int codec, bool sym, const SegArgs& a, const FpSpec& f,
   int64_t blocks = (a.total + (int64_t)BLOCK * SEG_RUN - 1) / ((int64_t)BLOCK * SEG_RUN);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  const bool red_sym = sym || codec == CODEC_GRID;
+  const bool red_sym = sym || codec != CODEC_FP;
   if (red_sym) hipLaunchKernelGGL((iwq::seg::k_seg_reduce<DT_F16, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   else hipLaunchKernelGGL((iwq::seg::k_seg_reduce<DT_F16, false>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   if (codec == CODEC_GRID) hipLaunchKernelGGL((k_fp_apply<CODEC_GRID, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
+  else if (codec == CODEC_APX) hipLaunchKernelGGL((k_fp_apply<CODEC_APX, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
   else if (sym) hipLaunchKernelGGL((k_fp_apply<CODEC_FP, true>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
   else hipLaunchKernelGGL((k_fp_apply<CODEC_FP, false>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a, f);
   return hipGetLastError();
@@ -285,7 +291,7 @@ int fp_spec(int exp_bits, int mant_bits, FpSpec& f) {
 int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
            int mant_bits, int64_t group, int symmetric, int quant_dim, void* out, int64_t ld_out, void* codes_out,
            void* scales, void* zeros, void* ws, int64_t ws_bytes, uint32_t* nan_flag, unsigned flags,
-           void* stream) {
+           void* stream, int hs = 0, int hf = 0, int tp = 0) {
   if (dtype != IWQ_F16) return IWQ_ERR_DTYPE;
   if (!w) return IWQ_ERR_ARG;
   if (rows <= 0 || cols <= 0 || ld_w < cols || (out && ld_out < cols)) return IWQ_ERR_SHAPE;
@@ -293,6 +299,9 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
   FpSpec f{};
   int st = fp_spec(exp_bits, mant_bits, f);
   if (st != IWQ_OK) return st;
+  f.hs = hs;
+  f.hf = hf;
+  f.tp = tp;
   const int64_t vr = quant_dim == 1 ? cols : rows;
   const int64_t vc = quant_dim == 1 ? rows : cols;
   int64_t L, G;
@@ -311,11 +320,11 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
   }
   int codes = 0;
   if (codes_out) {
-    if (codec == CODEC_GRID) return IWQ_ERR_CODES;
+    if (codec != CODEC_FP) return IWQ_ERR_CODES;
     codes = (exp_bits + mant_bits + 1) <= 4 ? 4 : 8;
     if (codes == 4 && (cols & 1)) return IWQ_ERR_CODES;
   }
-  const bool sym = codec == CODEC_GRID ? true : symmetric != 0;
+  const bool sym = codec != CODEC_FP ? true : symmetric != 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool al = aligned16p(w) && (!out || aligned16p(out)) && (!codes_out || aligned16p(codes_out));
   if (!(flags & IWQ_FLAG_FORCE_GENERIC) && quant_dim == 0 && group >= 8 && group <= 512 &&
@@ -359,9 +368,126 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
   return IWQ_OK;
 }
 
+struct DoubleArgs {
+  const uint8_t* codes;  // weight layout [rows, cols]: bytes, or nibbles (low = even column)
+  const _Float16* scales;
+  _Float16* out;
+  int64_t rows, cols, ld_out;
+  int64_t g, G, gpr;     // group length, group count, groups per grouped row
+  int64_t nquads;
+  int code_bits, quant_dim;
+  FpSpec f;
+};
+
+// element (group j, position i) of the grouped matrix -> (r, c) of the weight
+__device__ __forceinline__ void apx_locate(const DoubleArgs& a, int64_t j, int64_t i, int64_t& r, int64_t& c) {
+  const int64_t jr = j / a.gpr, jg = j - jr * a.gpr;
+  if (a.quant_dim == 0) { r = jr; c = jg * a.g + i; }
+  else { c = jr; r = jg * a.g + i; }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_apx_double(DoubleArgs a) {
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  const bool fast = (a.G & 3) == 0;
+  for (int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x; t < a.nquads; t += nthreads) {
+    int64_t rr[4], cc[4], jj[4];
+    if (fast) {  // quad = 4 consecutive groups at one position; consecutive threads: consecutive positions
+      const int64_t jq = t / a.g, i = t - jq * a.g;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { jj[k] = 4 * jq + k; apx_locate(a, jj[k], i, rr[k], cc[k]); }
+    } else {     // flattened [g, G] order: element f = 4t + k at (i, j) = divmod(f, G)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t fi = 4 * t + k, i = fi / a.G;
+        jj[k] = fi - i * a.G;
+        apx_locate(a, jj[k], i, rr[k], cc[k]);
+      }
+    }
+    uint32_t code[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t e = rr[k] * a.cols + cc[k];
+      code[k] = a.code_bits == 8 ? (uint32_t)gp<uint8_t>(a.codes)[e]
+                                 : ((uint32_t)gp<uint8_t>(a.codes)[e >> 1] >> ((e & 1) * 4)) & 0xFu;
+    }
+    float v[4];
+    fp_decode_double4(code, a.f, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float s = (float)gp<_Float16>(a.scales)[jj[k]];
+      // RN16(decoded * scales); opaque keeps LLVM from fusing this into v_fma_mix with a +0 addend,
+      // which would turn (-0) * s into +0
+      gp<_Float16>(a.out)[rr[k] * a.ld_out + cc[k]] = (_Float16)opaque(v[k] * s);
+    }
+  }
+}
+
+int64_t round256(int64_t b) { return (b + 255) / 256 * 256; }
+
+int64_t apx_codes_bytes(int64_t rows, int64_t cols, int exp_bits, int mant_bits) {
+  return round256((1 + exp_bits + mant_bits) <= 4 ? rows * (cols / 2) : rows * cols);
+}
+
 }  // namespace
 
 extern "C" {
+
+int64_t iwq_approx_workspace_bytes(int64_t rows, int64_t cols, int exp_bits, int mant_bits, int64_t group,
+                                   int quant_dim, int double_approx) {
+  if (rows <= 0 || cols <= 0 || group <= 0) return 0;
+  const int64_t G = rows * cols / group;
+  (void)quant_dim;
+  return round256(8 * G) + (double_approx ? apx_codes_bytes(rows, cols, exp_bits, mant_bits) : 0);
+}
+
+int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                           int mant_bits, int64_t group, int quant_dim, int hi_align_start, int hi_align_exp_field,
+                           int tail_pad_bits, int double_approx, void* out_deq, int64_t ld_out, void* out_scales,
+                           void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                           void* stream) {
+  if (group <= 0) return IWQ_ERR_GROUP_MODE;  // approximate needs w_group_size > 0 (ValueError)
+  if (!out_deq || !out_scales) return IWQ_ERR_ARG;
+  if (!double_approx)
+    return run_fp(CODEC_APX, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
+                  nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, flags, stream, hi_align_start,
+                  hi_align_exp_field, tail_pad_bits);
+  if (rows <= 0 || cols <= 0 || ld_out < cols) return IWQ_ERR_SHAPE;
+  const int64_t vr = quant_dim == 1 ? cols : rows, vc = quant_dim == 1 ? rows : cols;
+  if (vc % group != 0) return IWQ_ERR_GROUP;
+  const int64_t G = vr * vc / group;
+  if ((G * group) % 4 != 0) return IWQ_ERR_SHAPE;  // quads of 4 (reference ValueError)
+  const int64_t cb = apx_codes_bytes(rows, cols, exp_bits, mant_bits);
+  if (!workspace || workspace_bytes < cb || !aligned16p(workspace)) return IWQ_ERR_WORKSPACE;
+  uint8_t* codes = static_cast<uint8_t*>(workspace);
+  int st = run_fp(CODEC_FP, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, nullptr, cols,
+                  codes, out_scales, nullptr, codes + cb, workspace_bytes - cb, nan_flag, flags, stream);
+  if (st != IWQ_OK) return st;
+  FpSpec f{};
+  fp_spec(exp_bits, mant_bits, f);
+  f.hs = hi_align_start;
+  f.hf = hi_align_exp_field;
+  f.tp = tail_pad_bits;
+  DoubleArgs a{};
+  a.codes = codes;
+  a.scales = static_cast<const _Float16*>(out_scales);
+  a.out = static_cast<_Float16*>(out_deq);
+  a.rows = rows;
+  a.cols = cols;
+  a.ld_out = ld_out;
+  a.g = group;
+  a.G = G;
+  a.gpr = vc / group;
+  a.nquads = G * group / 4;
+  a.code_bits = (1 + exp_bits + mant_bits) <= 4 ? 4 : 8;
+  a.quant_dim = quant_dim;
+  a.f = f;
+  int64_t blocks = (a.nquads + BLOCK - 1) / BLOCK;
+  const int64_t cap = (int64_t)cu_count() * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(k_apx_double, dim3((unsigned)blocks), dim3(BLOCK), 0, static_cast<hipStream_t>(stream), a);
+  IWQ_HIP_FP(hipGetLastError());
+  return IWQ_OK;
+}
 
 int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits, int mant_bits,
                     int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out, void* out_codes,

@@ -25,8 +25,6 @@ using namespace iwq;
 
 namespace {
 
-thread_local int g_last_hip_error_gemm = 0;
-
 constexpr int BM = 128, BN = 128, BK = 128, NTHR = 256;
 constexpr int LDS_TILE = BM * BK * 2;  // bytes of one X tile
 
@@ -481,7 +479,7 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
-    g_last_hip_error_gemm = (int)e;
+    iwq::last_hip_error() = (int)e;
     return IWQ_ERR_HIP;
   }
   return IWQ_OK;

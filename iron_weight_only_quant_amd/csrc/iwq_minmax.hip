@@ -29,15 +29,18 @@ using iwq::seg::seg_locate;
 using iwq::seg::k_seg_init;
 using iwq::seg::k_seg_reduce;
 
-namespace {
+int& iwq::last_hip_error() {
+  static thread_local int e = 0;
+  return e;
+}
 
-thread_local int g_last_hip_error = 0;
+namespace {
 
 #define IWQ_HIP(call)                                   \
   do {                                                  \
     hipError_t e_ = (call);                             \
     if (e_ != hipSuccess) {                             \
-      g_last_hip_error = (int)e_;                       \
+      iwq::last_hip_error() = (int)e_;                  \
       return IWQ_ERR_HIP;                               \
     }                                                   \
   } while (0)
@@ -865,6 +868,6 @@ const char* iwq_status_string(int status) {
   return "unknown status";
 }
 
-int iwq_last_hip_error(void) { return g_last_hip_error; }
+int iwq_last_hip_error(void) { return iwq::last_hip_error(); }
 
 }  // extern "C"

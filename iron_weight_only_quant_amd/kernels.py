@@ -134,6 +134,71 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     return QuantResult(out, scales, zeros, codes, nan_flag)
 
 
+def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, quant_dim: int = 0,
+                       hi_align_start: int = 12, hi_align_exp_field: int = 15, tail_pad_bits: int = 1,
+                       double_approx: bool = False, out: Optional[torch.Tensor] = None,
+                       flags: int = 0) -> QuantResult:
+    """QuantLinear.quantize_weight_approximate arithmetic (quant_linear.py:470-632) on an fp16 weight:
+    symmetric absmax FP codes, aligned / double-approximate decode, RN16(decoded * scale)."""
+    L.require_device(w)
+    if w.dim() != 2:
+        raise AssertionError("weight must be 2-D")
+    if w.dtype != torch.float16:
+        raise TypeError("approximate FP formats are implemented for fp16 weights")
+    if group <= 0:
+        raise ValueError("approximate 仅支持分组量化，w_group_size 必须 > 0")
+    lib = L.load()
+    if w.stride(1) != 1 or w.stride(0) < w.shape[1]:
+        w = w.contiguous()
+    rows, cols = w.shape
+    _, G = group_geometry(rows, cols, group, quant_dim)
+    if double_approx and (G * group) % 4 != 0:
+        raise ValueError("double approx requires total elements divisible by 4")
+    dev = w.device
+    if out is None:
+        out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
+    scales = torch.empty(G, dtype=w.dtype, device=dev)
+    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    wsb = int(lib.iwq_approx_workspace_bytes(rows, cols, int(exp_bits), int(mant_bits), int(group), int(quant_dim),
+                                             int(bool(double_approx))))
+    ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        st = lib.iwq_quantize_fp_approx(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
+                                        int(group), int(quant_dim), int(hi_align_start), int(hi_align_exp_field),
+                                        int(tail_pad_bits), int(bool(double_approx)), L.ptr(out), out.stride(0),
+                                        L.ptr(scales), L.ptr(ws), ws.numel(), L.ptr(nan_flag), int(flags),
+                                        L.stream_handle(dev))
+    _raise_for(st, "iwq_quantize_fp_approx")
+    return QuantResult(out, scales, None, None, nan_flag)
+
+
+def quantize_bfp(w: torch.Tensor, w_bit: int, group: int, quant_dim: int = 0, out: Optional[torch.Tensor] = None,
+                 flags: int = 0) -> torch.Tensor:
+    """BFP branch of QuantLinear.quantize_weight (quant_linear.py:648-723) on the GPU: shared group
+    exponent, min(w_bit-1, 11)-bit mantissas; returns the dequantized weight (out may be w)."""
+    L.require_device(w)
+    if w.dim() != 2:
+        raise AssertionError("weight must be 2-D")
+    if w.dtype not in L.DTYPE_CODE:
+        raise TypeError(f"unsupported dtype {w.dtype}")
+    if group <= 0:
+        raise ValueError("BFP 仅支持分组量化，请将 w_group_size 设为正数")
+    if w_bit < 1:
+        raise ValueError("negative shift count")
+    lib = L.load()
+    if w.stride(1) != 1 or w.stride(0) < w.shape[1]:
+        w = w.contiguous()
+    rows, cols = w.shape
+    group_geometry(rows, cols, group, quant_dim)
+    if out is None:
+        out = torch.empty((rows, cols), dtype=w.dtype, device=w.device)
+    with torch.cuda.device(w.device):
+        st = lib.iwq_quantize_bfp(L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(w_bit), int(group),
+                                  int(quant_dim), L.ptr(out), out.stride(0), int(flags), L.stream_handle(w.device))
+    _raise_for(st, "iwq_quantize_bfp")
+    return out
+
+
 def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int = 0) -> QuantResult:
     """fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 arithmetic on the GPU; output in w's element order."""
     L.require_device(w)

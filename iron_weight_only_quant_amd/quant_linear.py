@@ -14,8 +14,9 @@ Differences by design (documented in DESIGN.md):
   * `keep_codes=True` additionally keeps the packed integer codes (`qweight`, include/iwq.h layout)
     for the fused dequant->GEMM forward.
 FP4/FP6/FP8 (quant_linear.py:724-883) run the gfx950 FP codec (fp16 weights), with the formats set
-by the same module-level `configure_fp_formats` (:84-110).  The BFP and "approximate"/double-
-approximate research decodes (:470-723) are out of scope and raise NotImplementedError.
+by the same module-level `configure_fp_formats` (:84-110).  The research formats run on the GPU too:
+`approximate=True` (+ `double_approximate`) = quantize_weight_approximate (:470-632, fp16 weights)
+and weight_format "bfp" = the block-floating-point branch (:648-723, fp16/bf16/fp32 weights).
 """
 import torch
 import torch.nn as nn
@@ -125,10 +126,10 @@ class QuantLinear(nn.Module):
     def quantize_weight(self):
         """quant_linear.py:635-958 — INT branch on the GPU; in-place on self.weight."""
         with torch.no_grad():
-            if self.approximate or self.weight_format == "bfp":
-                raise NotImplementedError(
-                    f"weight_format={self.weight_format!r} approximate={self.approximate}: the BFP and "
-                    "approximate FIGLUT decode simulations are outside this build's hot path")
+            if self.approximate:
+                return self.quantize_weight_approximate()
+            if self.weight_format == "bfp":
+                return self._quantize_weight_bfp()
             if self.weight_format in ("fp4", "fp6", "fp8"):
                 return self._quantize_weight_fp()
             if self.w_bit >= 16:
@@ -152,6 +153,55 @@ class QuantLinear(nn.Module):
             self.weight_fp6 = None
             self.weight_fp8 = None
             self.quantized.fill_(True)
+
+    def quantize_weight_approximate(self):
+        """quant_linear.py:470-632 on the GPU: symmetric absmax FP codes per group of w_group_size,
+        decoded by the aligned (or, with double_approximate, the quad-wise double-approximate)
+        decoder; weight <- RN16(decoded * scales) in place, scales [G,1] fp16, zeros None."""
+        with torch.no_grad():
+            if self.w_group_size <= 0:
+                raise ValueError("approximate 仅支持分组量化，w_group_size 必须 > 0")
+            fmt = self.weight_format
+            if fmt not in ("fp4", "fp6", "fp8"):
+                raise NotImplementedError("approximate 目前仅支持 fp4/fp6/fp8")
+            e, m = _fp_bits(fmt)
+            hs, hf, tp = (getattr(self, f"{fmt}_hi_align_start"), getattr(self, f"{fmt}_hi_align_exp_field"),
+                          getattr(self, f"{fmt}_tail_pad_bits"))
+            if fmt == "fp4" and e not in (1, 2):
+                # the reference's fp4 branch only decodes E1 / E2 layouts; `decoded` stays unbound
+                raise UnboundLocalError("cannot access local variable 'decoded' where it is not associated "
+                                        "with a value")
+            double = bool(self.double_approximate) and not (fmt == "fp4" and e == 1)
+            w = self.weight.data
+            res = kernels.quantize_fp_approx(w, e, m, self.w_group_size, self.quant_dim, hs, hf, tp, double,
+                                             out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None)
+            if res.out is not w:
+                w.copy_(res.out)
+            self.scales = res.scales.view(-1, 1).half()
+            self.zeros = None
+            for other in ("fp4", "fp6", "fp8"):
+                if other != fmt:
+                    setattr(self, f"weight_{other}", None)
+            self.quantized.fill_(True)
+            self.approximate = True
+
+    def _quantize_weight_bfp(self):
+        """BFP branch (quant_linear.py:648-723) on the GPU, in place on self.weight."""
+        if self.w_group_size <= 0:
+            raise ValueError("BFP 仅支持分组量化，请将 w_group_size 设为正数")
+        w = self.weight.data
+        out = kernels.quantize_bfp(w, self.w_bit, self.w_group_size, self.quant_dim,
+                                   out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None)
+        if out is not w:
+            w.copy_(out)
+        self.weight_bfp_mantissa = None
+        self.weight_bfp_exponent = None
+        self.scales = None
+        self.zeros = None
+        self.weight_fp4 = None
+        self.weight_fp6 = None
+        self.weight_fp8 = None
+        self.quantized.fill_(True)
 
     def _quantize_weight_fp(self):
         """FP4/FP6/FP8 branches (quant_linear.py:724-883) on the GPU, in place on self.weight."""
