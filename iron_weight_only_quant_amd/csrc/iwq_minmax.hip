@@ -429,6 +429,85 @@ __global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
   flag_nan(a.nan_flag, any_nan);
 }
 
+
+// =============================================================================================
+// per-tensor (group -1; one group, so the element-wise apply is the same for quant_dim 0 and 1):
+//   k_tensor_reduce  persistent grid, 16-B loads, one (min, max) key pair per workgroup -> workspace
+//   k_tensor_apply   every workgroup folds the partials (<= a few thousand x 8 B, L2-resident),
+//                    derives the tensor's scale / zero point and quantizes its share
+// 6 B per fp16 element of HBM traffic (read, read, write) instead of the segmented path's scalar walk.
+// =============================================================================================
+template <int DT, bool SYM>
+__global__ __launch_bounds__(BLOCK) void k_tensor_reduce(const char* w, int64_t nunits, int32_t* partial) {
+  using F = Fmt<DT>;
+  constexpr int UN = 4;
+  __shared__ int32_t smn[WAVES_PER_BLOCK], smx[WAVES_PER_BLOCK];
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
+  for (int64_t u0 = (int64_t)blockIdx.x * BLOCK + threadIdx.x; u0 < nunits; u0 += nthreads * UN) {
+    Vec8<DT> v[UN];
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t u = u0 + k * nthreads;
+      v[k].load(w + (u < nunits ? u : 0) * 8 * F::BYTES);
+    }
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      if (u0 + k * nthreads < nunits) {
+        int32_t a, b;
+        minmax8<DT, SYM>(v[k], a, b);
+        mn = min(mn, a);
+        mx = max(mx, b);
+      }
+    }
+  }
+  group_minmax<64>(mn, mx);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < WAVES_PER_BLOCK; ++i) { mn = min(mn, smn[i]); mx = max(mx, smx[i]); }
+    partial[2 * blockIdx.x] = mn;
+    partial[2 * blockIdx.x + 1] = mx;
+  }
+}
+
+template <int DT, bool SYM, int CODES>
+__global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out, uint8_t* codes, void* scales,
+                                                        void* zeros, int64_t nunits, const int32_t* partial,
+                                                        int nparts, int n_bits, uint32_t* nan_flag) {
+  using F = Fmt<DT>;
+  __shared__ int32_t smn[WAVES_PER_BLOCK], smx[WAVES_PER_BLOCK];
+  int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
+  for (int i = threadIdx.x; i < nparts; i += BLOCK) {
+    mn = min(mn, partial[2 * i]);
+    mx = max(mx, partial[2 * i + 1]);
+  }
+  group_minmax<64>(mn, mx);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[wv] = mn; smx[wv] = mx; }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < WAVES_PER_BLOCK; ++i) { mn = min(mn, smn[i]); mx = max(mx, smx[i]); }
+  const GroupParams p = params_from_keys<DT, SYM>(mn, mx, n_bits, rmax_for(n_bits, SYM));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (scales) store_param<DT>(scales, 0, p.s);
+    if (!SYM && zeros) store_param<DT>(zeros, 0, p.z);
+  }
+  bool any_nan = false;
+  const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
+  for (int64_t u = (int64_t)blockIdx.x * BLOCK + threadIdx.x; u < nunits; u += nthreads) {
+    Vec8<DT> v, o;
+    v.load(w + u * 8 * F::BYTES);
+    uint32_t c[4];
+    any_nan |= quant8<DT, SYM>(v, p, n_bits, o, c);
+    if (out) o.store(out + u * 8 * F::BYTES);
+    if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+  }
+  flag_nan(nan_flag, any_nan);
+}
+
 template <int DT, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_seg_apply(SegArgs a) {
   using F = Fmt<DT>;
@@ -667,6 +746,46 @@ hipError_t launch_seg(int dt, bool sym, const SegArgs& a, hipStream_t st) {
   return sym ? launch_seg_t<DT_F32, true>(a, st) : launch_seg_t<DT_F32, false>(a, st);
 }
 
+
+constexpr int TENSOR_PARTS_MAX = 4096;
+
+template <int DT, bool SYM, int CODES>
+hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+  const int64_t nunits = numel / 8;
+  int64_t blocks = (int64_t)device_cu_count() * 8;
+  const int64_t need = (nunits + BLOCK - 1) / BLOCK;
+  if (blocks > need) blocks = need;
+  if (blocks > TENSOR_PARTS_MAX) blocks = TENSOR_PARTS_MAX;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_tensor_reduce<DT, SYM>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
+                     static_cast<const char*>(w), nunits, ws);
+  hipLaunchKernelGGL((k_tensor_apply<DT, SYM, CODES>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
+                     static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales,
+                     zeros, nunits, ws, (int)blocks, n_bits, nan_flag);
+  return hipGetLastError();
+}
+
+template <int DT, bool SYM>
+hipError_t launch_tensor_c(int codes, const void* w, void* out, void* cd, void* sc, void* zr, int64_t numel,
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+  if (codes == 0) return launch_tensor_t<DT, SYM, 0>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+  if (codes == 4) return launch_tensor_t<DT, SYM, 4>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+  return launch_tensor_t<DT, SYM, 8>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+}
+
+hipError_t launch_tensor(int dt, bool sym, int codes, const void* w, void* out, void* cd, void* sc, void* zr,
+                         int64_t numel, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+  if (dt == IWQ_F16)
+    return sym ? launch_tensor_c<DT_F16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
+               : launch_tensor_c<DT_F16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+  if (dt == IWQ_BF16)
+    return sym ? launch_tensor_c<DT_BF16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
+               : launch_tensor_c<DT_BF16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+  return sym ? launch_tensor_c<DT_F32, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
+             : launch_tensor_c<DT_F32, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+}
+
 int group_geometry(int64_t rows, int64_t cols, int64_t group, int quant_dim, int64_t& L, int64_t& G) {
   const int64_t vr = quant_dim == 1 ? cols : rows;
   const int64_t vc = quant_dim == 1 ? rows : cols;
@@ -697,6 +816,7 @@ int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant
   int64_t L = 0, G = 0;
   if (rows <= 0 || cols <= 0) return 0;
   if (group_geometry(rows, cols, group, quant_dim, L, G) != IWQ_OK) return 0;
+  if (group == IWQ_GROUP_PER_TENSOR) return (int64_t)TENSOR_PARTS_MAX * 8;  // per-workgroup partial keys
   return ((8 * G + 255) / 256) * 256;
 }
 
@@ -736,6 +856,14 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     a.n_bits = n_bits;
     a.nan_flag = nan_flag;
     IWQ_HIP(launch_group<false>(dtype, group, sym, codes, a, s));
+    return IWQ_OK;
+  }
+  if (!generic && group == IWQ_GROUP_PER_TENSOR && al && fastbits && ld_w == cols &&
+      (!out_deq || ld_out == cols) && (rows * cols) % 8 == 0) {
+    const int64_t need = iwq_workspace_bytes(rows, cols, group, quant_dim);
+    if (!workspace || workspace_bytes < need || !aligned16(workspace)) return IWQ_ERR_WORKSPACE;
+    IWQ_HIP(launch_tensor(dtype, sym, codes, w, out_deq, out_codes, out_scales, sym ? nullptr : out_zeros,
+                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s));
     return IWQ_OK;
   }
   if (!generic && quant_dim == 0 && group != IWQ_GROUP_PER_TENSOR && L % 8 == 0 && L <= ROW_MAX_L && al && fastbits) {

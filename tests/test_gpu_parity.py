@@ -476,3 +476,26 @@ def test_quantlinear_fused_forward(K):
     ref = torch.nn.functional.linear(x, q.weight, q.bias)
     assert y.shape == ref.shape
     torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_per_tensor_fast_path(K, dtype):
+    """group -1 (per-tensor) on a tensor big enough for many partial-key workgroups, quant_dim 0 and 1,
+    sym / asym, with codes: the two-kernel reduce + apply path vs the oracle, bit-exact."""
+    x = synth(55, (1536, 2048), dtype)
+    big = np.float32(-3.25)  # a single outlier decides the scale
+    x.reshape(-1)[123457] = O.f32_to_bf16_bits(big) if dtype == "bfloat16" else big
+    xd = to_dev(x, dtype)
+    for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
+        exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
+        for flags in FLAG_SETS:
+            r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
+            assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
+            assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)
+            codes = r.codes.cpu().numpy()
+            assert np.array_equal(codes.reshape(-1), O.pack_codes(exp.codes, bits).reshape(-1)), (bits, sym, qd, flags)
+    # NaN poisons the tensor's scale: every output NaN, flag raised
+    y = x.copy()
+    y.reshape(-1)[999] = np.nan if dtype != "bfloat16" else 0x7FC0
+    r = K.quantize_minmax(to_dev(y, dtype), 4, -1, False, 0)
+    assert r.has_nan()

@@ -1,0 +1,81 @@
+"""Throughput of every weight-format path on one Llama-2-7B gate_proj weight ([11008, 4096] fp16,
+resident in HBM): INT (pseudo_quantize_tensor / QuantLinear modes), FP8/FP6/FP4 (config 5), the E2M1
+grid, BFP and the approximate / double-approximate decodes.
+
+Prints one JSON line per path: weights GB/s (fp16 input bytes / time), algorithmic HBM bytes per call
+(read weight + write dequant + scales/zeros [+ codes]), achieved GB/s and the fraction of 8 TB/s.
+Timing: HIP events on the launching stream around R back-to-back calls, median of 5 rounds.
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8.0e12
+
+
+def timed(fn, reps, rounds=5):
+    st = torch.cuda.current_stream()
+    out = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) / reps * 1e-3)
+    out.sort()
+    return out[len(out) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=11008)
+    ap.add_argument("--cols", type=int, default=4096)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    from iron_weight_only_quant_amd import kernels as K
+    R, C = a.rows, a.cols
+    n = R * C
+    w = torch.empty(R, C, dtype=torch.float16, device="cuda")
+    K.fill_synthetic(w, 1)
+    out = torch.empty_like(w)
+    g = 128
+    G = n // g
+    cases = [
+        ("int4_g128_asym", lambda: K.quantize_minmax(w, 4, g, False, 0, out=out), 4 * n + 4 * G),
+        ("int4_g128_asym_codes", lambda: K.quantize_minmax(w, 4, g, False, 0, out=out, want_codes=True),
+         4 * n + 4 * G + n // 2),
+        ("int8_perchannel_asym", lambda: K.quantize_minmax(w, 8, -2, False, 0, out=out), 4 * n + 4 * R),
+        ("int4_g128_quant_dim1", lambda: K.quantize_minmax(w, 4, g, False, 1, out=out), 4 * n + 4 * G),
+        ("int4_per_tensor", lambda: K.quantize_minmax(w, 4, -1, False, 0, out=out), 4 * n + 4),
+        ("fp8_e4m3_g128_sym", lambda: K.quantize_fp(w, 4, 3, g, True, 0, out=out), 4 * n + 2 * G),
+        ("fp8_e4m3_g128_asym", lambda: K.quantize_fp(w, 4, 3, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp6_e3m2_g128_asym", lambda: K.quantize_fp(w, 3, 2, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp4_e2m1_g128_asym", lambda: K.quantize_fp(w, 2, 1, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp4_grid_g128", lambda: K.fp4_grid(w, g), 4 * n + 2 * G),
+        ("bfp_w4_g128", lambda: K.quantize_bfp(w, 4, g, out=out), 4 * n),
+        ("bfp_w8_g32", lambda: K.quantize_bfp(w, 8, 32, out=out), 4 * n),
+        ("approx_fp8_g128", lambda: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, False, out=out), 4 * n + 2 * G),
+        # double: FP pass writes codes (1 B), decode pass reads codes + scales, writes dequant
+        ("approx_fp8_g128_double", lambda: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, True, out=out),
+         2 * n + n + n + 2 * n + 2 * G + 2 * G),
+    ]
+    for name, fn, algo in cases:
+        fn()
+        torch.cuda.synchronize()
+        t = timed(fn, a.reps)
+        print(json.dumps({"path": name, "shape": [R, C], "ms": round(t * 1e3, 4),
+                          "weights_GBps": round(2 * n / t / 1e9, 1), "algo_bytes": int(algo),
+                          "achieved_GBps": round(algo / t / 1e9, 1), "frac_of_8TBps": round(algo / t / PEAK, 3)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

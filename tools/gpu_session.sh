@@ -45,6 +45,12 @@ if [[ $WHAT == *ppl* ]]; then
   step ppl_opt125m 600 python tools/ppl_delta.py --random opt-125m --synthetic_tokens 65536 --w_bits 8 4 --w_group_size -2
   step ppl_opt125m_g128 600 python tools/ppl_delta.py --random opt-125m --synthetic_tokens 65536 --w_bits 4 3 --w_group_size 128
 fi
+if [[ $WHAT == *formats* ]]; then
+  step bench_formats 600 python tools/bench_formats.py
+  cd /tmp
+  step prof_formats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_formats" -o run -- python3 "$ROOT/tools/bench_formats.py" --reps 10
+  cd "$ROOT"
+fi
 if [[ $WHAT == *ab* ]]; then
   step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
 fi
