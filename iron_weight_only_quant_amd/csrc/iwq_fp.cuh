@@ -24,10 +24,35 @@ struct FpSpec {
   float rmax;        // RN32(1/fp_max): corrected division when fp_max is an fp16 value
   int fpmax_is_f16;  // fp_max exactly representable in fp16
   int hs, hf, tp;    // approximate decodes: hi_align_start, hi_align_exp_field, tail_pad_bits
+  // fast-path constants (fp_roundtrip_fast), all formats that pass fp_spec have E <= 4
+  uint32_t sh;        // 10 - M: fp16 mantissa bits dropped
+  uint32_t rne_bias;  // 2^(sh-1) - 1
+  uint32_t mmax;      // 2^M - 1
+  uint32_t fpmax_bits, emin_bits;  // fp16 bits of fp_max and of 2^emin
+  float sub_c;        // 2^(23 + emin - M): (x + c) - c rounds x to the FP subnormal grid (RNE)
+  float sub_max;      // (2^M - 1) * 2^(emin - M): largest FP subnormal (no carry into the normals)
+  float sub_inv;      // 2^(M - emin)
 };
 
+// The log2 threshold tables live in LDS during a kernel (a per-lane index into __constant__ memory
+// would be one vector-memory load per element): kernels call stage_log2_tables() once.
+typedef __attribute__((address_space(3))) const uint16_t lds_u16;
+struct Log2Tabs {
+  lds_u16* up;  // kLog2UpThresh
+  lds_u16* p1;  // kLog2P1UpThresh
+};
+// all threads of the block must call it (contains a barrier); `buf` = a __shared__ uint16_t[80]
+__device__ __forceinline__ Log2Tabs stage_log2_tables(uint16_t* buf) {
+  if (threadIdx.x < 40) {
+    buf[threadIdx.x] = kLog2UpThresh[threadIdx.x];
+    buf[40 + threadIdx.x] = kLog2P1UpThresh[threadIdx.x];
+  }
+  __syncthreads();
+  return Log2Tabs{(lds_u16*)buf, (lds_u16*)buf + 40};
+}
+
 // floor(RN16(log2 x)) for a positive fp16 magnitude (bit pattern, 1..0x7BFF)
-__device__ __forceinline__ int fp16_floor_log2_torch(uint32_t mag, const uint16_t* thresh) {
+__device__ __forceinline__ int fp16_floor_log2_torch(uint32_t mag, lds_u16* thresh) {
   const int ef = (int)(mag >> 10);
   const int e_true = ef > 0 ? ef - 15 : (31 - __builtin_clz(mag)) - 24;
   return e_true + (mag >= (uint32_t)thresh[e_true + 24] ? 1 : 0);
@@ -35,11 +60,11 @@ __device__ __forceinline__ int fp16_floor_log2_torch(uint32_t mag, const uint16_
 
 // _float_to_fp on an fp16 value (bit pattern).  NaN inputs (only reachable when the group's scale
 // is NaN, where every output is NaN anyway) encode as 0.
-__device__ __forceinline__ uint32_t fp_encode(uint32_t b, const FpSpec& f) {
+__device__ __forceinline__ uint32_t fp_encode(uint32_t b, const FpSpec& f, const Log2Tabs& tb) {
   const uint32_t mag = b & 0x7FFFu;
   if (mag == 0 || mag > 0x7C00u) return 0;                // zero_mask (:132,:161); NaN
   const uint32_t sign = b >> 15;                          // x < 0 (:130)
-  const int e = fp16_floor_log2_torch(mag < 0x7C00u ? mag : 0x7BFFu, kLog2UpThresh);
+  const int e = fp16_floor_log2_torch(mag < 0x7C00u ? mag : 0x7BFFu, tb.up);
   const float xa = (float)__builtin_bit_cast(_Float16, (uint16_t)mag);
   const float ms = (float)(1u << f.M);
   uint32_t exp_field, mant;
@@ -67,6 +92,37 @@ __device__ __forceinline__ float fp_decode(uint32_t code, const FpSpec& f) {
   const float v = raw_exp == 0 ? __builtin_ldexpf((float)mant, f.emin - f.M)
                                : __builtin_ldexpf((float)((1 << f.M) + mant), raw_exp - f.bias - f.M);
   return sign ? -v : v;
+}
+
+// Fast path of _float_to_fp + _fp_to_float for a finite fp16 t already clamped to +-fp_max:
+// integer / fp32 bit work on t's fp16 pattern instead of the log2 / ldexp chain.  Returns the fp16
+// bits of the decoded value (exact in fp16 for E <= 4) and, with WANT_CODE, the code.
+//  normal FP range: RNE of the 10-bit fp16 mantissa to M bits, saturated at 2^M - 1 (no carry);
+//    the torch.log2 quirk (mantissa >= per-binade threshold -> exponent + 1) gives exactly
+//    2^(e+1) with mantissa 0 — the value a carry would give; capped at fp_max
+//  FP subnormal range (exponent < emin after the quirk): RNE of x to multiples of 2^(emin-M) by
+//    one fp32 add/sub pair, saturated below 2^emin
+template <bool WANT_CODE>
+__device__ __forceinline__ uint32_t fp_roundtrip_fast(uint32_t tb, float ta, const FpSpec& f, lds_u16* up_e16,
+                                                      uint32_t& code) {
+  const uint32_t u = tb & 0x7FFFu;
+  const uint32_t e16 = u >> 10;
+  const uint32_t fr = u & 0x3FFu;
+  uint32_t q = (fr + f.rne_bias + ((fr >> f.sh) & 1u)) >> f.sh;
+  q = q < f.mmax ? q : f.mmax;
+  uint32_t r = (e16 << 10) | (q << f.sh);
+  r = u >= (uint32_t)up_e16[e16] ? (e16 + 1u) << 10 : r;
+  r = r < f.fpmax_bits ? r : f.fpmax_bits;
+  float ys = opaque(ta + f.sub_c) - f.sub_c;
+  ys = ys < f.sub_max ? ys : f.sub_max;
+  const bool normal = r >= f.emin_bits;
+  const uint32_t mag = normal ? r : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)ys);
+  if constexpr (WANT_CODE) {
+    const uint32_t ef = normal ? (mag >> 10) - 15u + (uint32_t)f.bias : 0u;
+    const uint32_t m = normal ? (mag >> f.sh) & f.mmax : (uint32_t)(ys * f.sub_inv);
+    code = u == 0 ? 0u : ((((tb >> 15) & 1u) << (f.E + f.M)) | (ef << f.M) | m);
+  }
+  return u == 0 ? 0u : (mag | (tb & 0x8000u));
 }
 
 struct FpParams {
@@ -117,14 +173,24 @@ __device__ __forceinline__ FpParams fp_params_asym(float mn, float mx, const FpS
 }
 
 // one element of the FP branches: returns the dequantized value (fp32 holding an fp16 value)
-template <bool SYM>
-__device__ __forceinline__ float fp_quant_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+template <bool SYM, bool WANT_CODE = true>
+__device__ __forceinline__ float fp_quant_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code,
+                                               const Log2Tabs& tabs) {
+  if (p.fast) {  // finite group: corrected division, med3 clamp, bit-level codec, native fp16 mul/add
+    const float q = SYM ? div_f16vals(w, p.s, p.rs) : div_f16vals(f16r(w - p.z), p.s, p.rs);
+    const float t = __builtin_amdgcn_fmed3f((float)(_Float16)q, -f.fp_max16, f.fp_max16);
+    const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
+    const uint32_t d = fp_roundtrip_fast<WANT_CODE>(tb, __builtin_fabsf(t), f, tabs.up + 9, code);
+    _Float16 y = __builtin_bit_cast(_Float16, (uint16_t)d) * (_Float16)p.s;  // RN16(exact product)
+    if constexpr (!SYM) y = y + (_Float16)p.z;   // RN16(exact sum) == RN16(RN32(sum)) (24 >= 2*11+2)
+    return (float)y;
+  }
   float t;
   if constexpr (SYM) t = div16(w, p.s, p.rs, p.fast);                    // W / scales
   else t = div16(f16r(w - p.z), p.s, p.rs, p.fast);                      // (W - zeros) / scales
   t = clamp_nan(t, -f.fp_max16, f.fp_max16);                             // clamp(-fp_max, fp_max)
   const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
-  code = fp_encode(tb, f);
+  code = fp_encode(tb, f, tabs);
   float y = f16r(f16r(fp_decode(code, f)) * p.s);                        // .to(fp16) * scales
   if constexpr (!SYM) y = f16r(y + p.z);                                  // + zeros
   if (t != t) y = t;                                                      // NaN scale: NaN out
@@ -171,10 +237,13 @@ __device__ __forceinline__ float fp_decode_aligned(uint32_t code, const FpSpec& 
 
 // one element of quantize_weight_approximate (:470-632), single-aligned decode: symmetric absmax
 // codes exactly as the FP branch, then RN16(RN16(decode_aligned(code)) * scales)
-__device__ __forceinline__ float fp_apx_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+__device__ __forceinline__ float fp_apx_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code,
+                                             const Log2Tabs& tabs) {
   float t = div16(w, p.s, p.rs, p.fast);
   t = clamp_nan(t, -f.fp_max16, f.fp_max16);
-  code = fp_encode((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t), f);
+  const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
+  if (p.fast) fp_roundtrip_fast<true>(tb, __builtin_fabsf(t), f, tabs.up + 9, code);
+  else code = fp_encode(tb, f, tabs);
   const float y = f16r(f16r(fp_decode_aligned(code, f)) * p.s);
   return t != t ? t : y;
 }
@@ -225,13 +294,13 @@ __device__ __forceinline__ void fp_decode_double4(const uint32_t (&code)[4], con
 }
 
 // fp4_quantize_cpu._fp_scale element (:37-44) with S = RN16(max(absmax, fp16(1e-8)) / 6)
-__device__ __forceinline__ float grid_elem(float x, float S, float rS, bool fast) {
+__device__ __forceinline__ float grid_elem(float x, float S, float rS, bool fast, const Log2Tabs& tabs) {
   float u = (fast && S > 0.0f) ? (float)(_Float16)div_f16vals(x, S, rS) : f16r(x / S);
   u = clamp_nan(u, -6.0f, 6.0f);
   if (u != u) return u;
   const uint32_t mag = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)u) & 0x7FFFu;
   // ls = clamp(floor(log2|u| + 1), 1): |u| == 0 -> -inf -> 1
-  int ls = mag == 0 ? 1 : fp16_floor_log2_torch(mag, kLog2P1UpThresh) + 1;
+  int ls = mag == 0 ? 1 : fp16_floor_log2_torch(mag, tabs.p1) + 1;
   ls = ls < 1 ? 1 : ls;
   const float sc = __builtin_ldexpf(1.0f, ls - 2);                        // 2^(ls - M - bias)
   const float q = __builtin_rintf(u / sc) * sc;                           // exact (power-of-two scale)

@@ -79,15 +79,16 @@ __device__ __forceinline__ FpParams fp_group_params(int32_t mn, int32_t mx, cons
   }
 }
 
-template <int CODEC, bool SYM>
-__device__ __forceinline__ float fp_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code) {
+template <int CODEC, bool SYM, bool WANT_CODE = true>
+__device__ __forceinline__ float fp_elem(float w, const FpParams& p, const FpSpec& f, uint32_t& code,
+                                         const Log2Tabs& tabs) {
   if constexpr (CODEC == CODEC_GRID) {
     code = 0;
-    return grid_elem(w, p.s, p.rs, p.fast);
+    return grid_elem(w, p.s, p.rs, p.fast, tabs);
   } else if constexpr (CODEC == CODEC_APX) {
-    return fp_apx_elem(w, p, f, code);
+    return fp_apx_elem(w, p, f, code, tabs);
   } else {
-    return fp_quant_elem<SYM>(w, p, f, code);
+    return fp_quant_elem<SYM, WANT_CODE>(w, p, f, code, tabs);
   }
 }
 
@@ -111,6 +112,8 @@ __device__ __forceinline__ void store_fp_codes8(uint8_t* base, int64_t elem0, co
 template <int CODEC, int G, bool SYM, int CODES>
 __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
   using F = Fmt<DT_F16>;
+  __shared__ uint16_t tab_buf[80];
+  const Log2Tabs tabs = stage_log2_tables(tab_buf);
   constexpr int UNROLL = 4;
   constexpr int LPG = G / 8;
   const int lane = threadIdx.x & 63;
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
       bool nan8 = false;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float y = fp_elem<CODEC, SYM>(F::to_f(v[k].get(i)), p, a.f, c[i]);
+        const float y = fp_elem<CODEC, SYM, CODES != 0>(F::to_f(v[k].get(i)), p, a.f, c[i], tabs);
         nan8 |= (y != y);
         o.set(i, F::from_f(y));
       }
@@ -165,6 +168,8 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
 template <int CODEC, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
   using F = Fmt<DT_F16>;
+  __shared__ uint16_t tab_buf[80];
+  const Log2Tabs tabs = stage_log2_tables(tab_buf);
   const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
   const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   int64_t curj = -1;
@@ -185,7 +190,7 @@ __global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
       int64_t ow, oo, r, c;
       seg_locate(a, fi, ow, oo, r, c);
       uint32_t code;
-      const float y = fp_elem<CODEC, SYM>(F::to_f(gp<uint16_t>(a.w)[ow]), p, f, code);
+      const float y = fp_elem<CODEC, SYM>(F::to_f(gp<uint16_t>(a.w)[ow]), p, f, code, tabs);
       any_nan |= (y != y);
       if (a.out) gp<uint16_t>(a.out)[oo] = (uint16_t)F::from_f(y);
       if (a.codes_bits) {
@@ -285,6 +290,14 @@ int fp_spec(int exp_bits, int mant_bits, FpSpec& f) {
   f.fp_max16 = r16;
   f.fpmax_is_f16 = r16 == f.fp_max ? 1 : 0;
   f.rmax = 1.0f / f.fp_max;
+  f.sh = (uint32_t)(10 - mant_bits);
+  f.rne_bias = (1u << (f.sh - 1)) - 1u;
+  f.mmax = (1u << mant_bits) - 1u;
+  f.fpmax_bits = ((uint32_t)(f.emax + 15) << 10) | (f.mmax << f.sh);
+  f.emin_bits = (uint32_t)(f.emin + 15) << 10;
+  f.sub_c = __builtin_ldexpf(1.0f, 23 + f.emin - mant_bits);
+  f.sub_max = __builtin_ldexpf((float)f.mmax, f.emin - mant_bits);
+  f.sub_inv = __builtin_ldexpf(1.0f, mant_bits - f.emin);
   return IWQ_OK;
 }
 
