@@ -430,6 +430,92 @@ __global__ __launch_bounds__(TX * TY) void k_column(ColArgs a) {
 }
 
 
+// k_column_reg: k_column for g = RPT * TY rows per group (g in {32, 64, 128, 256}): every thread
+// issues the loads of its RPT rows once, keeps them in registers across the reduction, and the
+// block's per-column (min, max) is folded by 64 threads instead of every thread re-reading all
+// TY partials (one pass over HBM, no second read of the tile).
+template <int DT, bool SYM, int CODES, int TX, int TY, int RPT>
+__global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
+  using F = Fmt<DT>;
+  constexpr int NC = TX * 8;  // columns per block
+  __shared__ int32_t s_mn[TY][NC];
+  __shared__ int32_t s_mx[TY][NC];
+  __shared__ int32_t f_mn[NC], f_mx[NC];
+  const int tx = threadIdx.x % TX;
+  const int ty = threadIdx.x / TX;
+  const int64_t c0 = ((int64_t)blockIdx.x * TX + tx) * 8;
+  const int64_t jr = blockIdx.y;
+  const int64_t r0 = jr * a.g;
+  const bool cvalid = c0 < a.cols;
+  const int64_t cl = cvalid ? c0 : 0;  // unconditional loads (clamped column)
+  Vec8<DT> v[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) v[k].load(a.w + ((r0 + ty + k * TY) * a.ld_w + cl) * F::BYTES);
+  int32_t mn[8], mx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mn[i] = 0x7FFFFFFF; mx[i] = (int32_t)0x80000000; }
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (SYM) {
+        mx[i] = max(mx[i], mag_key<DT>(v[k].get(i)));
+      } else {
+        const int32_t kk = key_of<DT>(v[k].get(i));
+        mn[i] = min(mn[i], kk);
+        mx[i] = max(mx[i], kk);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s_mn[ty][tx * 8 + i] = mn[i]; s_mx[ty][tx * 8 + i] = mx[i]; }
+  __syncthreads();
+  if (threadIdx.x < NC) {
+    int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
+#pragma unroll 8
+    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][threadIdx.x]); a_mx = max(a_mx, s_mx[y][threadIdx.x]); }
+    f_mn[threadIdx.x] = a_mn;
+    f_mx[threadIdx.x] = a_mx;
+  }
+  __syncthreads();
+  const float rmax = rmax_for(a.n_bits, SYM);
+  GroupParams p[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p[i] = params_from_keys<DT, SYM>(f_mn[tx * 8 + i], f_mx[tx * 8 + i], a.n_bits, rmax);
+  bool any_nan = false;
+  if (cvalid) {
+    if (ty == 0) {
+      const int64_t ng = a.rows / a.g;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t gidx = (c0 + i) * ng + jr;
+        if (a.scales) store_param<DT>(a.scales, gidx, p[i].s);
+        if (!SYM && a.zeros) store_param<DT>(a.zeros, gidx, p[i].z);
+      }
+    }
+    const uint32_t off = SYM ? (1u << (a.n_bits - 1)) : 0u;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int64_t r = r0 + ty + k * TY;
+      Vec8<DT> o;
+      uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float cf, y;
+        y = quant_exact_or_fast<DT, SYM>(F::to_f(v[k].get(i)), p[i], cf);
+        any_nan |= (y != y);
+        o.set(i, F::from_f(y));
+        const uint32_t cc = (cf == cf) ? ((uint32_t)(int32_t)cf + off) & 0xFFFFu : 0u;
+        c[i >> 1] |= (i & 1) ? (cc << 16) : cc;
+      }
+      if (a.out) o.store(a.out + (r * a.ld_out + c0) * F::BYTES);
+      if constexpr (CODES != 0) store_codes8<CODES>(a.codes, r * a.cols + c0, c);
+    }
+  }
+  flag_nan(a.nan_flag, any_nan);
+}
+
+
 // =============================================================================================
 // per-tensor (group -1; one group, so the element-wise apply is the same for quant_dim 0 and 1):
 //   k_tensor_reduce  persistent grid, 16-B loads, one (min, max) key pair per workgroup -> workspace
@@ -712,7 +798,13 @@ template <int DT, bool SYM, int CODES>
 hipError_t launch_col_t(const ColArgs& a, hipStream_t st) {
   constexpr int TX = 8, TY = 32;
   dim3 grid((unsigned)((a.cols + 8 * TX - 1) / (8 * TX)), (unsigned)(a.rows / a.g));
-  hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, dim3(TX * TY), 0, st, a);
+  switch (a.g) {
+    case 32: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 1>), grid, dim3(TX * TY), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 2>), grid, dim3(TX * TY), 0, st, a); break;
+    case 128: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 4>), grid, dim3(TX * TY), 0, st, a); break;
+    case 256: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 8>), grid, dim3(TX * TY), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, dim3(TX * TY), 0, st, a); break;
+  }
   return hipGetLastError();
 }
 template <int DT, bool SYM>

@@ -499,3 +499,22 @@ def test_per_tensor_fast_path(K, dtype):
     y.reshape(-1)[999] = np.nan if dtype != "bfloat16" else 0x7FC0
     r = K.quantize_minmax(to_dev(y, dtype), 4, -1, False, 0)
     assert r.has_nan()
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_quant_dim1_register_kernel(K, dtype):
+    """quant_dim 1 with groups of 32/64/128/256 rows (the register-resident column kernel; cols not a
+    multiple of the 64-column block) vs the oracle, bit-exact incl. codes, scales and zero points."""
+    x = synth(61, (512, 328), dtype)
+    xd = to_dev(x, dtype)
+    for g in (32, 64, 128, 256):
+        for bits, sym in ((4, False), (8, True), (3, False)):
+            exp = O.quantlinear_int(x, bits, g, sym, 1, dtype)
+            for flags in FLAG_SETS:
+                r = K.quantize_minmax(xd, bits, g, sym, 1, want_codes=True, flags=flags)
+                assert bits_equal(to_np(r.out), exp.dequant), (g, bits, sym, flags)
+                assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (g, bits, sym, flags)
+                if not sym:
+                    assert bits_equal(to_np(r.zeros), exp.zeros.reshape(-1)), (g, bits, flags)
+                assert np.array_equal(r.codes.cpu().numpy().reshape(-1),
+                                      O.pack_codes(exp.codes, bits).reshape(-1)), (g, bits, sym, flags)
