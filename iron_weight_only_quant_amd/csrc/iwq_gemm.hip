@@ -418,6 +418,139 @@ void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_big: prefill (large M), per-channel scales.  256x256 output tile per 512-thread
+// workgroup (8 waves as 2 (M) x 4 (N), 128x64 per wave = 8x4 MFMA tiles), K in steps of 64.
+// Both operands are staged by LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring
+// (X 32 KiB + codes 8 KiB per stage): tile t+2 is in flight while tile t is computed, with ONE
+// raw s_barrier per K-step and a counted `s_waitcnt vmcnt(5)` (5 DMA instructions per thread per
+// stage), never a full drain inside the loop.  The DMA writes lane-linearly, so the X image is
+// XOR-swizzled through the SOURCE addresses (16-B chunk c of row r lands at chunk c ^ ((r>>1)&7):
+// conflict-free ds_read_b128 of A fragments).  k runs in natural order on both operands: lane
+// group q of k-slice s holds k = 16q + 8s + [0, 8), i.e. one 8-byte codes read per 16-column
+// subtile per K-step, dequantized in registers by v_perm + and-or (1024+q / 64+q magic), one exact
+// subtraction of the zero point and one rounding multiply by the scale (= the fake-quant weight).
+// ---------------------------------------------------------------------------------------------
+constexpr int BG_M = 256, BG_N = 256, BG_K = 64, BG_THR = 512;
+constexpr int BG_XS = BG_M * BG_K * 2;   // 32 KiB of X per stage
+constexpr int BG_CS = BG_N * BG_K / 2;   // 8 KiB of codes per stage
+constexpr int BG_STAGE = BG_XS + BG_CS;
+constexpr int BG_NSTAGE = 3;
+
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+// 8 codes (nibble p of w = k offset p) -> 8 fp16 RN16((q - z) * s) in natural k order.
+// zz = (1024 + z, 64 + z): even k come out as 1024 + q (low nibble, 0x6400), odd k as 64 + q
+// (high nibble at mantissa bits 4..7, 0x5400).
+__device__ __forceinline__ h8 dequant8_nat(uint32_t w, h2 zz, h2 s) {
+  const h2 d0 = (as_h2((perm(w, w, 0x0C000C00u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
+  const h2 d1 = (as_h2((perm(w, w, 0x0C010C01u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
+  const h2 d2 = (as_h2((perm(w, w, 0x0C020C02u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
+  const h2 d3 = (as_h2((perm(w, w, 0x0C030C03u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
+  return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
+}
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[BG_NSTAGE * BG_STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int tiles_n = a.N / BG_N;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * BG_M, n0 = (int)(t % tiles_n) * BG_N;
+  const int nk = a.K / BG_K;
+  const int64_t crow = a.K / 2;
+
+  // DMA sources: X instruction i of this wave fills rows (wid*4 + i)*8 + lane/8, chunk lane%8
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;   // rows past M: any valid row (discarded)
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    xsrc[i] = a.x + (int64_t)gm * a.lda + c * 8;
+  }
+  // codes: this wave fills columns wid*32 + lane/2, half lane%2 of their 32 bytes
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + wid * 32 + (lane >> 1)) * crow + (lane & 1) * 16;
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * BG_STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * BG_K, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (BG_K / 2), base + BG_XS + wid * 1024);
+  };
+
+  // per-channel scale / zero point of this lane's column in each 16-wide subtile
+  h2 sv[4], zz[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wn * 64 + nt * 16 + r16;
+    const _Float16 sc = gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    sv[nt] = h2{sc, sc};
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
+  }
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMA of tile kt retired (tile kt+1's 5 may stay in flight); the barrier makes every
+    // wave's part visible and proves every wave is done reading the stage about to be refilled
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % BG_NSTAGE);
+    const uint8_t* xs = smem + (kt % BG_NSTAGE) * BG_STAGE;
+    const uint8_t* cs = xs + BG_XS;
+    h8 bf[4][2];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const u32x2v w2 = *reinterpret_cast<const u32x2v*>(cs + (wn * 64 + nt * 16 + r16) * 32 + 8 * q);
+      bf[nt][0] = dequant8_nat(w2.x, zz[nt], sv[nt]);
+      bf[nt][1] = dequant8_nat(w2.y, zz[nt], sv[nt]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int row = wm * 128 + mt * 16 + r16;
+      const int sw = (row >> 1) & 7;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const h8 af = *reinterpret_cast<const h8*>(xs + row * 128 + (((2 * q + s2) ^ sw) << 4));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[nt][s2], acc[mt][nt], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: C layout col = lane & 15, row = 4 * (lane >> 4) + reg
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wn * 64 + nt * 16 + r16;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 128 + mt * 16 + 4 * q + r;
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(acc[mt][nt][r] + b);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -473,6 +606,10 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 13: launch_gemv<2, 16, 1>(a, st, true); break;
       default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
     }
+  } else if (a.gpr == 1 && N % BG_N == 0 && K % BG_K == 0 && M >= 512 && variant != 1 &&
+             !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+    const int64_t blocks = ((M + BG_M - 1) / BG_M) * (N / BG_N);
+    hipLaunchKernelGGL(k_w4a16_big, dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
   } else {
     const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, st, a);

@@ -518,3 +518,34 @@ def test_quant_dim1_register_kernel(K, dtype):
                     assert bits_equal(to_np(r.zeros), exp.zeros.reshape(-1)), (g, bits, flags)
                 assert np.array_equal(r.codes.cpu().numpy().reshape(-1),
                                       O.pack_codes(exp.codes, bits).reshape(-1)), (g, bits, sym, flags)
+
+
+@pytest.mark.parametrize("M", [512, 600, 1024])
+@pytest.mark.parametrize("sym", [False, True])
+def test_w4a16_prefill_big_tile(K, M, sym):
+    """The 256x256 LDS-DMA prefill kernel (per-channel, N % 256 == 0, M >= 512): vs an fp32 GEMM on the
+    bit-exact dequantized weight, and against the 128x128 kernel (variant 1)."""
+    N, Kd = 512, 4352
+    torch.manual_seed(1)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 91)
+    r = K.quantize_minmax(w, 4, -2, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b)
+    err = (y.float() - ref).abs()
+    assert bool((err <= tol).all()), float(err.max())
+    y1 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(1))
+    assert float((y.float() - y1.float()).abs().max()) <= 2 * float(err.max()) + 2e-3
+
+
+def test_w4a16_prefill_big_identity(K):
+    """A = I (512x512) through the big-tile kernel: picks W_deq^T exactly (layout / swizzle check)."""
+    N, Kd = 512, 512
+    w = (torch.arange(N * Kd, device=DEV, dtype=torch.float32).reshape(N, Kd) % 13 - 6).half()
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = torch.eye(Kd, device=DEV, dtype=torch.float16)
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
+    assert torch.equal(y, r.out.t().contiguous())
