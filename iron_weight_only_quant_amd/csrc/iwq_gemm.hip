@@ -431,22 +431,46 @@ void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
 // subtile per K-step, dequantized in registers by v_perm + and-or (1024+q / 64+q magic), one exact
 // subtraction of the zero point and one rounding multiply by the scale (= the fake-quant weight).
 // ---------------------------------------------------------------------------------------------
-constexpr int BG_M = 256, BG_N = 256, BG_K = 64, BG_THR = 512;
-constexpr int BG_XS = BG_M * BG_K * 2;   // 32 KiB of X per stage
-constexpr int BG_CS = BG_N * BG_K / 2;   // 8 KiB of codes per stage
-constexpr int BG_STAGE = BG_XS + BG_CS;
-constexpr int BG_NSTAGE = 3;
+constexpr int BG_M = 256, BG_N = 256, BG_THR = 512;
+
+template <int BK>
+struct BigCfg {
+  static constexpr int XS = BG_M * BK * 2;                 // X bytes per stage
+  static constexpr int CS = BG_N * BK / 2;                 // codes bytes per stage
+  static constexpr int STAGE = XS + CS;
+  static constexpr int NSTAGE = BK == 64 ? 3 : 2;          // 120 KiB / 160 KiB of LDS
+  static constexpr int XI = BK / 16;                       // X DMA instructions per thread per stage
+  static constexpr int CI = BK / 64;                       // codes DMA instructions per thread per stage
+  static constexpr int XROWS = 512 / BK;                   // rows per 1-KiB DMA instruction
+  static constexpr int XCH = BK / 8;                       // 16-B chunks per X row
+  static constexpr int CCOLS = 2048 / BK;                  // columns per 1-KiB codes DMA instruction
+  static constexpr int CCH = BK / 32;                      // 16-B chunks per codes column
+  static constexpr int KS = BK / 32;                       // MFMA k-slices per stage
+  // X: chunk c of row r sits at chunk c ^ xswz(r); 16 lanes reading 16 consecutive rows at one
+  // logical chunk hit 16 distinct 16-B slots of the 256-B bank row
+  __device__ static int xswz(int r) { return BK == 64 ? ((r >> 1) & 7) : (r & 15); }
+  // codes: chunk c of column n sits at c ^ cswz(n) (BK=128: 16 columns x 4 chunks -> distinct slots)
+  __device__ static int cswz(int n) { return BK == 64 ? 0 : ((n >> 2) & 3); }
+};
 
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+// one v_and_or_b32 (gfx9 VOP3 takes no literal, so the compiler would otherwise split it into a
+// VOP2 and + or): mask in an SGPR, magic in a VGPR
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
+  return r;
+}
 
 // 8 codes (nibble p of w = k offset p) -> 8 fp16 RN16((q - z) * s) in natural k order.
 // zz = (1024 + z, 64 + z): even k come out as 1024 + q (low nibble, 0x6400), odd k as 64 + q
 // (high nibble at mantissa bits 4..7, 0x5400).
-__device__ __forceinline__ h8 dequant8_nat(uint32_t w, h2 zz, h2 s) {
-  const h2 d0 = (as_h2((perm(w, w, 0x0C000C00u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
-  const h2 d1 = (as_h2((perm(w, w, 0x0C010C01u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
-  const h2 d2 = (as_h2((perm(w, w, 0x0C020C02u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
-  const h2 d3 = (as_h2((perm(w, w, 0x0C030C03u) & 0x00F0000Fu) | 0x54006400u) - zz) * s;
+__device__ __forceinline__ h8 dequant8_nat(uint32_t w, h2 zz, h2 s, uint32_t mask_s, uint32_t magic_v) {
+  const h2 d0 = (as_h2(and_or(perm(w, w, 0x0C000C00u), mask_s, magic_v)) - zz) * s;
+  const h2 d1 = (as_h2(and_or(perm(w, w, 0x0C010C01u), mask_s, magic_v)) - zz) * s;
+  const h2 d2 = (as_h2(and_or(perm(w, w, 0x0C020C02u), mask_s, magic_v)) - zz) * s;
+  const h2 d3 = (as_h2(and_or(perm(w, w, 0x0C030C03u), mask_s, magic_v)) - zz) * s;
   return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
 }
 
@@ -455,8 +479,10 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+template <int BK>
 __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[BG_NSTAGE * BG_STAGE];
+  using C = BigCfg<BK>;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[C::NSTAGE * C::STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -465,25 +491,31 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
   const int tiles_n = a.N / BG_N;
   const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
   const int m0 = (int)(t / tiles_n) * BG_M, n0 = (int)(t % tiles_n) * BG_N;
-  const int nk = a.K / BG_K;
+  const int nk = a.K / BK;
   const int64_t crow = a.K / 2;
 
-  // DMA sources: X instruction i of this wave fills rows (wid*4 + i)*8 + lane/8, chunk lane%8
-  const _Float16* xsrc[4];
+  // DMA sources (per lane); destinations are wave-uniform 1-KiB slots, filled lane-linearly
+  const _Float16* xsrc[C::XI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+  for (int i = 0; i < C::XI; ++i) {
+    const int row = (wid * C::XI + i) * C::XROWS + lane / C::XCH;
     const int gm = m0 + row < a.M ? m0 + row : a.M - 1;   // rows past M: any valid row (discarded)
-    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int c = (lane % C::XCH) ^ C::xswz(row);
     xsrc[i] = a.x + (int64_t)gm * a.lda + c * 8;
   }
-  // codes: this wave fills columns wid*32 + lane/2, half lane%2 of their 32 bytes
-  const uint8_t* csrc = a.codes + (int64_t)(n0 + wid * 32 + (lane >> 1)) * crow + (lane & 1) * 16;
-  auto issue = [&](int kt, int stg) {
-    uint8_t* base = smem + stg * BG_STAGE;
+  const uint8_t* csrc[C::CI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * BG_K, base + (wid * 4 + i) * 1024);
-    glds16(csrc + kt * (BG_K / 2), base + BG_XS + wid * 1024);
+  for (int j = 0; j < C::CI; ++j) {
+    const int col = (wid * C::CI + j) * C::CCOLS + lane / C::CCH;
+    const int c = (lane % C::CCH) ^ C::cswz(col);
+    csrc[j] = a.codes + (int64_t)(n0 + col) * crow + c * 16;
+  }
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::XI; ++i) glds16(xsrc[i] + kt * BK, base + (wid * C::XI + i) * 1024);
+#pragma unroll
+    for (int j = 0; j < C::CI; ++j) glds16(csrc[j] + kt * (BK / 2), base + C::XS + (wid * C::CI + j) * 1024);
   };
 
   // per-channel scale / zero point of this lane's column in each 16-wide subtile
@@ -496,6 +528,9 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
     sv[nt] = h2{sc, sc};
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
   }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
 
   f4 acc[8][4];
 #pragma unroll
@@ -504,30 +539,46 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
 
   issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  if constexpr (C::NSTAGE == 3) {
+    if (nk > 1) issue(1, 1);
+  }
   for (int kt = 0; kt < nk; ++kt) {
-    // own DMA of tile kt retired (tile kt+1's 5 may stay in flight); the barrier makes every
-    // wave's part visible and proves every wave is done reading the stage about to be refilled
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // own DMA of tile kt retired (with 3 stages tile kt+1's may stay in flight); the barrier makes
+    // every wave's part visible and proves every wave is done reading the stage about to be refilled
+    if constexpr (C::NSTAGE == 3) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % BG_NSTAGE);
-    const uint8_t* xs = smem + (kt % BG_NSTAGE) * BG_STAGE;
-    const uint8_t* cs = xs + BG_XS;
-    h8 bf[4][2];
+    if (kt + C::NSTAGE - 1 < nk) issue(kt + C::NSTAGE - 1, (kt + C::NSTAGE - 1) % C::NSTAGE);
+    const uint8_t* xs = smem + (kt % C::NSTAGE) * C::STAGE;
+    const uint8_t* cs = xs + C::XS;
+    // B fragments: lane group q holds k = (BK/4) q + 8 s + [0, 8) for k-slice s
+    h8 bf[4][C::KS];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const u32x2v w2 = *reinterpret_cast<const u32x2v*>(cs + (wn * 64 + nt * 16 + r16) * 32 + 8 * q);
-      bf[nt][0] = dequant8_nat(w2.x, zz[nt], sv[nt]);
-      bf[nt][1] = dequant8_nat(w2.y, zz[nt], sv[nt]);
+      const int col = wn * 64 + nt * 16 + r16;
+      if constexpr (BK == 64) {
+        const u32x2v w2 = *reinterpret_cast<const u32x2v*>(cs + col * 32 + 8 * q);
+        bf[nt][0] = dequant8_nat(w2.x, zz[nt], sv[nt], mask_s, magic_v);
+        bf[nt][1] = dequant8_nat(w2.y, zz[nt], sv[nt], mask_s, magic_v);
+      } else {
+        const u32x4 w4 = *reinterpret_cast<const u32x4*>(cs + col * 64 + ((q ^ C::cswz(col)) << 4));
+        bf[nt][0] = dequant8_nat(w4.x, zz[nt], sv[nt], mask_s, magic_v);
+        bf[nt][1] = dequant8_nat(w4.y, zz[nt], sv[nt], mask_s, magic_v);
+        bf[nt][2] = dequant8_nat(w4.z, zz[nt], sv[nt], mask_s, magic_v);
+        bf[nt][3] = dequant8_nat(w4.w, zz[nt], sv[nt], mask_s, magic_v);
+      }
     }
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
       const int row = wm * 128 + mt * 16 + r16;
-      const int sw = (row >> 1) & 7;
+      const int sw = C::xswz(row);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const h8 af = *reinterpret_cast<const h8*>(xs + row * 128 + (((2 * q + s2) ^ sw) << 4));
+      for (int s2 = 0; s2 < C::KS; ++s2) {
+        const h8 af = *reinterpret_cast<const h8*>(xs + row * (BK * 2) + (((C::KS * q + s2) ^ sw) << 4));
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf[nt][s2], acc[mt][nt], 0, 0, 0);
@@ -606,10 +657,13 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 13: launch_gemv<2, 16, 1>(a, st, true); break;
       default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
     }
-  } else if (a.gpr == 1 && N % BG_N == 0 && K % BG_K == 0 && M >= 512 && variant != 1 &&
+  } else if (a.gpr == 1 && N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 &&
              !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     const int64_t blocks = ((M + BG_M - 1) / BG_M) * (N / BG_N);
-    hipLaunchKernelGGL(k_w4a16_big, dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+    if (variant == 23 && K % 128 == 0)
+      hipLaunchKernelGGL((k_w4a16_big<128>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_w4a16_big<64>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
   } else {
     const int64_t blocks = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k_w4a16, dim3((unsigned)blocks), dim3(NTHR), 0, st, a);

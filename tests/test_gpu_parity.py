@@ -537,6 +537,8 @@ def test_w4a16_prefill_big_tile(K, M, sym):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b)
     err = (y.float() - ref).abs()
     assert bool((err <= tol).all()), float(err.max())
+    y23 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(23))  # BK=128
+    assert bool(((y23.float() - ref).abs() <= tol).all())
     y1 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(1))
     assert float((y.float() - y1.float()).abs().max()) <= 2 * float(err.max()) + 2e-3
 

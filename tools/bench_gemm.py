@@ -79,7 +79,7 @@ def main():
             ref = lambda: torch.nn.functional.linear(x, r.out)
             ref()
             t_r = timed(ref, a.reps) if M >= 1024 else timed_graph(ref, 50)
-            for v in ([0] if M >= 1024 else [int(t) for t in a.variants.split(",")]):
+            for v in [int(t) for t in a.variants.split(",")]:
                 fl = kernels.gemm_variant_flags(v)
                 fused = lambda: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N, flags=fl)
                 fused(); torch.cuda.synchronize()
