@@ -56,12 +56,29 @@ __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel)
 // (fp16 mantissa ulp 1 at 1024); nibbles 1/5 and 3/7 sit at mantissa bits 4..7, so or-ing 0x5400
 // (64, ulp 1/16) gives (64 + q) with no shift.  (q - z) is then one exact subtraction and the only
 // rounding is the multiply by s — the reference's fp16 dequant, element for element.
-__device__ __forceinline__ h8 dequant8(uint32_t w, h2 z1024, h2 z64, h2 s) {
+// Each mask-and-magic is ONE v_and_or_b32 (gfx9 VOP3 takes no literal: masks live in SGPRs, the
+// magics in VGPRs, see DqConst); left to itself the compiler splits it into a VOP2 and + or.
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
+  return r;
+}
+struct DqConst {
+  uint32_t m0, m1;  // SGPR masks 0x000F000F, 0x00F000F0
+  uint32_t k0, k1;  // VGPR magics 0x64006400, 0x54005400
+  __device__ __forceinline__ DqConst() {
+    m0 = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+    m1 = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+    asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(k0));
+    asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(k1));
+  }
+};
+__device__ __forceinline__ h8 dequant8(uint32_t w, h2 z1024, h2 z64, h2 s, const DqConst& c) {
   const uint32_t w8 = w >> 8;
-  const h2 d0 = (as_h2((w & 0x000F000Fu) | 0x64006400u) - z1024) * s;
-  const h2 d1 = (as_h2((w & 0x00F000F0u) | 0x54005400u) - z64) * s;
-  const h2 d2 = (as_h2((w8 & 0x000F000Fu) | 0x64006400u) - z1024) * s;
-  const h2 d3 = (as_h2((w8 & 0x00F000F0u) | 0x54005400u) - z64) * s;
+  const h2 d0 = (as_h2(and_or(w, c.m0, c.k0)) - z1024) * s;
+  const h2 d1 = (as_h2(and_or(w, c.m1, c.k1)) - z64) * s;
+  const h2 d2 = (as_h2(and_or(w8, c.m0, c.k0)) - z1024) * s;
+  const h2 d3 = (as_h2(and_or(w8, c.m1, c.k1)) - z64) * s;
   return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
 }
 
@@ -115,6 +132,7 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) ncol[nt] = n0 + wn * 64 + nt * 16 + r16;
 
+  const DqConst dq;
   f4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(NTHR) void k_w4a16(GemmArgs a) {
       }
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const h8 bf = dequant8(bc[nt][s], zv[nt] + k1024, zv[nt] + k64, sv[nt]);
+        const h8 bf = dequant8(bc[nt][s], zv[nt] + k1024, zv[nt] + k64, sv[nt], dq);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[mt], bf, acc[mt][nt], 0, 0, 0);
       }
@@ -222,6 +240,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
   const int64_t crow = a.K / 2;
   const bool mvalid = r16 < a.M;  // A row of this lane = r16
   const _Float16* xrow = a.x + (int64_t)(mvalid ? r16 : 0) * a.lda;
+  const DqConst dq;
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int c0 = kb; c0 < ke; c0 += CH) {
     const int ns = min(CH, ke - c0);
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
         const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
                           perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
         const h8 af = __builtin_bit_cast(h8, pa);
-        const h8 bf = dequant8(bc[i][s], zv, zv64, sv);
+        const h8 bf = dequant8(bc[i][s], zv, zv64, sv, dq);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
       }
     }
@@ -353,6 +372,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
     __syncthreads();
   }
   const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+  const DqConst dq;
 
   f4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nj; j0 += PF) {
@@ -380,7 +400,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
           const uint32_t w = bc[u][s];
           bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
         } else {
-          bf = dequant8(bc[u][s], z1024, z64, s2);
+          bf = dequant8(bc[u][s], z1024, z64, s2, dq);
         }
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
       }
@@ -454,14 +474,6 @@ struct BigCfg {
 };
 
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-
-// one v_and_or_b32 (gfx9 VOP3 takes no literal, so the compiler would otherwise split it into a
-// VOP2 and + or): mask in an SGPR, magic in a VGPR
-__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
-  return r;
-}
 
 // 8 codes (nibble p of w = k offset p) -> 8 fp16 RN16((q - z) * s) in natural k order.
 // zz = (1024 + z, 64 + z): even k come out as 1024 + q (low nibble, 0x6400), odd k as 64 + q
