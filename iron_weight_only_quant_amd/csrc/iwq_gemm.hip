@@ -491,10 +491,22 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BK>
+__device__ __forceinline__ void glds2(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 2, 0, 0);
+}
+
+// GROUPED: scales / zero points of groups of g (multiple of BK) k: the K-step's 256 scales and 256
+// zero points ride in the same ring stage (waves 0-3 DMA the scales, 4-7 the zeros).  A 2-byte
+// LDS-DMA writes one zero-extended DWORD per lane (measured: tools/probes/glds_ushort.hip), so each
+// parameter occupies 4 bytes of LDS.
+template <int BK, bool SOUTER = false, bool GROUPED = false>
 __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
   using C = BigCfg<BK>;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[C::NSTAGE * C::STAGE];
+  constexpr int STAGE = C::STAGE + (GROUPED ? 2048 : 0);
+  constexpr int PER_STAGE = C::XI + C::CI + (GROUPED ? 1 : 0);  // DMA instructions per thread per stage
+  static_assert(!GROUPED || C::NSTAGE == 3, "grouped scales: 3-stage ring only");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[C::NSTAGE * STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -522,23 +534,35 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
     const int c = (lane % C::CCH) ^ C::cswz(col);
     csrc[j] = a.codes + (int64_t)(n0 + col) * crow + c * 16;
   }
+  // grouped: wave w < 4 fills the scale of column 64w + lane, wave w >= 4 the zero point
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
   auto issue = [&](int kt, int stg) {
-    uint8_t* base = smem + stg * C::STAGE;
+    uint8_t* base = smem + stg * STAGE;
 #pragma unroll
     for (int i = 0; i < C::XI; ++i) glds16(xsrc[i] + kt * BK, base + (wid * C::XI + i) * 1024);
 #pragma unroll
     for (int j = 0; j < C::CI; ++j) glds16(csrc[j] + kt * (BK / 2), base + C::XS + (wid * C::CI + j) * 1024);
+    if constexpr (GROUPED) {
+      const int gk = (kt * BK) / a.group;  // a K-step never straddles a group (g % BK == 0)
+      glds2(psrc + gk, base + C::XS + C::CS + wid * 256);
+    }
   };
 
   // per-channel scale / zero point of this lane's column in each 16-wide subtile
   h2 sv[4], zz[4];
+  if constexpr (!GROUPED) {
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int col = n0 + wn * 64 + nt * 16 + r16;
-    const _Float16 sc = gp<_Float16>(a.scales)[col];
-    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
-    sv[nt] = h2{sc, sc};
-    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = n0 + wn * 64 + nt * 16 + r16;
+      const _Float16 sc = gp<_Float16>(a.scales)[col];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+      sv[nt] = h2{sc, sc};
+      zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
+    }
   }
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
   uint32_t magic_v;
@@ -558,15 +582,65 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
     // own DMA of tile kt retired (with 3 stages tile kt+1's may stay in flight); the barrier makes
     // every wave's part visible and proves every wave is done reading the stage about to be refilled
     if constexpr (C::NSTAGE == 3) {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (kt + 1 < nk) {
+        if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     if (kt + C::NSTAGE - 1 < nk) issue(kt + C::NSTAGE - 1, (kt + C::NSTAGE - 1) % C::NSTAGE);
-    const uint8_t* xs = smem + (kt % C::NSTAGE) * C::STAGE;
+    const uint8_t* xs = smem + (kt % C::NSTAGE) * STAGE;
     const uint8_t* cs = xs + C::XS;
+    if constexpr (GROUPED) {
+      const uint32_t* ps = reinterpret_cast<const uint32_t*>(cs + C::CS);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int col = wn * 64 + nt * 16 + r16;
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
+        const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[256 + col]) : a.zsym;
+        sv[nt] = h2{sc, sc};
+        zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      }
+    }
+    if constexpr (SOUTER && BK == 64) {
+      // k-slice-outer order: slice 0's dequant, then its 32 MFMAs with slice 1's dequant VALU
+      // interleaved (sched_group_barrier: 1 MFMA : 2 VALU), then slice 1's 32 MFMAs
+      u32x2v w2[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        w2[nt] = *reinterpret_cast<const u32x2v*>(cs + (wn * 64 + nt * 16 + r16) * 32 + 8 * q);
+      h8 b0[4], b1[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) b0[nt] = dequant8_nat(w2[nt].x, zz[nt], sv[nt], mask_s, magic_v);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) b1[nt] = dequant8_nat(w2[nt].y, zz[nt], sv[nt], mask_s, magic_v);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = wm * 128 + mt * 16 + r16;
+        const h8 af = *reinterpret_cast<const h8*>(xs + row * 128 + (((2 * q) ^ C::xswz(row)) << 4));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, b0[nt], acc[mt][nt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+      }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = wm * 128 + mt * 16 + r16;
+        const h8 af = *reinterpret_cast<const h8*>(xs + row * 128 + (((2 * q + 1) ^ C::xswz(row)) << 4));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, b1[nt], acc[mt][nt], 0, 0, 0);
+      }
+      continue;
+    }
     // B fragments: lane group q holds k = (BK/4) q + 8 s + [0, 8) for k-slice s
     h8 bf[4][C::KS];
 #pragma unroll
@@ -669,11 +743,15 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 13: launch_gemv<2, 16, 1>(a, st, true); break;
       default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
     }
-  } else if (a.gpr == 1 && N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 &&
-             !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+  } else if (N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+             (a.gpr == 1 || a.group % 64 == 0)) {
     const int64_t blocks = ((M + BG_M - 1) / BG_M) * (N / BG_N);
-    if (variant == 23 && K % 128 == 0)
+    if (a.gpr != 1)
+      hipLaunchKernelGGL((k_w4a16_big<64, false, true>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+    else if (variant == 23 && K % 128 == 0)
       hipLaunchKernelGGL((k_w4a16_big<128>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+    else if (variant == 24)
+      hipLaunchKernelGGL((k_w4a16_big<64, true>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
     else
       hipLaunchKernelGGL((k_w4a16_big<64>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
   } else {

@@ -522,24 +522,28 @@ def test_quant_dim1_register_kernel(K, dtype):
 
 @pytest.mark.parametrize("M", [512, 600, 1024])
 @pytest.mark.parametrize("sym", [False, True])
-def test_w4a16_prefill_big_tile(K, M, sym):
+@pytest.mark.parametrize("group", [-2, 128, 64])
+def test_w4a16_prefill_big_tile(K, M, sym, group):
     """The 256x256 LDS-DMA prefill kernel (per-channel, N % 256 == 0, M >= 512): vs an fp32 GEMM on the
     bit-exact dequantized weight, and against the 128x128 kernel (variant 1)."""
     N, Kd = 512, 4352
     torch.manual_seed(1)
     w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
     K.fill_synthetic(w, 91)
-    r = K.quantize_minmax(w, 4, -2, sym, 0, want_codes=True)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
     x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b)
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
     err = (y.float() - ref).abs()
     assert bool((err <= tol).all()), float(err.max())
-    y23 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(23))  # BK=128
-    assert bool(((y23.float() - ref).abs() <= tol).all())
-    y1 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(1))
+    if group == -2:
+        y24 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(24))
+        assert torch.equal(y24, y)  # same BK, same accumulation order
+        y23 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(23))  # BK=128
+        assert bool(((y23.float() - ref).abs() <= tol).all())
+    y1 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(1))
     assert float((y.float() - y1.float()).abs().max()) <= 2 * float(err.max()) + 2e-3
 
 
