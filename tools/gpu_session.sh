@@ -51,6 +51,12 @@ if [[ $WHAT == *formats* ]]; then
   step prof_formats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_formats" -o run -- python3 "$ROOT/tools/bench_formats.py" --reps 10
   cd "$ROOT"
 fi
+if [[ $WHAT == *gpmc* ]]; then
+  cd /tmp
+  step gemm_pmc 600 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$OUT/gemm_pmc" -o run -- python3 "$ROOT/tools/gemm_pmc.py"
+  step gemm_pmc_dec 600 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_WAVES --output-format csv -d "$OUT/gemm_pmc_dec" -o run -- python3 "$ROOT/tools/gemm_pmc.py" --m 1 --n 28672 --k 8192
+  cd "$ROOT"
+fi
 if [[ $WHAT == *ab* ]]; then
   step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
 fi
