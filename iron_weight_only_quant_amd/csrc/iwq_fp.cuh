@@ -32,23 +32,27 @@ struct FpSpec {
   float sub_c;        // 2^(23 + emin - M): (x + c) - c rounds x to the FP subnormal grid (RNE)
   float sub_max;      // (2^M - 1) * 2^(emin - M): largest FP subnormal (no carry into the normals)
   float sub_inv;      // 2^(M - emin)
+  float sub_c16;      // 2^(10 + emin - M): fp16 form of sub_c
 };
 
 // The log2 threshold tables live in LDS during a kernel (a per-lane index into __constant__ memory
 // would be one vector-memory load per element): kernels call stage_log2_tables() once.
 typedef __attribute__((address_space(3))) const uint16_t lds_u16;
 struct Log2Tabs {
-  lds_u16* up;  // kLog2UpThresh
-  lds_u16* p1;  // kLog2P1UpThresh
+  lds_u16* up;   // kLog2UpThresh
+  lds_u16* p1;   // kLog2P1UpThresh
+  lds_u16* up7;  // kLog2UpThresh with "none" (0xFFFF) as 0x7FFF: u - thr is then a valid int16
 };
-// all threads of the block must call it (contains a barrier); `buf` = a __shared__ uint16_t[80]
+// all threads of the block must call it (contains a barrier); `buf` = a __shared__ uint16_t[120]
 __device__ __forceinline__ Log2Tabs stage_log2_tables(uint16_t* buf) {
   if (threadIdx.x < 40) {
-    buf[threadIdx.x] = kLog2UpThresh[threadIdx.x];
+    const uint16_t u = kLog2UpThresh[threadIdx.x];
+    buf[threadIdx.x] = u;
     buf[40 + threadIdx.x] = kLog2P1UpThresh[threadIdx.x];
+    buf[80 + threadIdx.x] = u == 0xFFFFu ? (uint16_t)0x7FFFu : u;
   }
   __syncthreads();
-  return Log2Tabs{(lds_u16*)buf, (lds_u16*)buf + 40};
+  return Log2Tabs{(lds_u16*)buf, (lds_u16*)buf + 40, (lds_u16*)buf + 80};
 }
 
 // floor(RN16(log2 x)) for a positive fp16 magnitude (bit pattern, 1..0x7BFF)
@@ -125,6 +129,51 @@ __device__ __forceinline__ uint32_t fp_roundtrip_fast(uint32_t tb, float ta, con
   return u == 0 ? 0u : (mag | (tb & 0x8000u));
 }
 
+// Packed-pair form of fp_roundtrip_fast: two fp16 t (bits in one dword, finite, clamped) -> the two
+// decoded fp16 values, all integer steps on 16-bit halves (v_pk_*_u16, bitwise selects), the FP
+// subnormal grid in fp16 arithmetic: (|t| + C) - C with C = 2^(10 + emin - M) rounds |t| < 2^emin to
+// multiples of 2^(emin - M) (RNE) because the fp16 spacing in [C, 2C) is exactly that.
+__device__ __forceinline__ uint32_t pk_lt_mask(u16x2 a, u16x2 b) {  // 0xFFFF per half where a < b
+  // valid when |a - b| < 2^15 (all callers); (a - b) >> 15 = 1 iff a < b
+  const u16x2 lt = (a - b) >> (u16x2)15;
+  return __builtin_bit_cast(uint32_t, (u16x2)0 - lt);
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {  // mask ? a : b
+  return (mask & a) | (~mask & b);
+}
+__device__ __forceinline__ uint32_t fp_roundtrip_pk(uint32_t tpair, const FpSpec& f, const Log2Tabs& tabs,
+                                                    h2 c16, h2 submax16) {
+  const u16x2 tb = __builtin_bit_cast(u16x2, tpair);
+  const u16x2 u = tb & (u16x2)0x7FFF;
+  const u16x2 e16 = u >> (u16x2)10;
+  const u16x2 fr = u & (u16x2)0x3FF;
+  const u16x2 sh = (u16x2)(uint16_t)f.sh;
+  u16x2 q = (fr + (u16x2)(uint16_t)f.rne_bias + ((fr >> sh) & (u16x2)1)) >> sh;
+  q = __builtin_elementwise_min(q, (u16x2)(uint16_t)f.mmax);
+  const uint32_t rn = __builtin_bit_cast(uint32_t, (u16x2)((e16 << (u16x2)10) | (q << sh)));
+  const u16x2 thr = {tabs.up7[e16.x + 9], tabs.up7[e16.y + 9]};
+  const uint32_t rup = __builtin_bit_cast(uint32_t, (u16x2)((e16 + (u16x2)1) << (u16x2)10));
+  uint32_t r = bfi(pk_lt_mask(u, thr), rn, rup);                        // u < thr: RNE result, else 2^(e+1)
+  r = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, r),
+                                                             (u16x2)(uint16_t)f.fpmax_bits));
+  const h2 ta = __builtin_bit_cast(h2, __builtin_bit_cast(uint32_t, u));
+  const uint32_t rs = __builtin_bit_cast(uint32_t, pk_min((ta + c16) - c16, submax16));
+  const uint32_t mag = bfi(pk_lt_mask(__builtin_bit_cast(u16x2, r), (u16x2)(uint16_t)f.emin_bits), rs, r);
+  const u16x2 nz = (u + (u16x2)0x7FFF) >> (u16x2)15;                    // 1 where t != 0
+  const uint32_t nzm = __builtin_bit_cast(uint32_t, (u16x2)0 - nz);
+  return (mag | (tpair & 0x80008000u)) & nzm;
+}
+
+// code of one element from its decoded fp16 magnitude bits (see fp_roundtrip_fast)
+__device__ __forceinline__ uint32_t fp_code_from_mag(uint32_t mag, uint32_t tb, const FpSpec& f) {
+  const uint32_t u = tb & 0x7FFFu;
+  const bool normal = mag >= f.emin_bits;
+  const uint32_t ef = normal ? (mag >> 10) - 15u + (uint32_t)f.bias : 0u;
+  const uint32_t m = normal ? (mag >> f.sh) & f.mmax
+                            : (uint32_t)((float)__builtin_bit_cast(_Float16, (uint16_t)mag) * f.sub_inv);
+  return u == 0 ? 0u : ((((tb >> 15) & 1u) << (f.E + f.M)) | (ef << f.M) | m);
+}
+
 struct FpParams {
   float s;    // scales (fp16 value)
   float rs;   // RN32(1/s)
@@ -195,6 +244,37 @@ __device__ __forceinline__ float fp_quant_elem(float w, const FpParams& p, const
   if constexpr (!SYM) y = f16r(y + p.z);                                  // + zeros
   if (t != t) y = t;                                                      // NaN scale: NaN out
   return y;
+}
+
+// Two elements of the FP branches at once (finite group): corrected fp32 divisions as a float2
+// (v_pk_mul/fma_f32), pair conversion, packed clamp, the packed codec, packed fp16 dequant.
+template <bool SYM, bool WANT_CODE>
+__device__ __forceinline__ uint32_t fp_quant_pair_fast(uint32_t wpair, const FpParams& p, const FpSpec& f,
+                                                       const Log2Tabs& tabs, uint32_t& c0, uint32_t& c1) {
+  const h2 s16 = h2{(_Float16)p.s, (_Float16)p.s};
+  const h2 z16 = h2{(_Float16)p.z, (_Float16)p.z};
+  h2 d = __builtin_bit_cast(h2, wpair);
+  if constexpr (!SYM) d = d - z16;                              // RN16(w - z): fp16 sub == ATen's fp32-then-round
+  const f2 df = {(float)d.x, (float)d.y};
+  const f2 rs2 = {p.rs, p.rs}, s2 = {p.s, p.s};
+  f2 q0 = df * rs2;
+  f2 e = __builtin_elementwise_fma(-q0, s2, df);
+  f2 q1 = __builtin_elementwise_fma(e, rs2, q0);
+  asm volatile("" : "+v"(q1));                                   // keep the fp32 rounding (no fma_mix)
+  h2 t = __builtin_convertvector(q1, h2);                        // RN16(d / s)
+  const h2 fm = h2{(_Float16)f.fp_max16, (_Float16)f.fp_max16};
+  t = pk_max(pk_min(t, fm), -fm);
+  const uint32_t tb = __builtin_bit_cast(uint32_t, t);
+  const h2 c16 = h2{(_Float16)f.sub_c16, (_Float16)f.sub_c16};
+  const h2 sm16 = h2{(_Float16)f.sub_max, (_Float16)f.sub_max};
+  const uint32_t dec = fp_roundtrip_pk(tb, f, tabs, c16, sm16);
+  if constexpr (WANT_CODE) {
+    c0 = fp_code_from_mag(dec & 0x7FFFu, tb & 0xFFFFu, f);
+    c1 = fp_code_from_mag((dec >> 16) & 0x7FFFu, tb >> 16, f);
+  }
+  h2 y = __builtin_bit_cast(h2, dec) * s16;                     // RN16(exact product)
+  if constexpr (!SYM) y = y + z16;
+  return __builtin_bit_cast(uint32_t, y);
 }
 
 // ---------------------------------------------------------------------------------------------

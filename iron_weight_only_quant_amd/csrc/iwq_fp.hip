@@ -112,7 +112,7 @@ __device__ __forceinline__ void store_fp_codes8(uint8_t* base, int64_t elem0, co
 template <int CODEC, int G, bool SYM, int CODES>
 __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
   using F = Fmt<DT_F16>;
-  __shared__ uint16_t tab_buf[80];
+  __shared__ uint16_t tab_buf[120];
   const Log2Tabs tabs = stage_log2_tables(tab_buf);
   constexpr int UNROLL = 4;
   constexpr int LPG = G / 8;
@@ -145,11 +145,17 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
       Vec8<DT_F16> o;
       uint32_t c[8];
       bool nan8 = false;
+      if (CODEC == CODEC_FP && p.fast) {  // finite group: packed pairs, no NaN possible
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float y = fp_elem<CODEC, SYM, CODES != 0>(F::to_f(v[k].get(i)), p, a.f, c[i], tabs);
-        nan8 |= (y != y);
-        o.set(i, F::from_f(y));
+        for (int j = 0; j < 4; ++j)
+          o.u[j] = fp_quant_pair_fast<SYM, CODES != 0>(v[k].u[j], p, a.f, tabs, c[2 * j], c[2 * j + 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float y = fp_elem<CODEC, SYM, CODES != 0>(F::to_f(v[k].get(i)), p, a.f, c[i], tabs);
+          nan8 |= (y != y);
+          o.set(i, F::from_f(y));
+        }
       }
       if (valid) {
         any_nan |= nan8;
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
 template <int CODEC, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
   using F = Fmt<DT_F16>;
-  __shared__ uint16_t tab_buf[80];
+  __shared__ uint16_t tab_buf[120];
   const Log2Tabs tabs = stage_log2_tables(tab_buf);
   const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
   const int64_t tid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -298,6 +304,7 @@ int fp_spec(int exp_bits, int mant_bits, FpSpec& f) {
   f.sub_c = __builtin_ldexpf(1.0f, 23 + f.emin - mant_bits);
   f.sub_max = __builtin_ldexpf((float)f.mmax, f.emin - mant_bits);
   f.sub_inv = __builtin_ldexpf(1.0f, mant_bits - f.emin);
+  f.sub_c16 = __builtin_ldexpf(1.0f, 10 + f.emin - mant_bits);
   return IWQ_OK;
 }
 
