@@ -27,6 +27,35 @@ class QuantResult:
         return bool(self.nan_flag.item() != 0)
 
 
+class _FlagPool:
+    """Per-device pool of pre-zeroed NaN flags: one int32 slot per call instead of a zero-fill kernel
+    per call (the fill alone cost ~4 us of device time, 10-30 % of a 4096x4096 quantization).
+    Slots are handed out round-robin; the pool is re-zeroed (one fill) when it wraps, so a result's
+    flag stays valid for the next 65535 calls on that device."""
+    SIZE = 65536
+
+    def __init__(self):
+        self.buf = {}
+        self.next = {}
+
+    def take(self, dev):
+        key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+        buf = self.buf.get(key)
+        i = self.next.get(key, 0)
+        if buf is None or i >= self.SIZE:
+            if buf is None:
+                buf = torch.zeros(self.SIZE, dtype=torch.int32, device=dev)
+                self.buf[key] = buf
+            else:
+                buf.zero_()
+            i = 0
+        self.next[key] = i + 1
+        return buf[i:i + 1]
+
+
+_flags = _FlagPool()
+
+
 def group_geometry(rows, cols, group, quant_dim):
     """(L, G) of the grouped view, or raise like the reference (quant_linear.py:896-906)."""
     vr, vc = (cols, rows) if quant_dim == 1 else (rows, cols)
@@ -86,7 +115,7 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
         if n_bits > 8:
             raise ValueError("packed codes need n_bits <= 8")
         codes = torch.empty(codes_nbytes(rows, cols, n_bits), dtype=torch.uint8, device=dev)
-    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    nan_flag = _flags.take(dev)
     wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
     ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev) if wsb > 0 else None
     with torch.cuda.device(dev):
@@ -122,7 +151,7 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     zeros = None if symmetric else torch.empty(G, dtype=w.dtype, device=dev)
     codes = torch.empty(fp_code_nbytes(rows, cols, exp_bits, mant_bits), dtype=torch.uint8, device=dev) \
         if want_codes else None
-    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    nan_flag = _flags.take(dev)
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
@@ -158,7 +187,7 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     if out is None:
         out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
     scales = torch.empty(G, dtype=w.dtype, device=dev)
-    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    nan_flag = _flags.take(dev)
     wsb = int(lib.iwq_approx_workspace_bytes(rows, cols, int(exp_bits), int(mant_bits), int(group), int(quant_dim),
                                              int(bool(double_approx))))
     ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
@@ -216,7 +245,7 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     dev = w.device
     out = torch.empty_like(w)
     scales = torch.empty(G, dtype=w.dtype, device=dev)
-    nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    nan_flag = _flags.take(dev)
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):

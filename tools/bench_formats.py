@@ -4,7 +4,9 @@ grid, BFP and the approximate / double-approximate decodes.
 
 Prints one JSON line per path: weights GB/s (fp16 input bytes / time), algorithmic HBM bytes per call
 (read weight + write dequant + scales/zeros [+ codes]), achieved GB/s and the fraction of 8 TB/s.
-Timing: HIP events on the launching stream around R back-to-back calls, median of 5 rounds.
+Timing: R calls captured in one hipGraph and replayed, HIP events around the replay, median of 5
+rounds — device time per call without the Python wrapper's host cost (which exceeds the device
+time of a single 90 MB tensor).
 """
 import argparse
 import json
@@ -20,13 +22,23 @@ PEAK = 8.0e12
 
 
 def timed(fn, reps, rounds=5):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     out = []
     for _ in range(rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        for _ in range(reps):
-            fn()
+        g.replay()
         e1.record(st)
         torch.cuda.synchronize()
         out.append(e0.elapsed_time(e1) / reps * 1e-3)
