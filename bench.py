@@ -48,6 +48,7 @@ def parse():
                     help="also time the all_gather of packed codes+scales to rank 0 (RCCL), reported separately")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ppl", action="store_true", help="skip the PPL-harness plumbing run (random-init OPT-125M)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--variant", type=int, default=0, help="kernel tuning variant for the timed run")
     ap.add_argument("--variants", default="", help="A/B: comma list of variants timed in interleaved rounds")
@@ -104,6 +105,35 @@ def make_weights(model, rank, world):
         ws.append(t)
         names.append(name)
     return ws, names, shapes
+
+
+def ppl_plumbing(bits, group, symmetric, chunks=8, seqlen=2048):
+    """Second half of the metric, as far as it can be measured offline: the SequentialPPLEvaluator
+    arithmetic (main.py:42-140) before and after quantize_model on a RANDOM-INIT OPT-125M-shaped
+    model with synthetic tokens (no weights / datasets exist here).  Exercises the harness and the
+    module swap; the perplexities themselves carry no quality information."""
+    try:
+        import copy
+        from types import SimpleNamespace
+        import transformers
+        from iron_weight_only_quant_amd.ppl import SequentialPPLEvaluator
+        from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+        torch.manual_seed(0)
+        base = transformers.OPTForCausalLM(transformers.OPTConfig()).half().cuda().eval()
+        toks = torch.randint(0, base.config.vocab_size, (1, chunks * seqlen), generator=torch.Generator().manual_seed(1))
+        p0, ntok, _ = SequentialPPLEvaluator(base, device="cuda", seqlen=seqlen, tokens=toks).calculate_ppl("wikitext")
+        q = copy.deepcopy(base)
+        quantize_model(q, SimpleNamespace(w_bit=bits, a_bit=16, w_group_size=group, w_symmetric=symmetric,
+                                          w_format="int", quant_dim=0), verbose=False)
+        p1, _, _ = SequentialPPLEvaluator(q, device="cuda", seqlen=seqlen, tokens=toks).calculate_ppl("wikitext")
+        del base, q
+        torch.cuda.empty_cache()
+        return {"model": "random-init OPT-125M-shaped (transformers OPTConfig defaults; no weights offline)",
+                "tokens": "synthetic", "num_tokens": ntok, "seqlen": seqlen, "ppl_fp16": round(p0, 3),
+                "ppl_quant": round(p1, 3), "delta": round(p1 - p0, 3),
+                "note": "plumbing check of the PPL half of the metric; not a quality measurement"}
+    except Exception as e:  # transformers missing etc.: report, do not fail the bench
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def cpu_baseline(weights, bits, group, symmetric, budget_s):
@@ -242,6 +272,10 @@ def main():
     if rank == 0 and ws_n == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(weights, args.bits, args.group, args.symmetric, args.cpu_seconds)
 
+    ppl = None
+    if rank == 0 and ws_n == 1 and not args.no_ppl:
+        ppl = ppl_plumbing(args.bits, args.group, args.symmetric)
+
     if rank == 0:
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ws_n, "steps": args.steps,
@@ -261,6 +295,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "ppl_delta": None,
+            "ppl_plumbing": ppl,
             "gather_ms": gather_ms,
         }
         print(json.dumps(rec), flush=True)
