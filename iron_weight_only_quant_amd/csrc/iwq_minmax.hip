@@ -652,11 +652,15 @@ bool is_pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
 
+// Single tensors (QuantLinear / pseudo_quantize_tensor, a few iterations per wave) run with the
+// next iteration's loads prefetched and plain (temporal) loads; the whole-model batched walk
+// (hundreds of iterations per wave) with non-temporal loads and no prefetch.  Both picked by
+// in-run A/B (tools/ab_single.py, bench.py --variants; profiles/r01_ab_*).
 template <int DT, int G, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   constexpr int UNROLL = 4;
   static int cache[64] = {0};
-  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL>;
+  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ BATCHED>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);

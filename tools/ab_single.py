@@ -1,0 +1,35 @@
+"""A/B the k_group tuning variants (and the copy probes) on ONE weight tensor (QuantLinear-style
+per-layer use) instead of the whole model: graph-replayed device time per launch."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from tools.bench_formats import timed  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=11008)
+    ap.add_argument("--cols", type=int, default=4096)
+    ap.add_argument("--variants", default="0,1,2,5,6,8,100,102")
+    a = ap.parse_args()
+    from iron_weight_only_quant_amd import kernels as K
+    w = torch.empty(a.rows, a.cols, dtype=torch.float16, device="cuda")
+    K.fill_synthetic(w, 3)
+    out = torch.empty_like(w)
+    plan = K.BatchPlan([w], 4, 128, False, outs=[out])
+    n = w.numel()
+    algo = 4 * n + 4 * (n // 128)
+    for v in [int(t) for t in a.variants.split(",")]:
+        t = timed(lambda: plan.run(variant=v), 20)
+        print(json.dumps({"variant": v, "shape": [a.rows, a.cols], "us": round(t * 1e6, 2),
+                          "achieved_GBps": round(algo / t / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
