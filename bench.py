@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--inplace", action="store_true",
                     help="write the dequantized weights over the inputs (QuantLinear / quantize_model semantics)")
+    ap.add_argument("--ramp-seconds", type=float, default=1.0,
+                    help="untimed clock ramp before the copy-ceiling probe and the W warmup steps")
+    ap.add_argument("--no-shapes", action="store_true",
+                    help="skip the cold single-tensor calls per Llama shape (4096x4096, 11008x4096, 4096x11008)")
     return ap.parse_args()
 
 
@@ -174,6 +178,84 @@ def time_gather(plan, names, all_shapes, args, ws_n):
     return round((time.perf_counter() - t0) * 1e3, 3)
 
 
+def clock_ramp(plan, seconds):
+    """Untimed back-to-back launches until `seconds` of wall time have passed: a few warmup steps
+    (23 ms at W=5) leave the GPU below its sustained clock and cost up to ~15 % on a fresh box."""
+    stream = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(10):
+            plan.run(stream)
+        torch.cuda.synchronize()
+
+
+def copy_ceiling(plan, steps=5):
+    """In-run ceiling: a plain 16-B non-temporal copy of the same bytes (read w, write out), same grid
+    shape policy (probe variant 100).  Overwrites plan.outs; call before the timed warmup."""
+    stream = torch.cuda.current_stream()
+    plan.run(stream, variant=100)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        plan.run(stream, variant=100)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return round(plan.numel * 4 / (ms / 1e3) / 1e9, 1)
+
+
+def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
+    """Single-tensor drop-in calls (kernels.quantize_minmax == pseudo_quantize_tensor's device path)
+    per Llama weight shape, COLD: `reps` consecutive calls on distinct resident instances of the
+    shape (>= 1 GB per replay, so the 256 MB MALL holds none of it), captured in one hipGraph and
+    replayed; device time per call = event time / reps (includes the inter-kernel boundary).
+    value per shape = all ranks' fp16 input bytes / max-over-ranks time."""
+    from iron_weight_only_quant_amd import kernels as K
+    by_shape = {}
+    for i, w in enumerate(plan.weights):
+        by_shape.setdefault(tuple(w.shape), []).append(i)
+    out = {}
+    for shp in sorted(by_shape):
+        idx = by_shape[shp][:reps]
+        fns = [(lambda i=i: K.quantize_minmax(plan.weights[i], args.bits, args.group, args.symmetric, 0,
+                                              out=plan.outs[i])) for i in idx]
+        for f in fns:
+            f()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for f in fns:
+                f()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for f in fns:
+                f()
+        g.replay()
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        ts = []
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            g.replay()
+            e1.record(st)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / len(idx) * 1e-3)
+        ts.sort()
+        t = max_over_ranks(ts[len(ts) // 2], ws_n)
+        n = shp[0] * shp[1]
+        alg = n * 4 + (n // args.group) * 2 * (1 if args.symmetric else 2)
+        out[f"{shp[0]}x{shp[1]}"] = {
+            "us_per_call": round(t * 1e6, 2), "weights_GBps": round(ws_n * n * 2 / t / 1e9, 1),
+            "achieved_GBps_per_gpu": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+            "calls": len(idx), "cold": True}
+        del g
+    return out
+
+
 def ab_variants(plan, variants, args):
     """Interleaved in-process A/B of kernel variants (cdna_hip_programming.md §5.4 rule 24)."""
     stream = torch.cuda.current_stream()
@@ -220,6 +302,8 @@ def main():
     stream = torch.cuda.current_stream()
     if args.variants:
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
+    clock_ramp(plan, args.ramp_seconds)
+    ceiling = copy_ceiling(plan) if not args.inplace else None  # the copy probe would clobber in-place inputs
     for _ in range(args.warmup):
         plan.run(variant=args.variant)
     torch.cuda.synchronize()
@@ -240,6 +324,10 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
     wall_max = max_over_ranks(wall, ws_n)
     ms_per_step = wall_max / args.steps * 1e3
+
+    shapes_rec = None
+    if not args.no_shapes and not strong:
+        shapes_rec = per_shape(plan, names, ws_n, args)
 
     gather_ms = None
     if args.gather and ws_n > 1:
@@ -292,7 +380,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_group<f16,128,asym,batched>", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes, "in_run_copy_ceiling_GBps": ceiling},
+            "shapes": shapes_rec,
             "cpu_baseline": cpu,
             "ppl_delta": None,
             "ppl_plumbing": ppl,

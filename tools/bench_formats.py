@@ -6,7 +6,9 @@ Prints one JSON line per path: weights GB/s (fp16 input bytes / time), algorithm
 (read weight + write dequant + scales/zeros [+ codes]), achieved GB/s and the fraction of 8 TB/s.
 Timing: R calls captured in one hipGraph and replayed, HIP events around the replay, median of 5
 rounds — device time per call without the Python wrapper's host cost (which exceeds the device
-time of a single 90 MB tensor).
+time of a single 90 MB tensor).  The calls rotate over --copies distinct resident weights (default
+16 = 1.4 GB of input per replay), so the 256 MB MALL holds none of a call's bytes (cold, as when
+quantize_model walks a model's layers); --copies 1 re-runs one MALL-warm tensor.
 """
 import argparse
 import json
@@ -50,40 +52,52 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=11008)
     ap.add_argument("--cols", type=int, default=4096)
-    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=2, help="passes over the copies per graph")
+    ap.add_argument("--copies", type=int, default=16)
+    ap.add_argument("--only", default="", help="comma list of path names to run")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels as K
     R, C = a.rows, a.cols
     n = R * C
-    w = torch.empty(R, C, dtype=torch.float16, device="cuda")
-    K.fill_synthetic(w, 1)
-    out = torch.empty_like(w)
+    ws = []
+    for c in range(a.copies):
+        t = torch.empty(R, C, dtype=torch.float16, device="cuda")
+        K.fill_synthetic(t, 1 + c)
+        ws.append(t)
+    outs = [torch.empty_like(t) for t in ws]
     g = 128
     G = n // g
     cases = [
-        ("int4_g128_asym", lambda: K.quantize_minmax(w, 4, g, False, 0, out=out), 4 * n + 4 * G),
-        ("int4_g128_asym_codes", lambda: K.quantize_minmax(w, 4, g, False, 0, out=out, want_codes=True),
+        ("int4_g128_asym", lambda w, out: K.quantize_minmax(w, 4, g, False, 0, out=out), 4 * n + 4 * G),
+        ("int4_g128_asym_codes", lambda w, out: K.quantize_minmax(w, 4, g, False, 0, out=out, want_codes=True),
          4 * n + 4 * G + n // 2),
-        ("int8_perchannel_asym", lambda: K.quantize_minmax(w, 8, -2, False, 0, out=out), 4 * n + 4 * R),
-        ("int4_g128_quant_dim1", lambda: K.quantize_minmax(w, 4, g, False, 1, out=out), 4 * n + 4 * G),
-        ("int4_per_tensor", lambda: K.quantize_minmax(w, 4, -1, False, 0, out=out), 4 * n + 4),
-        ("fp8_e4m3_g128_sym", lambda: K.quantize_fp(w, 4, 3, g, True, 0, out=out), 4 * n + 2 * G),
-        ("fp8_e4m3_g128_asym", lambda: K.quantize_fp(w, 4, 3, g, False, 0, out=out), 4 * n + 4 * G),
-        ("fp6_e3m2_g128_asym", lambda: K.quantize_fp(w, 3, 2, g, False, 0, out=out), 4 * n + 4 * G),
-        ("fp4_e2m1_g128_asym", lambda: K.quantize_fp(w, 2, 1, g, False, 0, out=out), 4 * n + 4 * G),
-        ("fp4_grid_g128", lambda: K.fp4_grid(w, g), 4 * n + 2 * G),
-        ("bfp_w4_g128", lambda: K.quantize_bfp(w, 4, g, out=out), 4 * n),
-        ("bfp_w8_g32", lambda: K.quantize_bfp(w, 8, 32, out=out), 4 * n),
-        ("approx_fp8_g128", lambda: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, False, out=out), 4 * n + 2 * G),
+        ("int8_perchannel_asym", lambda w, out: K.quantize_minmax(w, 8, -2, False, 0, out=out), 4 * n + 4 * R),
+        ("int4_g128_quant_dim1", lambda w, out: K.quantize_minmax(w, 4, g, False, 1, out=out), 4 * n + 4 * G),
+        ("int4_per_tensor", lambda w, out: K.quantize_minmax(w, 4, -1, False, 0, out=out), 4 * n + 4),
+        ("fp8_e4m3_g128_sym", lambda w, out: K.quantize_fp(w, 4, 3, g, True, 0, out=out), 4 * n + 2 * G),
+        ("fp8_e4m3_g128_asym", lambda w, out: K.quantize_fp(w, 4, 3, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp6_e3m2_g128_asym", lambda w, out: K.quantize_fp(w, 3, 2, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp4_e2m1_g128_asym", lambda w, out: K.quantize_fp(w, 2, 1, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp4_grid_g128", lambda w, out: K.fp4_grid(w, g), 4 * n + 2 * G),
+        ("bfp_w4_g128", lambda w, out: K.quantize_bfp(w, 4, g, out=out), 4 * n),
+        ("bfp_w8_g32", lambda w, out: K.quantize_bfp(w, 8, 32, out=out), 4 * n),
+        ("approx_fp8_g128", lambda w, out: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, False, out=out), 4 * n + 2 * G),
         # double: FP pass writes codes (1 B), decode pass reads codes + scales, writes dequant
-        ("approx_fp8_g128_double", lambda: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, True, out=out),
+        ("approx_fp8_g128_double", lambda w, out: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, True, out=out),
          2 * n + n + n + 2 * n + 2 * G + 2 * G),
     ]
-    for name, fn, algo in cases:
+    only = set(a.only.split(",")) if a.only else None
+    for name, f1, algo in cases:
+        if only is not None and name not in only:
+            continue
+
+        def fn(f1=f1):
+            for w, out in zip(ws, outs):
+                f1(w, out)
         fn()
         torch.cuda.synchronize()
-        t = timed(fn, a.reps)
-        print(json.dumps({"path": name, "shape": [R, C], "ms": round(t * 1e3, 4),
+        t = timed(fn, a.reps) / len(ws)
+        print(json.dumps({"path": name, "shape": [R, C], "copies": len(ws), "ms": round(t * 1e3, 4),
                           "weights_GBps": round(2 * n / t / 1e9, 1), "algo_bytes": int(algo),
                           "achieved_GBps": round(algo / t / 1e9, 1), "frac_of_8TBps": round(algo / t / PEAK, 3)}),
               flush=True)

@@ -60,6 +60,10 @@ fi
 if [[ $WHAT == *ab* ]]; then
   step ab 600 python bench.py --no-cpu-baseline --variants "${AB_VARIANTS:-0,1,2,3,4,5,6,7,8}" --steps 10 --rounds 5
 fi
+if [[ $WHAT == *single* ]]; then
+  step ab_single 600 python tools/ab_single.py ${SINGLE_ARGS:-}
+  step ab_single_4096 600 python tools/ab_single.py --rows 4096 --cols 4096 --copies 64 ${SINGLE_ARGS:-}
+fi
 if [[ $WHAT == *pmc* ]]; then
   cd /tmp
   B="python3 $ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1"
