@@ -509,6 +509,80 @@ __device__ __forceinline__ bool quant8(const Vec8<DT>& v, const GroupParams& p, 
   return any_nan;
 }
 
+// ---------------------------------------------------------------------------------------------
+// biased fast path (fp16, n_bits <= 9, p.fast groups): 11 VALU ops per element pair
+// ---------------------------------------------------------------------------------------------
+// With B = 1536:  u = RN16(t + B) is rint(t) + B exactly for |t| < 512 (u in [1024, 2048), where
+// fp16 spacing is 1; B is even, so RNE ties go to the same integer as torch.round's); and
+// c - z = clamp(rint(t) + z, lo, hi) - z = clamp(rint(t), lo - z, hi - z)  (integers, exact), so
+//   y = (clamp(u, B + lo - z, B + hi - z) - B) * s
+// For n_bits <= 9 both bounds lie in [1025, 2047]: a t with |t| >= 512 gives a u outside
+// [1024, 2048) that clamps to the same bound as rint(t) would.  The code is
+// c + off = u_clamped + (z + off - B) (an integer in [0, 2^b), exact), read from the mantissa of
+// u_clamped + (z + off - B + 1024) in [1024, 2048).
+// The division w / s is the corrected (Markstein) quotient of div_f16vals, two lanes per
+// v_pk_mul_f32 / v_pk_fma_f32 (scalar operands broadcast by op_sel_hi).
+constexpr float BIAS = 1536.0f;
+
+__device__ __forceinline__ f2 opaque2(f2 x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ f2 pk_div_f16vals(f2 w, float rs1, float s1) {
+  const f2 rs = {rs1, rs1}, s = {s1, s1};
+  const f2 q0 = w * rs;
+  const f2 e = __builtin_elementwise_fma(-q0, s, w);
+  return opaque2(__builtin_elementwise_fma(e, rs, q0));
+}
+// both halves clamped to [bounds.lo, bounds.hi]
+__device__ __forceinline__ h2 pk_clamp_bc(h2 u, uint32_t bounds) {
+  h2 r;
+  asm("v_pk_max_f16 %0, %1, %2 op_sel_hi:[1,0]\n\t"
+      "v_pk_min_f16 %0, %0, %2 op_sel:[0,1]"
+      : "=&v"(r) : "v"(u), "v"(bounds));
+  return r;
+}
+// d * (s_lo, s_lo)
+__device__ __forceinline__ h2 pk_mul_bc_lo(h2 d, uint32_t s) {
+  h2 r;
+  asm("v_pk_mul_f16 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(d), "v"(s));
+  return r;
+}
+
+// Per-group words of the biased path, built once per group by the lane that owns its parameters.
+struct BiasedWords {
+  uint32_t bounds;  // fp16 (B + lo - z) | (B + hi - z) << 16
+  uint32_t sz;      // fp16 s | z << 16 (the stored scale / zero bits)
+  uint32_t kc;      // fp16 (z + off - B + 1024) in both halves (codes)
+  // RN(1/s) and s in fp32.  Kept as two scalars, never an f2: ROCm 7.2's LLVM merged the DPP
+  // broadcasts of the two halves of an f2 into ONE (both lanes got .x) -- a silent miscompile.
+  float rs, s;
+};
+template <bool SYM>
+__device__ __forceinline__ BiasedWords biased_words(const GroupParams& p, int n_bits) {
+  BiasedWords b;
+  const uint32_t lo = Fmt<DT_F16>::from_f(BIAS + p.lo - p.z), hi = Fmt<DT_F16>::from_f(BIAS + p.hi - p.z);
+  b.bounds = lo | (hi << 16);
+  b.sz = Fmt<DT_F16>::from_f(p.s) | (Fmt<DT_F16>::from_f(p.z) << 16);
+  const float off = SYM ? (float)(1u << (n_bits - 1)) : 0.0f;
+  const uint32_t k = Fmt<DT_F16>::from_f(p.z + off - BIAS + 1024.0f);
+  b.kc = k | (k << 16);
+  b.rs = p.rs;
+  b.s = p.s;
+  return b;
+}
+
+// Two fp16 weights -> two dequantized fp16 (bits); cpair receives the codes (CODES only).
+template <int CODES>
+__device__ __forceinline__ uint32_t quant2_biased(uint32_t wpair, const BiasedWords& b, uint32_t& cpair) {
+  const f2 w = __builtin_convertvector(as_h2(wpair), f2);
+  const h2 t = __builtin_convertvector(pk_div_f16vals(w, b.rs, b.s), h2);
+  const h2 bias = {(_Float16)BIAS, (_Float16)BIAS};
+  const h2 u = pk_clamp_bc(t + bias, b.bounds);
+  if constexpr (CODES != 0) cpair = as_u32(u + as_h2(b.kc)) & 0x03FF03FFu;
+  return as_u32(pk_mul_bc_lo(u - bias, b.sz));
+}
+
 // Store the codes of 8 consecutive elements (element index elem0, multiple of 8):
 // CODES == 4: 4 B (low nibble = even element), CODES == 8: 8 B.
 template <int CODES>

@@ -134,6 +134,84 @@ __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<
   return r.valid && any_nan;
 }
 
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, CTRL, 0xF, 0xF, false);
+}
+template <int K, int CODES>
+__device__ __forceinline__ BiasedWords bcast_words_k(const BiasedWords& w) {
+  constexpr int C = K * 0x55;  // quad_perm [K,K,K,K]
+  BiasedWords b;
+  b.bounds = dpp_u32<C>(w.bounds);
+  b.sz = dpp_u32<C>(w.sz);
+  b.rs = __builtin_bit_cast(float, dpp_u32<C>(__builtin_bit_cast(uint32_t, w.rs)));
+  b.s = __builtin_bit_cast(float, dpp_u32<C>(__builtin_bit_cast(uint32_t, w.s)));
+  b.kc = CODES != 0 ? dpp_u32<C>(w.kc) : 0u;
+  return b;
+}
+// the words of unit k of this lane's group (held by lane k of the quad)
+template <int CODES>
+__device__ __forceinline__ BiasedWords bcast_words(const BiasedWords& w, int k) {
+  switch (k) {
+    case 0: return bcast_words_k<0, CODES>(w);
+    case 1: return bcast_words_k<1, CODES>(w);
+    case 2: return bcast_words_k<2, CODES>(w);
+    default: return bcast_words_k<3, CODES>(w);
+  }
+}
+
+// One iteration of NU (<= UNROLL) units of an fp16 tensor with SHARED group parameters: the
+// NU x (64 / LPG) groups of the iteration get their parameters from ONE pass of the parameter
+// math (lane l computes unit (l % UNROLL) of its own group), instead of one pass per unit in which
+// every lane of a group repeats it; each unit then takes its group's words from lane k of the quad
+// by DPP broadcast (quads never straddle a group: LPG >= 4).  Elementwise: quant2_biased.
+// Returns false (nothing stored) when some group of the iteration is not on the fast path or
+// n_bits > 9; the caller then runs the per-unit path.
+template <int G, bool SYM, int CODES, int UNROLL, bool NTS>
+__device__ __forceinline__ bool iter_shared_f16(const GroupTensor& t, int64_t e0, int32_t nu,
+                                                const Vec8<DT_F16> (&v)[UNROLL], int lane, int n_bits,
+                                                float rmax) {
+  static_assert(G >= 32 && (UNROLL == 1 || UNROLL == 2 || UNROLL == 4), "quad broadcast layout");
+  constexpr int LPG = G / 8;
+  int32_t mn[UNROLL], mx[UNROLL];
+#pragma unroll
+  for (int k = 0; k < UNROLL; ++k) {
+    minmax8<DT_F16, SYM>(v[k], mn[k], mx[k]);
+    if constexpr (SYM) group_max<LPG>(mx[k]);
+    else group_minmax<LPG>(mn[k], mx[k]);
+  }
+  const int kk = lane & (UNROLL - 1);
+  int32_t smn = mn[0], smx = mx[0];
+#pragma unroll
+  for (int k = 1; k < UNROLL; ++k) {
+    if (kk == k) { smn = mn[k]; smx = mx[k]; }
+  }
+  const GroupParams p = params_from_keys<DT_F16, SYM>(smn, smx, n_bits, rmax);
+  if (n_bits > 9 || __ballot(kk < nu && !p.fast) != 0) return false;
+  const BiasedWords bw = biased_words<SYM>(p, n_bits);
+#pragma unroll
+  for (int k = 0; k < UNROLL; ++k) {
+    if (k < nu) {
+      const BiasedWords b = bcast_words<CODES>(bw, k);
+      Vec8<DT_F16> o;
+      uint32_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o.u[j] = quant2_biased<CODES>(v[k].u[j], b, c[j]);
+      const int64_t e = e0 + (int64_t)k * UNIT;
+      if (e < t.numel) {
+        if (t.out) o.template store<NTS>(static_cast<char*>(t.out) + e * 2);
+        if constexpr (CODES != 0) store_codes8<CODES>(static_cast<uint8_t*>(t.codes), e, c);
+        if ((lane % LPG) == 0) {
+          const int64_t gidx = e / G;
+          if (t.scales) gp<uint16_t>(t.scales)[gidx] = (uint16_t)b.sz;
+          if (!SYM && t.zeros) gp<uint16_t>(t.zeros)[gidx] = (uint16_t)(b.sz >> 16);
+        }
+      }
+    }
+  }
+  return true;
+}
+
 // Persistent launch; wave w owns the contiguous unit range [w*per, (w+1)*per) and walks it in
 // iterations of up to UNROLL units that never straddle two tensors, so one iteration has ONE
 // (wave-uniform, SGPR-resident) tensor descriptor and the lane offsets of its units differ by
@@ -204,7 +282,7 @@ __device__ __forceinline__ void load_iter(const Iter& it, Vec8<DT> (&v)[UNROLL])
 // occupancy API still answers 8 (MI355X_MICROARCH.md "Residency"), and this persistent grid is
 // sized for full residency.
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
-          bool NTS = true>
+          bool NTS = true, bool SHARED = true>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -225,6 +303,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_
     it.e0 = (u0 - cursor.begin) * UNIT + (int64_t)lane * 8;
   };
   auto compute_iter = [&](const Iter& it, const Vec8<DT> (&v)[UNROLL]) {
+    if constexpr (SHARED && DT == DT_F16 && G >= 32 && (UNROLL == 1 || UNROLL == 2 || UNROLL == 4)) {
+      if (iter_shared_f16<G, SYM, CODES, UNROLL, NTS>(it.t, it.e0, it.n, v, lane, a.n_bits, rmax)) return;
+    }
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       if (k < it.n) {
@@ -653,14 +734,14 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
 
 // Single tensors (QuantLinear / pseudo_quantize_tensor, a few iterations per wave) run with the
-// next iteration's loads prefetched and plain (temporal) loads; the whole-model batched walk
-// (hundreds of iterations per wave) with non-temporal loads and no prefetch.  Both picked by
-// in-run A/B (tools/ab_single.py, bench.py --variants; profiles/r01_ab_*).
+// next iteration's loads prefetched; the whole-model batched walk (hundreds of iterations per
+// wave) without.  Both with non-temporal loads.  Picked by cold in-run A/B (tools/ab_single.py
+// rotating over >= 1 GB of distinct tensors, bench.py --variants; profiles/r01_ab_*).
 template <int DT, int G, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   constexpr int UNROLL = 4;
   static int cache[64] = {0};
-  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ BATCHED>;
+  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ true>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
@@ -672,10 +753,10 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
 
 // Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
 // selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
-template <int UNROLL, bool PF, bool NTL, bool NTS>
+template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true>
 hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
   static int cache[64] = {0};
-  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS>;
+  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS, SHARED>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
@@ -725,12 +806,12 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
   switch (v) {
     case 1: return launch_variant_t<4, true, true, true>(a, st);
     case 2: return launch_variant_t<4, true, false, true>(a, st);
-    case 3: return launch_variant_t<4, true, true, false>(a, st);
-    case 4: return launch_variant_t<4, true, false, false>(a, st);
-    case 5: return launch_variant_t<8, false, true, true>(a, st);
-    case 6: return launch_variant_t<2, true, true, true>(a, st);
+    case 3: return launch_variant_t<4, false, true, true, false>(a, st);   // per-unit parameters (r1 default)
+    case 4: return launch_variant_t<2, true, true, true>(a, st);
+    case 5: return launch_variant_t<8, false, true, true>(a, st);          // per-unit (UNROLL 8)
+    case 6: return launch_variant_t<2, false, true, true>(a, st);
     case 7: return launch_variant_t<4, false, false, false>(a, st);
-    case 8: return launch_variant_t<8, true, true, true>(a, st);
+    case 8: return launch_variant_t<4, true, false, true, false>(a, st);   // per-unit, single-tensor r1 default
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
