@@ -68,11 +68,23 @@ def init_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU (RCCL); IWQ_DIST_BACKEND=gloo with more ranks than GPUs rehearses the
+        # multi-rank path on a 1-GPU box (ranks share devices round-robin)
+        backend = os.environ.get("IWQ_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
+
+
+def coll_device():
+    import torch.distributed as dist
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
 
 
 def barrier(ws):
@@ -85,7 +97,7 @@ def max_over_ranks(x, ws):
     if ws == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=coll_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -336,7 +348,7 @@ def main():
     total_numel = numel
     if ws_n > 1:
         import torch.distributed as dist
-        t = torch.tensor([numel], dtype=torch.int64, device="cuda")
+        t = torch.tensor([numel], dtype=torch.int64, device=coll_device())
         dist.all_reduce(t)
         total_numel = int(t.item())
     in_bytes = numel * 2

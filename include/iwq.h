@@ -146,6 +146,34 @@ int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld
                            void* stream);
 
 /*
+ * Decode tables for the FP paths (no reference counterpart: an execution aid).  On a finite group
+ * the fake-quantized value of an element is sign | T[|t|] (times scale, plus zero) where t is its
+ * clamped normalized fp16 value; iwq_fp_build_lut writes T (fp16 magnitudes, at most
+ * IWQ_FP_LUT_BYTES, 16-B aligned) for one format, computed on the device by the exact codec.
+ * The *_lut entry points take such a table (built with the SAME codec / exp / mant / approximate
+ * parameters) and read it through LDS instead of running the bit-level codec per element; lut NULL
+ * is the plain entry point.  Packed codes (out_codes) always take the ALU codec.
+ * codec: IWQ_CODEC_FP (iwq_quantize_fp), IWQ_CODEC_GRID (iwq_fp4_grid; exp/mant ignored),
+ * IWQ_CODEC_APX (iwq_quantize_fp_approx, single-aligned decode).
+ */
+#define IWQ_FP_LUT_BYTES 65536
+enum iwq_fp_codec { IWQ_CODEC_FP = 0, IWQ_CODEC_GRID = 1, IWQ_CODEC_APX = 2 };
+int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start, int hi_align_exp_field,
+                     int tail_pad_bits, void* lut, int64_t lut_bytes, void* stream);
+int iwq_quantize_fp_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                        int mant_bits, int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out,
+                        void* out_codes, void* out_scales, void* out_zeros, void* workspace, int64_t workspace_bytes,
+                        uint32_t* nan_flag, unsigned flags, void* stream, const void* lut);
+int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                               int mant_bits, int64_t group, int quant_dim, int hi_align_start,
+                               int hi_align_exp_field, int tail_pad_bits, int double_approx, void* out_deq,
+                               int64_t ld_out, void* out_scales, void* workspace, int64_t workspace_bytes,
+                               uint32_t* nan_flag, unsigned flags, void* stream, const void* lut);
+int iwq_fp4_grid_lut(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                     void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                     void* stream, const void* lut);
+
+/*
  * QuantLinear.quantize_weight, weight_format "bfp" (quant_linear.py:648-723): block floating point
  * with a shared per-group exponent (max fp16 exponent field of the group) and min(w_bit-1, 11)
  * mantissa bits incl. the leading one (round-half-up, saturating).  dtype F16 / BF16 / F32 (taken to

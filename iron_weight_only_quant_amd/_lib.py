@@ -28,7 +28,11 @@ EXPORTS = (
     "iwq_fill_synthetic", "iwq_status_string", "iwq_last_hip_error", "iwq_build_info",
     "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
     "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
+    "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
 )
+
+IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX = 0, 1, 2
+IWQ_FP_LUT_BYTES = 65536
 
 
 class IwqBatchEntry(ctypes.Structure):
@@ -92,6 +96,14 @@ def load():
         lib.iwq_quantize_fp_approx.restype = i32
         lib.iwq_quantize_bfp.argtypes = [vp, i64, i64, i64, i32, i32, i64, i32, vp, i64, u32, vp]
         lib.iwq_quantize_bfp.restype = i32
+        lib.iwq_fp_build_lut.argtypes = [i32, i32, i32, i32, i32, i32, vp, i64, vp]
+        lib.iwq_fp_build_lut.restype = i32
+        lib.iwq_quantize_fp_lut.argtypes = lib.iwq_quantize_fp.argtypes + [vp]
+        lib.iwq_quantize_fp_lut.restype = i32
+        lib.iwq_fp4_grid_lut.argtypes = lib.iwq_fp4_grid.argtypes + [vp]
+        lib.iwq_fp4_grid_lut.restype = i32
+        lib.iwq_quantize_fp_approx_lut.argtypes = lib.iwq_quantize_fp_approx.argtypes + [vp]
+        lib.iwq_quantize_fp_approx_lut.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]
         lib.iwq_selftest_division.restype = i32
         _lib = lib

@@ -51,7 +51,80 @@ struct FpArgs {
   int64_t total_units;
   FpSpec f;
   uint32_t* nan_flag;
+  const uint16_t* lut;  // decode table (iwq_fp_build_lut) or null: ALU codec
+  int32_t lut_n8;       // table entries, rounded up to a multiple of 8
 };
+
+// ---------------------------------------------------------------------------------------------
+// Decode tables.  On a finite group every element's fake-quantized value is
+//   sign(t) | T[|t|]   (times s, plus z)
+// where t = clamp(RN16(w / s)) is an fp16 value in [-bound, bound] and T maps each fp16 magnitude
+// to the fp16 magnitude of its decoded code: RN16(_fp_to_float(_float_to_fp(|t|))) (FP),
+// RN16(_fp_decode_aligned(code)) (approximate), RN16(q) of fp4_quantize_cpu._fp_scale (grid).
+// T is built once per format on the device by the exact ALU codec (fp_encode / fp_decode, the
+// log2 threshold tables) and staged into LDS by every workgroup of the table kernel: one LDS read
+// per element replaces ~20 VALU ops of the bit-level codec.
+// Sign: FP and approximate codes of t == +-0 are code 0 -> +0, every other t keeps its sign (a
+// sign-only code decodes to -0); the grid keeps the sign of t always (rint(-0) = -0).
+// ---------------------------------------------------------------------------------------------
+constexpr int LUT_BLOCK = 512;
+constexpr int LUT_MAX = 32768;
+
+__host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
+  return codec == CODEC_GRID ? 0x4600u /* 6.0 */ : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f.fp_max16);
+}
+
+template <int CODEC>
+__global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut, int32_t n, int32_t n8) {
+  __shared__ uint16_t tab_buf[120];
+  const Log2Tabs tabs = stage_log2_tables(tab_buf);
+  for (int32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n8; i += gridDim.x * BLOCK) {
+    float d = 0.0f;
+    if (i < n && i > 0) {
+      const uint32_t u = (uint32_t)i;
+      if constexpr (CODEC == CODEC_GRID) {  // fp4_quantize_cpu.py:37-44 on u = |x / S| (grid_elem)
+        const float uv = (float)__builtin_bit_cast(_Float16, (uint16_t)u);
+        int ls = fp16_floor_log2_torch(u, tabs.p1) + 1;
+        ls = ls < 1 ? 1 : ls;
+        const float sc = __builtin_ldexpf(1.0f, ls - 2);
+        d = __builtin_rintf(uv / sc) * sc;
+      } else if constexpr (CODEC == CODEC_APX) {
+        d = fp_decode_aligned(fp_encode(u, f, tabs), f);
+      } else {
+        d = fp_decode(fp_encode(u, f, tabs), f);
+      }
+    }
+    lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
+  }
+}
+
+typedef __attribute__((address_space(3))) const char lds_char;
+typedef __attribute__((address_space(3))) const _Float16 lds_h;
+
+// Two fp16 weights of a finite group -> two fake-quantized fp16 values through the LDS table.
+template <int CODEC, bool SYM>
+__device__ __forceinline__ uint32_t fp_pair_lut(uint32_t wpair, const FpParams& p, h2 bound2, lds_char* lut) {
+  const h2 s16 = h2{(_Float16)p.s, (_Float16)p.s};
+  const h2 z16 = h2{(_Float16)p.z, (_Float16)p.z};
+  h2 d = as_h2(wpair);
+  if constexpr (!SYM) d = d - z16;                     // RN16(w - z)
+  const f2 df = __builtin_convertvector(d, f2);
+  h2 t = __builtin_convertvector(pk_div_f16vals(df, p.rs, p.s), h2);  // RN16(d / s)
+  t = pk_max(pk_min(t, bound2), -bound2);
+  const uint32_t tb = as_u32(t);
+  const uint32_t a2 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, tb) << (u16x2)1);  // 2|t| per half
+  const h2 r = {*(lds_h*)(lut + (a2 & 0xFFFFu)), *(lds_h*)(lut + (a2 >> 16))};
+  uint32_t rb = as_u32(r);
+  if constexpr (CODEC == CODEC_GRID) {
+    rb |= tb & 0x80008000u;
+  } else {  // sign where |t| != 0: bit 15 of (tb + 0x7FFF) is clear exactly for negative nonzero t
+    const uint32_t sum = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, tb) + (u16x2)0x7FFF);
+    rb |= tb & ~sum & 0x80008000u;
+  }
+  h2 y = as_h2(rb) * s16;                              // RN16(exact product)
+  if constexpr (!SYM) y = y + z16;                     // RN16(exact sum)
+  return as_u32(y);
+}
 
 __device__ __forceinline__ void fp_flag_nan(uint32_t* nan_flag, bool any_nan) {
   uint64_t m = __ballot(any_nan);
@@ -171,6 +244,74 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
   fp_flag_nan(a.nan_flag, any_nan);
 }
 
+// k_fp_group with the decode table in LDS (no packed codes): 512-thread workgroups, each stages the
+// table (<= 48 KB for E4M3) once; finite groups take fp_pair_lut, the rest the exact ALU chain.
+template <int CODEC, int G, bool SYM>
+__global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
+  using F = Fmt<DT_F16>;
+  extern __shared__ u32x4 lut_dyn[];
+  __shared__ uint16_t tab_buf[120];
+  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_BLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
+  const Log2Tabs tabs = stage_log2_tables(tab_buf);  // its barrier also publishes the table
+  lds_char* lut = (lds_char*)lut_dyn;
+  constexpr int WPBL = LUT_BLOCK / WAVE;
+  constexpr int UNROLL = 4;
+  constexpr int LPG = G / 8;
+  constexpr bool RED_SYM = SYM || CODEC != CODEC_FP;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * WPBL + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * WPBL;
+  int64_t per = (a.total_units + nwaves - 1) / nwaves;
+  per = (per + UNROLL - 1) / UNROLL * UNROLL;
+  const int64_t ubeg = wave * per;
+  const int64_t uend = min(ubeg + per, a.total_units);
+  const _Float16 bnd = __builtin_bit_cast(_Float16, (uint16_t)lut_bound_bits(CODEC, a.f));
+  const h2 bound2 = {bnd, bnd};
+  bool any_nan = false;
+  for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+    Vec8<DT_F16> v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
+      const bool ok = (u0 + k < uend) && e < a.numel;
+      v[k].load(a.w + (ok ? e : 0) * F::BYTES);
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      if (u0 + k >= uend) break;
+      const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
+      int32_t mn, mx;
+      minmax8<DT_F16, RED_SYM>(v[k], mn, mx);
+      if constexpr (RED_SYM) group_max<LPG>(mx);
+      else group_minmax<LPG>(mn, mx);
+      const FpParams p = fp_group_params<CODEC, SYM>(mn, mx, a.f);
+      Vec8<DT_F16> o;
+      bool nan8 = false;
+      if (p.fast && p.s > 0.0f) {  // finite group (grid: S > 0): table path, no NaN possible
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o.u[j] = fp_pair_lut<CODEC, SYM>(v[k].u[j], p, bound2, lut);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          uint32_t c;
+          const float y = fp_elem<CODEC, SYM, false>(F::to_f(v[k].get(i)), p, a.f, c, tabs);
+          nan8 |= (y != y);
+          o.set(i, F::from_f(y));
+        }
+      }
+      if (e0 < a.numel) {
+        any_nan |= nan8;
+        if (a.out) o.store(a.out + e0 * F::BYTES);
+        if ((lane % LPG) == 0) {
+          if (a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
+          if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, e0 / G, p.z);
+        }
+      }
+    }
+  }
+  fp_flag_nan(a.nan_flag, any_nan);
+}
+
 template <int CODEC, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
   using F = Fmt<DT_F16>;
@@ -249,7 +390,41 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+template <int CODEC, int G, bool SYM>
+hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
+  auto kern = k_fp_group_lut<CODEC, G, SYM>;
+  const size_t lds = (size_t)a.lut_n8 * 2;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
+  constexpr int WPBL = LUT_BLOCK / WAVE;
+  int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
+  const int64_t cap = (int64_t)cu_count() * occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int CODEC, bool SYM>
+hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
+  switch (g) {
+    case 8: return launch_fp_lut_t<CODEC, 8, SYM>(a, st);
+    case 16: return launch_fp_lut_t<CODEC, 16, SYM>(a, st);
+    case 32: return launch_fp_lut_t<CODEC, 32, SYM>(a, st);
+    case 64: return launch_fp_lut_t<CODEC, 64, SYM>(a, st);
+    case 128: return launch_fp_lut_t<CODEC, 128, SYM>(a, st);
+    case 256: return launch_fp_lut_t<CODEC, 256, SYM>(a, st);
+    case 512: return launch_fp_lut_t<CODEC, 512, SYM>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpArgs& a, hipStream_t st) {
+  if (a.lut && codes == 0) {
+    if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true>(g, a, st);
+    if (codec == CODEC_APX) return launch_fp_lut_g<CODEC_APX, true>(g, a, st);
+    return sym ? launch_fp_lut_g<CODEC_FP, true>(g, a, st) : launch_fp_lut_g<CODEC_FP, false>(g, a, st);
+  }
   if (codec == CODEC_GRID) return launch_fp_group_g<CODEC_GRID, true, 0>(g, a, st);
   if (codec == CODEC_APX) return launch_fp_group_g<CODEC_APX, true, 0>(g, a, st);
   if (sym) {
@@ -311,7 +486,7 @@ int fp_spec(int exp_bits, int mant_bits, FpSpec& f) {
 int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
            int mant_bits, int64_t group, int symmetric, int quant_dim, void* out, int64_t ld_out, void* codes_out,
            void* scales, void* zeros, void* ws, int64_t ws_bytes, uint32_t* nan_flag, unsigned flags,
-           void* stream, int hs = 0, int hf = 0, int tp = 0) {
+           void* stream, int hs = 0, int hf = 0, int tp = 0, const void* lut = nullptr) {
   if (dtype != IWQ_F16) return IWQ_ERR_DTYPE;
   if (!w) return IWQ_ERR_ARG;
   if (rows <= 0 || cols <= 0 || ld_w < cols || (out && ld_out < cols)) return IWQ_ERR_SHAPE;
@@ -359,6 +534,11 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
     a.total_units = (a.numel + UNIT - 1) / UNIT;
     a.f = f;
     a.nan_flag = nan_flag;
+    if (lut) {
+      if (!aligned16p(lut)) return IWQ_ERR_ARG;
+      a.lut = static_cast<const uint16_t*>(lut);
+      a.lut_n8 = (int32_t)((lut_bound_bits(codec, f) + 1 + 7) / 8 * 8);
+    }
     IWQ_HIP_FP(launch_fp_group(codec, group, sym, codes, a, s));
     return IWQ_OK;
   }
@@ -460,17 +640,17 @@ int64_t iwq_approx_workspace_bytes(int64_t rows, int64_t cols, int exp_bits, int
   return round256(8 * G) + (double_approx ? apx_codes_bytes(rows, cols, exp_bits, mant_bits) : 0);
 }
 
-int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
-                           int mant_bits, int64_t group, int quant_dim, int hi_align_start, int hi_align_exp_field,
-                           int tail_pad_bits, int double_approx, void* out_deq, int64_t ld_out, void* out_scales,
-                           void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
-                           void* stream) {
+int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                               int mant_bits, int64_t group, int quant_dim, int hi_align_start,
+                               int hi_align_exp_field, int tail_pad_bits, int double_approx, void* out_deq,
+                               int64_t ld_out, void* out_scales, void* workspace, int64_t workspace_bytes,
+                               uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
   if (group <= 0) return IWQ_ERR_GROUP_MODE;  // approximate needs w_group_size > 0 (ValueError)
   if (!out_deq || !out_scales) return IWQ_ERR_ARG;
   if (!double_approx)
     return run_fp(CODEC_APX, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
                   nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, flags, stream, hi_align_start,
-                  hi_align_exp_field, tail_pad_bits);
+                  hi_align_exp_field, tail_pad_bits, lut);
   if (rows <= 0 || cols <= 0 || ld_out < cols) return IWQ_ERR_SHAPE;
   const int64_t vr = quant_dim == 1 ? cols : rows, vc = quant_dim == 1 ? rows : cols;
   if (vc % group != 0) return IWQ_ERR_GROUP;
@@ -509,22 +689,72 @@ int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld
   return IWQ_OK;
 }
 
+int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                           int mant_bits, int64_t group, int quant_dim, int hi_align_start, int hi_align_exp_field,
+                           int tail_pad_bits, int double_approx, void* out_deq, int64_t ld_out, void* out_scales,
+                           void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                           void* stream) {
+  return iwq_quantize_fp_approx_lut(w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, quant_dim,
+                                    hi_align_start, hi_align_exp_field, tail_pad_bits, double_approx, out_deq, ld_out,
+                                    out_scales, workspace, workspace_bytes, nan_flag, flags, stream, nullptr);
+}
+
+int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start, int hi_align_exp_field,
+                     int tail_pad_bits, void* lut, int64_t lut_bytes, void* stream) {
+  if (codec != CODEC_FP && codec != CODEC_GRID && codec != CODEC_APX) return IWQ_ERR_ARG;
+  if (codec == CODEC_GRID) { exp_bits = 2; mant_bits = 1; }
+  FpSpec f{};
+  const int st = fp_spec(exp_bits, mant_bits, f);
+  if (st != IWQ_OK) return st;
+  f.hs = hi_align_start;
+  f.hf = hi_align_exp_field;
+  f.tp = tail_pad_bits;
+  const int32_t n = (int32_t)lut_bound_bits(codec, f) + 1;
+  const int32_t n8 = (n + 7) / 8 * 8;
+  if (!lut || !aligned16p(lut) || lut_bytes < (int64_t)n8 * 2 || n8 > LUT_MAX) return IWQ_ERR_WORKSPACE;
+  const unsigned blocks = (unsigned)((n8 + BLOCK - 1) / BLOCK);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint16_t* t = static_cast<uint16_t*>(lut);
+  if (codec == CODEC_GRID) hipLaunchKernelGGL(k_fp_build_lut<CODEC_GRID>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
+  else if (codec == CODEC_APX) hipLaunchKernelGGL(k_fp_build_lut<CODEC_APX>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
+  else hipLaunchKernelGGL(k_fp_build_lut<CODEC_FP>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
+  IWQ_HIP_FP(hipGetLastError());
+  return IWQ_OK;
+}
+
+int iwq_quantize_fp_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+                        int mant_bits, int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out,
+                        void* out_codes, void* out_scales, void* out_zeros, void* workspace, int64_t workspace_bytes,
+                        uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
+  return run_fp(CODEC_FP, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, symmetric, quant_dim, out_deq,
+                ld_out, out_codes, out_scales, out_zeros, workspace, workspace_bytes, nan_flag, flags, stream, 0, 0, 0,
+                lut);
+}
+
 int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits, int mant_bits,
                     int64_t group, int symmetric, int quant_dim, void* out_deq, int64_t ld_out, void* out_codes,
                     void* out_scales, void* out_zeros, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag,
                     unsigned flags, void* stream) {
-  return run_fp(CODEC_FP, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, symmetric, quant_dim, out_deq,
-                ld_out, out_codes, out_scales, out_zeros, workspace, workspace_bytes, nan_flag, flags, stream);
+  return iwq_quantize_fp_lut(w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, symmetric, quant_dim, out_deq,
+                             ld_out, out_codes, out_scales, out_zeros, workspace, workspace_bytes, nan_flag, flags,
+                             stream, nullptr);
+}
+
+int iwq_fp4_grid_lut(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                     void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
+                     void* stream, const void* lut) {
+  // grouping of fp4_quantize_cpu.py:55-60: reshape(-1, g) when g > 0, then (1, -1) when per_tensor,
+  // else rows of the 2-D input
+  const int64_t g = per_tensor ? IWQ_GROUP_PER_TENSOR : (group > 0 ? group : IWQ_GROUP_PER_CHANNEL);
+  return run_fp(CODEC_GRID, w, rows, cols, cols, IWQ_F16, 2, 1, g, 1, 0, out, cols, nullptr, out_scales, nullptr,
+                workspace, workspace_bytes, nan_flag, flags, stream, 0, 0, 0, lut);
 }
 
 int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
                  void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
                  void* stream) {
-  // grouping of fp4_quantize_cpu.py:55-60: reshape(-1, g) when g > 0, then (1, -1) when per_tensor,
-  // else rows of the 2-D input
-  const int64_t g = per_tensor ? IWQ_GROUP_PER_TENSOR : (group > 0 ? group : IWQ_GROUP_PER_CHANNEL);
-  return run_fp(CODEC_GRID, w, rows, cols, cols, IWQ_F16, 2, 1, g, 1, 0, out, cols, nullptr, out_scales, nullptr,
-                workspace, workspace_bytes, nan_flag, flags, stream);
+  return iwq_fp4_grid_lut(w, rows, cols, group, per_tensor, out, out_scales, workspace, workspace_bytes, nan_flag,
+                          flags, stream, nullptr);
 }
 
 }  // extern "C"

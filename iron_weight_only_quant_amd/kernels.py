@@ -127,13 +127,46 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
     return QuantResult(out, scales, zeros, codes, nan_flag)
 
 
+class _LutCache:
+    """Per-device FP decode tables (include/iwq.h iwq_fp_build_lut), built once per format on first
+    use and reused by every later call.  Returns None (plain ALU codec) while a CUDA graph is being
+    captured and the table does not exist yet: a table allocated inside a capture would belong to
+    the graph's private pool."""
+
+    def __init__(self):
+        self.tabs = {}
+
+    def get(self, dev, codec, exp_bits=0, mant_bits=0, hs=0, hf=0, tp=0):
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        key = (idx, codec, exp_bits, mant_bits, hs, hf, tp)
+        t = self.tabs.get(key)
+        if t is not None:
+            return t
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = torch.empty(L.IWQ_FP_LUT_BYTES, dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            st = L.load().iwq_fp_build_lut(int(codec), int(exp_bits), int(mant_bits), int(hs), int(hf), int(tp),
+                                           L.ptr(t), t.numel(), L.stream_handle(dev))
+        if st != L.IWQ_OK:  # a format the table path does not cover: plain codec
+            return None
+        torch.cuda.current_stream(dev).synchronize()  # once per format: visible to every stream
+        self.tabs[key] = t
+        return t
+
+
+_luts = _LutCache()
+
+
 def fp_code_nbytes(rows, cols, exp_bits, mant_bits):
     return rows * (cols // 2) if (1 + exp_bits + mant_bits) <= 4 else rows * cols
 
 
 def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symmetric: bool, quant_dim: int = 0,
-                out: Optional[torch.Tensor] = None, want_codes: bool = False, flags: int = 0) -> QuantResult:
-    """FP4/FP6/FP8 fake quantization of an fp16 2-D weight (QuantLinear FP branches) on the GPU."""
+                out: Optional[torch.Tensor] = None, want_codes: bool = False, flags: int = 0,
+                use_lut: bool = True) -> QuantResult:
+    """FP4/FP6/FP8 fake quantization of an fp16 2-D weight (QuantLinear FP branches) on the GPU.
+    use_lut: decode through the per-format LDS table (same bits; False = bit-level ALU codec)."""
     L.require_device(w)
     if w.dim() != 2:
         raise AssertionError("weight must be 2-D")
@@ -154,11 +187,12 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     nan_flag = _flags.take(dev)
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    lut = _luts.get(dev, L.IWQ_CODEC_FP, exp_bits, mant_bits) if use_lut else None
     with torch.cuda.device(dev):
-        st = lib.iwq_quantize_fp(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
-                                 int(group), int(bool(symmetric)), int(quant_dim), L.ptr(out), out.stride(0),
-                                 L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag),
-                                 int(flags), L.stream_handle(dev))
+        st = lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
+                                     int(group), int(bool(symmetric)), int(quant_dim), L.ptr(out), out.stride(0),
+                                     L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag),
+                                     int(flags), L.stream_handle(dev), L.ptr(lut))
     _raise_for(st, "iwq_quantize_fp")
     return QuantResult(out, scales, zeros, codes, nan_flag)
 
@@ -166,7 +200,7 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
 def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, quant_dim: int = 0,
                        hi_align_start: int = 12, hi_align_exp_field: int = 15, tail_pad_bits: int = 1,
                        double_approx: bool = False, out: Optional[torch.Tensor] = None,
-                       flags: int = 0) -> QuantResult:
+                       flags: int = 0, use_lut: bool = True) -> QuantResult:
     """QuantLinear.quantize_weight_approximate arithmetic (quant_linear.py:470-632) on an fp16 weight:
     symmetric absmax FP codes, aligned / double-approximate decode, RN16(decoded * scale)."""
     L.require_device(w)
@@ -191,12 +225,14 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     wsb = int(lib.iwq_approx_workspace_bytes(rows, cols, int(exp_bits), int(mant_bits), int(group), int(quant_dim),
                                              int(bool(double_approx))))
     ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+    lut = (_luts.get(dev, L.IWQ_CODEC_APX, exp_bits, mant_bits, hi_align_start, hi_align_exp_field, tail_pad_bits)
+           if use_lut and not double_approx else None)
     with torch.cuda.device(dev):
-        st = lib.iwq_quantize_fp_approx(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
-                                        int(group), int(quant_dim), int(hi_align_start), int(hi_align_exp_field),
-                                        int(tail_pad_bits), int(bool(double_approx)), L.ptr(out), out.stride(0),
-                                        L.ptr(scales), L.ptr(ws), ws.numel(), L.ptr(nan_flag), int(flags),
-                                        L.stream_handle(dev))
+        st = lib.iwq_quantize_fp_approx_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
+                                            int(mant_bits), int(group), int(quant_dim), int(hi_align_start),
+                                            int(hi_align_exp_field), int(tail_pad_bits), int(bool(double_approx)),
+                                            L.ptr(out), out.stride(0), L.ptr(scales), L.ptr(ws), ws.numel(),
+                                            L.ptr(nan_flag), int(flags), L.stream_handle(dev), L.ptr(lut))
     _raise_for(st, "iwq_quantize_fp_approx")
     return QuantResult(out, scales, None, None, nan_flag)
 
@@ -228,7 +264,8 @@ def quantize_bfp(w: torch.Tensor, w_bit: int, group: int, quant_dim: int = 0, ou
     return out
 
 
-def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int = 0) -> QuantResult:
+def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int = 0,
+             use_lut: bool = True) -> QuantResult:
     """fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 arithmetic on the GPU; output in w's element order."""
     L.require_device(w)
     lib = L.load()
@@ -248,9 +285,11 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     nan_flag = _flags.take(dev)
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    lut = _luts.get(dev, L.IWQ_CODEC_GRID) if use_lut else None
     with torch.cuda.device(dev):
-        st = lib.iwq_fp4_grid(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out), L.ptr(scales),
-                              L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev))
+        st = lib.iwq_fp4_grid_lut(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out),
+                                  L.ptr(scales), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev),
+                                  L.ptr(lut))
     _raise_for(st, "iwq_fp4_grid")
     return QuantResult(out, scales, None, None, nan_flag)
 

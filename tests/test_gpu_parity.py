@@ -353,6 +353,70 @@ def test_fp_exhaustive_encode_decode(K, FPD, fmt):
         assert bits_equal(deq, dec[codes_exp].astype(np.float16)), (fmt, flags)
 
 
+def _scale_one_rows(vals, bound):
+    """Rows of 127 values behind a leading `bound`: with absmax == bound the group scale is exactly 1,
+    so t == the value itself and the output is the table entry (sign rules included)."""
+    per = 127
+    n = (len(vals) + per - 1) // per
+    pad = n * per - len(vals)
+    vals_p = np.concatenate([vals, np.zeros(pad, np.float16)]).reshape(n, per)
+    return np.concatenate([np.full((n, 1), bound, np.float16), vals_p], axis=1), n
+
+
+@pytest.mark.parametrize("fmt", ["e4m3", "e3m2", "e2m1"])
+def test_fp_exhaustive_lut(K, FPD, fmt):
+    """The LDS decode-table path (no codes requested) on every finite fp16 in [-fp_max, fp_max],
+    +-0 included: dequantized bits == _fp_to_float(_float_to_fp(x)) (reference tables) and == the
+    bit-level ALU codec (use_lut=False)."""
+    from oracle import fp_codec as C
+    e, m = FPF[fmt]
+    _, fp_max = C.fp_params(e, m)
+    xs = FPD["in/all_fp16"]
+    enc, dec = FPD[f"enc/{fmt}"], FPD[f"dec/{fmt}"]
+    sel = np.abs(xs.astype(np.float32)) <= fp_max
+    vals, codes_exp = xs[sel], enc[sel]
+    rows, n = _scale_one_rows(vals, fp_max)
+    x = to_dev(rows, "float16")
+    r_lut = K.quantize_fp(x, e, m, 128, True, 0)
+    r_alu = K.quantize_fp(x, e, m, 128, True, 0, use_lut=False)
+    assert torch.all(r_lut.scales == 1)
+    deq = to_np(r_lut.out)[:, 1:].reshape(-1)[: len(vals)]
+    assert bits_equal(deq, dec[codes_exp].astype(np.float16)), fmt
+    assert torch.equal(r_lut.out.view(torch.int16), r_alu.out.view(torch.int16)), fmt
+    # asymmetric: zero point != 0, the same table behind (w - z) / s
+    a = K.quantize_fp(x, e, m, 128, False, 0)
+    b = K.quantize_fp(x, e, m, 128, False, 0, use_lut=False)
+    assert torch.equal(a.out.view(torch.int16), b.out.view(torch.int16)), fmt
+
+
+def test_fp4_grid_exhaustive_lut(K):
+    """Grid table path on every fp16 in [-6, 6] at S == 1 (rows with absmax 6) vs the ALU path."""
+    xs = np.arange(1 << 16, dtype=np.uint32).astype(np.uint16).view(np.float16)
+    vals = xs[np.isfinite(xs) & (np.abs(xs.astype(np.float32)) <= 6.0)]
+    rows, _ = _scale_one_rows(vals, 6.0)
+    x = to_dev(rows, "float16")
+    a = K.fp4_grid(x, 128)
+    b = K.fp4_grid(x, 128, use_lut=False)
+    assert torch.all(a.scales == 1)
+    assert torch.equal(a.out.view(torch.int16), b.out.view(torch.int16))
+
+
+@pytest.mark.parametrize("hs,hf,tp", [(12, 15, 1), (4, 7, 2), (1, 3, 0), (2, 5, -1)])
+def test_fp_approx_exhaustive_lut(K, hs, hf, tp):
+    """Approximate (single-aligned) table path on every finite fp16 in [-fp_max, fp_max] at scale 1
+    vs the ALU path, E4M3 and E2M1."""
+    from oracle import fp_codec as C
+    xs = np.arange(1 << 16, dtype=np.uint32).astype(np.uint16).view(np.float16)
+    for e, m in ((4, 3), (2, 1)):
+        _, fp_max = C.fp_params(e, m)
+        vals = xs[np.isfinite(xs) & (np.abs(xs.astype(np.float32)) <= fp_max)]
+        rows, _ = _scale_one_rows(vals, fp_max)
+        x = to_dev(rows, "float16")
+        a = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, False)
+        b = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, False, use_lut=False)
+        assert torch.equal(a.out.view(torch.int16), b.out.view(torch.int16)), (e, m, hs, hf, tp)
+
+
 @pytest.mark.parametrize("flags", FLAG_SETS)
 def test_fp_quantlinear_golden(K, FPD, flags):
     x = to_dev(FPD["in/fp_a"], "float16")

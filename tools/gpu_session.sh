@@ -64,6 +64,13 @@ if [[ $WHAT == *single* ]]; then
   step ab_single 600 python tools/ab_single.py ${SINGLE_ARGS:-}
   step ab_single_4096 600 python tools/ab_single.py --rows 4096 --cols 4096 --copies 64 ${SINGLE_ARGS:-}
 fi
+if [[ $WHAT == *dist2* ]]; then
+  # rehearsal of the multi-rank bench on a 1-GPU box: 2 ranks share cuda:0 over gloo
+  export IWQ_DIST_BACKEND=gloo
+  step dist2_7b 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
+  step dist2_70b 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --model llama2-70b --steps 3 --warmup 1
+  unset IWQ_DIST_BACKEND
+fi
 if [[ $WHAT == *pmc* ]]; then
   cd /tmp
   B="python3 $ROOT/bench.py --no-cpu-baseline --no-ppl --no-shapes --ramp-seconds 0 --steps 3 --warmup 1"
