@@ -299,6 +299,9 @@ def gemm_variant_flags(v: int) -> int:
     return (int(v) & 0xFF) << 16
 
 
+GEMV_MAX_M = 16  # iwq_w4a16_gemm takes the weight-streaming decode kernel up to this many rows
+
+
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
     g = K if group == -2 else group
     return (x.is_cuda and x.dtype == torch.float16 and 2 <= n_bits <= 4 and N % 128 == 0 and K % 128 == 0

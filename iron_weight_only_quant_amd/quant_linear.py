@@ -226,10 +226,16 @@ class QuantLinear(nn.Module):
         """quant_linear.py:960-972: the dequantized weight already sits in self.weight.
 
         With fused_forward=True (INT, 2-4 bits, quant_dim 0) the GEMM reads the packed codes instead
-        (kernels.w4a16_gemm, MFMA): same weights, fp32 accumulation in a different order."""
+        (kernels.w4a16_gemm, MFMA): same weights, fp32 accumulation in a different order.
+        fused_forward="auto" takes the packed-weight kernel only where it is the faster one: decode
+        batches (M <= 16 rows: the weight-streaming GEMV, 1.8-3.6x hipBLASLt); larger M run
+        F.linear on the resident dequantized weight, like the reference."""
         if not self.quantized:
             return F.linear(input, self.weight, self.bias)
-        if (self.fused_forward and self.weight_format == "int" and self.quant_dim == 0 and self.qweight is not None
+        fused = self.fused_forward
+        if fused == "auto":
+            fused = input.numel() // max(1, self.in_features) <= kernels.GEMV_MAX_M
+        if (fused and self.weight_format == "int" and self.quant_dim == 0 and self.qweight is not None
                 and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
                                                  self.w_group_size)
                 and (self.bias is None or self.bias.dtype == torch.float16)):

@@ -542,6 +542,23 @@ def test_quantlinear_fused_forward(K):
     torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
 
 
+def test_quantlinear_fused_forward_auto(K, monkeypatch):
+    """fused_forward="auto": the packed-weight kernel for M <= 16 rows, F.linear above."""
+    from iron_weight_only_quant_amd import quant_linear as QLm
+    calls = []
+    real = QLm.kernels.w4a16_gemm
+    monkeypatch.setattr(QLm.kernels, "w4a16_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
+    lin = torch.nn.Linear(512, 256, bias=True).half().to(DEV)
+    q = QLm.QuantLinear.from_linear(lin, w_bit=4, w_group_size=128, symmetric=False, fused_forward="auto")
+    for shape, fused in (((1, 512), True), ((2, 8, 512), True), ((4, 64, 512), False)):
+        calls.clear()
+        x = torch.randn(*shape, device=DEV).half()
+        y = q(x)
+        ref = torch.nn.functional.linear(x, q.weight, q.bias)
+        torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
+        assert bool(calls) == fused, shape
+
+
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
 def test_per_tensor_fast_path(K, dtype):
     """group -1 (per-tensor) on a tensor big enough for many partial-key workgroups, quant_dim 0 and 1,
