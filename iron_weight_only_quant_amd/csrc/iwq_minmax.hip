@@ -282,25 +282,43 @@ __device__ __forceinline__ void load_iter(const Iter& it, Vec8<DT> (&v)[UNROLL])
 // occupancy API still answers 8 (MI355X_MICROARCH.md "Residency"), and this persistent grid is
 // sized for full residency.
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
-          bool NTS = true, bool SHARED = true>
+          bool NTS = true, bool SHARED = true, bool GS = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
   const float rmax = rmax_for(a.n_bits, SYM);
-  int64_t per = (a.total_units + nwaves - 1) / nwaves;
-  per = (per + UNROLL - 1) / UNROLL * UNROLL;
-  const int64_t ubeg = wave * per;
-  const int64_t uend = min(ubeg + per, a.total_units);
+  // The walk: contiguous (one chunk [wave*per, +per) per wave) or, with GS, grid-stride chunks of
+  // UNROLL units (c*UNROLL for c = wave, wave + nwaves, ...: at any moment the grid works on one
+  // contiguous window).  u0 = next unit, cend = end of the current chunk; u0 < cend <=> work left.
+  int64_t u0, cend;
+  if constexpr (GS) {
+    u0 = wave * UNROLL;
+    cend = min(u0 + UNROLL, a.total_units);
+  } else {
+    int64_t per = (a.total_units + nwaves - 1) / nwaves;
+    per = (per + UNROLL - 1) / UNROLL * UNROLL;
+    u0 = wave * per;
+    cend = min(u0 + per, a.total_units);
+  }
+  auto advance = [&](int64_t n) {
+    u0 += n;
+    if constexpr (GS) {
+      if (u0 >= cend) {
+        u0 += (nwaves - 1) * UNROLL;
+        cend = min(u0 + UNROLL, a.total_units);
+      }
+    }
+  };
   bool any_nan = false;
   TensorCursor<BATCHED> cursor;
   cursor.init(a);
-  auto plan_iter = [&](int64_t u0, Iter& it) {
-    cursor.seek(a, u0);
-    const int64_t lim = min(uend, cursor.next);
+  auto plan_iter = [&](int64_t u, Iter& it) {
+    cursor.seek(a, u);
+    const int64_t lim = min(cend, cursor.next);
     it.t = cursor.t;
-    it.n = (int32_t)min((int64_t)UNROLL, lim - u0);
-    it.e0 = (u0 - cursor.begin) * UNIT + (int64_t)lane * 8;
+    it.n = (int32_t)min((int64_t)UNROLL, lim - u);
+    it.e0 = (u - cursor.begin) * UNIT + (int64_t)lane * 8;
   };
   auto compute_iter = [&](const Iter& it, const Vec8<DT> (&v)[UNROLL]) {
     if constexpr (SHARED && DT == DT_F16 && G >= 32 && (UNROLL == 1 || UNROLL == 2 || UNROLL == 4)) {
@@ -317,35 +335,37 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_
       }
     }
   };
-  if (ubeg >= uend) {
+  if (!(u0 < cend)) {
     flag_nan(a.nan_flag, false);
     return;
   }
   if constexpr (PF) {
     Iter itn;
     Vec8<DT> vn[UNROLL];
-    plan_iter(ubeg, itn);
+    plan_iter(u0, itn);
     load_iter<DT, UNROLL, NTL>(itn, vn);
-    for (int64_t u0 = ubeg; u0 < uend;) {
+    while (true) {
       const Iter it = itn;
       Vec8<DT> v[UNROLL];
 #pragma unroll
       for (int k = 0; k < UNROLL; ++k) v[k] = vn[k];
-      u0 += it.n;
-      if (u0 < uend) {
+      advance(it.n);
+      const bool more = u0 < cend;
+      if (more) {
         plan_iter(u0, itn);
         load_iter<DT, UNROLL, NTL>(itn, vn);
       }
       compute_iter(it, v);
+      if (!more) break;
     }
   } else {
-    for (int64_t u0 = ubeg; u0 < uend;) {
+    while (u0 < cend) {
       Iter it;
       Vec8<DT> v[UNROLL];
       plan_iter(u0, it);
       load_iter<DT, UNROLL, NTL>(it, v);
       compute_iter(it, v);
-      u0 += it.n;
+      advance(it.n);
     }
   }
   flag_nan(a.nan_flag, any_nan);
@@ -733,16 +753,17 @@ bool is_pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 int elem_bytes(int dt) { return dt == IWQ_F32 ? 4 : 2; }
 
-// Single tensors (QuantLinear / pseudo_quantize_tensor, a few iterations per wave) run with the
-// next iteration's loads prefetched; the whole-model batched walk (hundreds of iterations per
-// wave) without.  Both with non-temporal loads.  Picked by cold in-run A/B (tools/ab_single.py
-// rotating over >= 1 GB of distinct tensors, bench.py --variants; profiles/r01_ab_*).
-template <int DT, int G, bool SYM, int CODES, bool BATCHED>
-hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
-  constexpr int UNROLL = 4;
-  static int cache[64] = {0};
-  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ true>;
-  const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
+// Walk policy, picked by cold in-run A/B (tools/ab_single.py rotating over >= 1 GB of distinct
+// tensors, bench.py --variants; profiles/r01_ab_*):
+//  * whole-model batched walk (hundreds of iterations per wave): contiguous chunk per wave, no
+//    prefetch (grid-stride: 4.68 vs 4.40 ms per 7B);
+//  * single fp16 tensors of >= 2 grid-rounds (11008x4096: 34.3 vs 36.8 us): grid-stride chunks;
+//  * smaller single tensors (4096x4096, ~1 round): contiguous chunk with the next iteration's
+//    loads prefetched (14.2 vs 15.1 us).
+// All with non-temporal loads.
+template <typename Kern>
+hipError_t launch_persistent(Kern kern, int* cache, int unroll, const GroupArgs& a, hipStream_t st) {
+  const int64_t waves_needed = (a.total_units + unroll - 1) / unroll;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
   if (blocks > cap) blocks = cap;
@@ -751,12 +772,28 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int DT, int G, bool SYM, int CODES, bool BATCHED>
+hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
+  constexpr int UNROLL = 4;
+  static int cache[64] = {0};
+  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ true>;
+  if constexpr (!BATCHED && DT == DT_F16) {
+    static int cache_gs[64] = {0};
+    auto kern_gs = k_group<DT, G, SYM, CODES, false, UNROLL, /*PF*/ false, /*NTL*/ true, /*NTS*/ true,
+                           /*SHARED*/ true, /*GS*/ true>;
+    const int64_t round_units =
+        (int64_t)device_cu_count() * resident_blocks_per_cu(kern_gs, cache_gs) * WAVES_PER_BLOCK * UNROLL;
+    if (a.total_units >= 2 * round_units) return launch_persistent(kern_gs, cache_gs, UNROLL, a, st);
+  }
+  return launch_persistent(kern, cache, UNROLL, a, st);
+}
+
 // Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
 // selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
-template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true>
+template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true, bool GS = false>
 hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
   static int cache[64] = {0};
-  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS, SHARED>;
+  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS, SHARED, GS>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
@@ -808,10 +845,10 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 2: return launch_variant_t<4, true, false, true>(a, st);
     case 3: return launch_variant_t<4, false, true, true, false>(a, st);   // per-unit parameters (r1 default)
     case 4: return launch_variant_t<2, true, true, true>(a, st);
-    case 5: return launch_variant_t<8, false, true, true>(a, st);          // per-unit (UNROLL 8)
-    case 6: return launch_variant_t<2, false, true, true>(a, st);
-    case 7: return launch_variant_t<4, false, false, false>(a, st);
-    case 8: return launch_variant_t<4, true, false, true, false>(a, st);   // per-unit, single-tensor r1 default
+    case 5: return launch_variant_t<4, false, true, true, true, true>(a, st);   // grid-stride walk
+    case 6: return launch_variant_t<4, true, true, true, true, true>(a, st);    // grid-stride + prefetch
+    case 7: return launch_variant_t<2, true, true, true, true, true>(a, st);    // grid-stride, UNROLL 2, prefetch
+    case 8: return launch_variant_t<1, true, true, true, true, true>(a, st);    // grid-stride, UNROLL 1, prefetch
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
