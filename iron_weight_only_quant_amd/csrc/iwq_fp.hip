@@ -244,9 +244,30 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
   fp_flag_nan(a.nan_flag, any_nan);
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int32_t, x), CTRL, 0xF, 0xF,
+                                                               false));
+}
+// the parameters of unit k of this lane's group, held by lane k of the quad (see iter_shared_f16
+// in iwq_minmax.hip; scalars only -- never an f2 across DPP)
+__device__ __forceinline__ FpParams bcast_fp_params(const FpParams& p, int k) {
+  FpParams q;
+  q.fast = true;
+  switch (k) {
+    case 0: q.s = dpp_f32<0x00>(p.s); q.rs = dpp_f32<0x00>(p.rs); q.z = dpp_f32<0x00>(p.z); break;
+    case 1: q.s = dpp_f32<0x55>(p.s); q.rs = dpp_f32<0x55>(p.rs); q.z = dpp_f32<0x55>(p.z); break;
+    case 2: q.s = dpp_f32<0xAA>(p.s); q.rs = dpp_f32<0xAA>(p.rs); q.z = dpp_f32<0xAA>(p.z); break;
+    default: q.s = dpp_f32<0xFF>(p.s); q.rs = dpp_f32<0xFF>(p.rs); q.z = dpp_f32<0xFF>(p.z); break;
+  }
+  return q;
+}
+
 // k_fp_group with the decode table in LDS (no packed codes): 512-thread workgroups, each stages the
 // table (<= 48 KB for E4M3) once; finite groups take fp_pair_lut, the rest the exact ALU chain.
-template <int CODEC, int G, bool SYM>
+// Group parameters are computed once per iteration of 4 units (g >= 32: lane l computes unit l % 4
+// of its group) and DPP-broadcast, as in k_group; GS = grid-stride walk (large single tensors).
+template <int CODEC, int G, bool SYM, bool GS>
 __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
@@ -258,54 +279,92 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   constexpr int UNROLL = 4;
   constexpr int LPG = G / 8;
   constexpr bool RED_SYM = SYM || CODEC != CODEC_FP;
+  constexpr bool SHARE = G >= 32;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WPBL + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * WPBL;
-  int64_t per = (a.total_units + nwaves - 1) / nwaves;
-  per = (per + UNROLL - 1) / UNROLL * UNROLL;
-  const int64_t ubeg = wave * per;
-  const int64_t uend = min(ubeg + per, a.total_units);
+  int64_t u0, cend;
+  if constexpr (GS) {
+    u0 = wave * UNROLL;
+    cend = min(u0 + UNROLL, a.total_units);
+  } else {
+    int64_t per = (a.total_units + nwaves - 1) / nwaves;
+    per = (per + UNROLL - 1) / UNROLL * UNROLL;
+    u0 = wave * per;
+    cend = min(u0 + per, a.total_units);
+  }
   const _Float16 bnd = __builtin_bit_cast(_Float16, (uint16_t)lut_bound_bits(CODEC, a.f));
   const h2 bound2 = {bnd, bnd};
   bool any_nan = false;
-  for (int64_t u0 = ubeg; u0 < uend; u0 += UNROLL) {
+  auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
+    Vec8<DT_F16> o;
+    bool nan8 = false;
+    if (table) {  // finite group (grid: S > 0): table path, no NaN possible
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o.u[j] = fp_pair_lut<CODEC, SYM>(vk.u[j], p, bound2, lut);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t c;
+        const float y = fp_elem<CODEC, SYM, false>(F::to_f(vk.get(i)), p, a.f, c, tabs);
+        nan8 |= (y != y);
+        o.set(i, F::from_f(y));
+      }
+    }
+    if (e0 < a.numel) {
+      any_nan |= nan8;
+      if (a.out) o.store(a.out + e0 * F::BYTES);
+      if ((lane % LPG) == 0) {
+        if (a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
+        if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, e0 / G, p.z);
+      }
+    }
+  };
+  while (u0 < cend) {
+    const int32_t nu = (int32_t)min((int64_t)UNROLL, cend - u0);
     Vec8<DT_F16> v[UNROLL];
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
-      const bool ok = (u0 + k < uend) && e < a.numel;
+      const bool ok = (k < nu) && e < a.numel;
       v[k].load(a.w + (ok ? e : 0) * F::BYTES);
+    }
+    int32_t mn[UNROLL], mx[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      minmax8<DT_F16, RED_SYM>(v[k], mn[k], mx[k]);
+      if constexpr (RED_SYM) group_max<LPG>(mx[k]);
+      else group_minmax<LPG>(mn[k], mx[k]);
+    }
+    bool shared_ok = false;
+    FpParams ps{};
+    if constexpr (SHARE) {
+      const int kk = lane & (UNROLL - 1);
+      int32_t smn = mn[0], smx = mx[0];
+#pragma unroll
+      for (int k = 1; k < UNROLL; ++k) {
+        if (kk == k) { smn = mn[k]; smx = mx[k]; }
+      }
+      ps = fp_group_params<CODEC, SYM>(smn, smx, a.f);
+      shared_ok = __ballot(kk < nu && !(ps.fast && ps.s > 0.0f)) == 0;
     }
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
-      if (u0 + k >= uend) break;
-      const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
-      int32_t mn, mx;
-      minmax8<DT_F16, RED_SYM>(v[k], mn, mx);
-      if constexpr (RED_SYM) group_max<LPG>(mx);
-      else group_minmax<LPG>(mn, mx);
-      const FpParams p = fp_group_params<CODEC, SYM>(mn, mx, a.f);
-      Vec8<DT_F16> o;
-      bool nan8 = false;
-      if (p.fast && p.s > 0.0f) {  // finite group (grid: S > 0): table path, no NaN possible
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o.u[j] = fp_pair_lut<CODEC, SYM>(v[k].u[j], p, bound2, lut);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          uint32_t c;
-          const float y = fp_elem<CODEC, SYM, false>(F::to_f(v[k].get(i)), p, a.f, c, tabs);
-          nan8 |= (y != y);
-          o.set(i, F::from_f(y));
+      if (k < nu) {
+        const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
+        if (SHARE && shared_ok) {
+          unit_out(k, e0, bcast_fp_params(ps, k), v[k], true);
+        } else {
+          const FpParams p = fp_group_params<CODEC, SYM>(mn[k], mx[k], a.f);
+          unit_out(k, e0, p, v[k], p.fast && p.s > 0.0f);
         }
       }
-      if (e0 < a.numel) {
-        any_nan |= nan8;
-        if (a.out) o.store(a.out + e0 * F::BYTES);
-        if ((lane % LPG) == 0) {
-          if (a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
-          if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, e0 / G, p.z);
-        }
+    }
+    u0 += nu;
+    if constexpr (GS) {
+      if (u0 >= cend) {
+        u0 += (nwaves - 1) * UNROLL;
+        cend = min(u0 + UNROLL, a.total_units);
       }
     }
   }
@@ -392,16 +451,20 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
 
 template <int CODEC, int G, bool SYM>
 hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
-  auto kern = k_fp_group_lut<CODEC, G, SYM>;
+  // walk policy as k_group's single tensors: grid-stride at >= 2 grid rounds, else contiguous
+  auto kern = k_fp_group_lut<CODEC, G, SYM, false>;
+  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true>;
   const size_t lds = (size_t)a.lut_n8 * 2;
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
   constexpr int WPBL = LUT_BLOCK / WAVE;
   int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
   const int64_t cap = (int64_t)cu_count() * occ;
+  const bool gs = a.total_units >= 2 * cap * WPBL * 4;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
   return hipGetLastError();
 }
 
