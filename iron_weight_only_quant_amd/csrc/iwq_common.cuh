@@ -583,6 +583,38 @@ __device__ __forceinline__ uint32_t quant2_biased(uint32_t wpair, const BiasedWo
   return as_u32(pk_mul_bc_lo(u - bias, b.sz));
 }
 
+// Biased path with DIFFERENT groups in the two halves of a pair (quant_dim = 1: adjacent columns):
+// the same 11 operations with per-half operands instead of broadcasts.
+struct BiasedPair {
+  f2 rs, s;        // per-half RN(1/s), s (fp32)
+  uint32_t lo, hi;  // per-half fp16 bounds B + lo - z, B + hi - z
+  uint32_t s16;     // per-half fp16 scales
+  uint32_t kc;      // per-half fp16 z + off - B + 1024
+};
+template <bool SYM>
+__device__ __forceinline__ BiasedPair biased_pair(const GroupParams& p0, const GroupParams& p1, int n_bits) {
+  const BiasedWords a = biased_words<SYM>(p0, n_bits), b = biased_words<SYM>(p1, n_bits);
+  BiasedPair r;
+  r.rs = f2{a.rs, b.rs};
+  r.s = f2{a.s, b.s};
+  r.lo = (a.bounds & 0xFFFFu) | (b.bounds << 16);
+  r.hi = (a.bounds >> 16) | (b.bounds & 0xFFFF0000u);
+  r.s16 = (a.sz & 0xFFFFu) | (b.sz << 16);
+  r.kc = (a.kc & 0xFFFFu) | (b.kc << 16);
+  return r;
+}
+template <int CODES>
+__device__ __forceinline__ uint32_t quant2_biased_pair(uint32_t wpair, const BiasedPair& b, uint32_t& cpair) {
+  const f2 w = __builtin_convertvector(as_h2(wpair), f2);
+  const f2 q0 = w * b.rs;
+  const f2 e = __builtin_elementwise_fma(-q0, b.s, w);
+  const h2 t = __builtin_convertvector(opaque2(__builtin_elementwise_fma(e, b.rs, q0)), h2);
+  const h2 bias = {(_Float16)BIAS, (_Float16)BIAS};
+  const h2 u = pk_min(pk_max(t + bias, as_h2(b.lo)), as_h2(b.hi));
+  if constexpr (CODES != 0) cpair = as_u32(u + as_h2(b.kc)) & 0x03FF03FFu;
+  return as_u32((u - bias) * as_h2(b.s16));
+}
+
 // Store the codes of 8 consecutive elements (element index elem0, multiple of 8):
 // CODES == 4: 4 B (low nibble = even element), CODES == 8: 8 B.
 template <int CODES>

@@ -389,23 +389,28 @@ struct RowArgs {
   uint32_t* nan_flag;
 };
 
-template <int DT, int CPL, bool SYM, int CODES>
-__global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
+template <int DT, int CPL>
+__device__ __forceinline__ void row_load(const RowArgs& a, int64_t j, int lane, Vec8<DT> (&v)[CPL]) {
   using F = Fmt<DT>;
-  const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (j >= a.G) return;  // whole wave exits together
   const int64_t row = j / a.gpr;
   const int64_t col0 = (j - row * a.gpr) * a.L;
   const char* src = a.w + (row * a.ld_w + col0) * F::BYTES;
-  Vec8<DT> v[CPL];
   const int64_t nchunks = a.L / 8;
-  const float rmax = rmax_for(a.n_bits, SYM);
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int64_t ch = (int64_t)k * WAVE + lane;
     if (ch < nchunks) v[k].load(src + ch * 8 * F::BYTES);
   }
+}
+
+// reduce + quantize + store one group held in registers; returns whether a NaN was produced
+template <int DT, int CPL, bool SYM, int CODES>
+__device__ __forceinline__ bool row_compute(const RowArgs& a, int64_t j, int lane, const Vec8<DT> (&v)[CPL],
+                                            float rmax) {
+  using F = Fmt<DT>;
+  const int64_t row = j / a.gpr;
+  const int64_t col0 = (j - row * a.gpr) * a.L;
+  const int64_t nchunks = a.L / 8;
   int32_t mn = 0x7FFFFFFF, mx = (int32_t)0x80000000;
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
@@ -422,13 +427,24 @@ __global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
   const GroupParams p = params_from_keys<DT, SYM>(mn, mx, a.n_bits, rmax);
   bool any_nan = false;
   char* dst = a.out ? a.out + (row * a.ld_out + col0) * F::BYTES : nullptr;
+  bool biased = false;
+  BiasedWords bw{};
+  if constexpr (DT == DT_F16) {
+    biased = p.fast && a.n_bits <= 9;  // wave-uniform (one group per wave)
+    if (biased) bw = biased_words<SYM>(p, a.n_bits);
+  }
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int64_t ch = (int64_t)k * WAVE + lane;
     if (ch < nchunks) {
       Vec8<DT> o;
       uint32_t c[4];
-      any_nan |= quant8<DT, SYM>(v[k], p, a.n_bits, o, c);
+      if (DT == DT_F16 && biased) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) o.u[jj] = quant2_biased<CODES>(v[k].u[jj], bw, c[jj]);
+      } else {
+        any_nan |= quant8<DT, SYM>(v[k], p, a.n_bits, o, c);
+      }
       if (dst) o.store(dst + ch * 8 * F::BYTES);
       if constexpr (CODES != 0) store_codes8<CODES>(a.codes, row * a.cols + col0 + ch * 8, c);
     }
@@ -436,6 +452,43 @@ __global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
   if (lane == 0) {
     if (a.scales) store_param<DT>(a.scales, j, p.s);
     if (!SYM && a.zeros) store_param<DT>(a.zeros, j, p.z);
+  }
+  return any_nan;
+}
+
+template <int DT, int CPL, bool SYM, int CODES>
+__global__ __launch_bounds__(BLOCK) void k_rowwave(RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= a.G) return;  // whole wave exits together
+  Vec8<DT> v[CPL];
+  row_load<DT, CPL>(a, j, lane, v);
+  flag_nan(a.nan_flag, row_compute<DT, CPL, SYM, CODES>(a, j, lane, v, rmax_for(a.n_bits, SYM)));
+}
+
+// Persistent form for short groups (CPL <= 8, rows up to 4096 elements): wave w takes groups
+// w, w + nwaves, ... and loads group j + nwaves while it quantizes group j (two register images),
+// so a 1.3-round grid (11008 rows of 4096) has neither a second-round tail nor exposed load latency.
+template <int DT, int CPL, bool SYM, int CODES>
+__global__ __launch_bounds__(BLOCK) void k_rowwave_pf(RowArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+  int64_t j = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bool any_nan = false;
+  if (j < a.G) {
+    const float rmax = rmax_for(a.n_bits, SYM);
+    Vec8<DT> v[CPL];
+    row_load<DT, CPL>(a, j, lane, v);
+    while (true) {
+      const int64_t jn = j + nwaves;
+      Vec8<DT> vn[CPL];
+      if (jn < a.G) row_load<DT, CPL>(a, jn, lane, vn);
+      any_nan |= row_compute<DT, CPL, SYM, CODES>(a, j, lane, v, rmax);
+      if (jn >= a.G) break;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) v[k] = vn[k];
+      j = jn;
+    }
   }
   flag_nan(a.nan_flag, any_nan);
 }
@@ -553,18 +606,50 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
 #pragma unroll
   for (int k = 0; k < RPT; ++k) v[k].load(a.w + ((r0 + ty + k * TY) * a.ld_w + cl) * F::BYTES);
   int32_t mn[8], mx[8];
+  if constexpr (Fmt<DT>::NB == 16) {
+    // per-column keys of the 16-bit dtypes in packed int16 (two columns per op), unpacked once
+    s16x2 pmn[4], pmx[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { mn[i] = 0x7FFFFFFF; mx[i] = (int32_t)0x80000000; }
+    for (int k = 0; k < RPT; ++k) {
 #pragma unroll
-  for (int k = 0; k < RPT; ++k) {
+      for (int jj = 0; jj < 4; ++jj) {
+        s16x2 kk;
+        if constexpr (SYM) {
+          kk = __builtin_bit_cast(s16x2, v[k].u[jj] & 0x7FFF7FFFu);
+        } else {
+          const s16x2 x = __builtin_bit_cast(s16x2, v[k].u[jj]);
+          kk = x ^ ((x >> (short)15) & (short)0x7FFF);
+        }
+        if (k == 0) {
+          pmn[jj] = kk;
+          pmx[jj] = kk;
+        } else {
+          if constexpr (!SYM) pmn[jj] = __builtin_elementwise_min(pmn[jj], kk);
+          pmx[jj] = __builtin_elementwise_max(pmx[jj], kk);
+        }
+      }
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if constexpr (SYM) {
-        mx[i] = max(mx[i], mag_key<DT>(v[k].get(i)));
-      } else {
-        const int32_t kk = key_of<DT>(v[k].get(i));
-        mn[i] = min(mn[i], kk);
-        mx[i] = max(mx[i], kk);
+    for (int jj = 0; jj < 4; ++jj) {
+      mn[2 * jj] = SYM ? 0 : (int32_t)pmn[jj].x;
+      mn[2 * jj + 1] = SYM ? 0 : (int32_t)pmn[jj].y;
+      mx[2 * jj] = (int32_t)pmx[jj].x;
+      mx[2 * jj + 1] = (int32_t)pmx[jj].y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { mn[i] = 0x7FFFFFFF; mx[i] = (int32_t)0x80000000; }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (SYM) {
+          mx[i] = max(mx[i], mag_key<DT>(v[k].get(i)));
+        } else {
+          const int32_t kk = key_of<DT>(v[k].get(i));
+          mn[i] = min(mn[i], kk);
+          mx[i] = max(mx[i], kk);
+        }
       }
     }
   }
@@ -595,6 +680,29 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
       }
     }
     const uint32_t off = SYM ? (1u << (a.n_bits - 1)) : 0u;
+    if constexpr (DT == DT_F16) {
+      // all 8 columns of this thread on the fast path: packed pairs with per-half group operands
+      bool fast = a.n_bits <= 9;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fast = fast && p[i].fast;
+      if (fast) {
+        BiasedPair bp[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) bp[jj] = biased_pair<SYM>(p[2 * jj], p[2 * jj + 1], a.n_bits);
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) {
+          const int64_t r = r0 + ty + k * TY;
+          Vec8<DT> o;
+          uint32_t c[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) o.u[jj] = quant2_biased_pair<CODES>(v[k].u[jj], bp[jj], c[jj]);
+          if (a.out) o.store(a.out + (r * a.ld_out + c0) * F::BYTES);
+          if constexpr (CODES != 0) store_codes8<CODES>(a.codes, r * a.cols + c0, c);
+        }
+        flag_nan(a.nan_flag, false);
+        return;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int64_t r = r0 + ty + k * TY;
@@ -887,8 +995,27 @@ hipError_t launch_group(int dt, int64_t g, bool sym, int codes, const GroupArgs&
 #undef IWQ_G_CODES
 }
 
+template <int DT, int CPL, bool SYM, int CODES>
+hipError_t launch_row_pf(const RowArgs& a, hipStream_t st) {
+  static int cache[64] = {0};
+  auto kern = k_rowwave_pf<DT, CPL, SYM, CODES>;
+  int64_t blocks = (a.G + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+  const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int DT, int CPL, bool SYM>
 hipError_t launch_row_t(int codes, const RowArgs& a, hipStream_t st) {
+  if constexpr (CPL <= 8 && DT != DT_F32) {
+    // persistent + prefetch once the groups overflow one resident grid (~8k waves)
+    if (a.G > (int64_t)device_cu_count() * 8 * WAVES_PER_BLOCK) {
+      if (codes == 0) return launch_row_pf<DT, CPL, SYM, 0>(a, st);
+      if (codes == 4) return launch_row_pf<DT, CPL, SYM, 4>(a, st);
+      return launch_row_pf<DT, CPL, SYM, 8>(a, st);
+    }
+  }
   const int64_t blocks = (a.G + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   if (codes == 0) hipLaunchKernelGGL((k_rowwave<DT, CPL, SYM, 0>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   else if (codes == 4) hipLaunchKernelGGL((k_rowwave<DT, CPL, SYM, 4>), dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
@@ -916,29 +1043,41 @@ hipError_t launch_row(int dt, bool sym, int codes, const RowArgs& a, hipStream_t
   return sym ? launch_row_c<DT_F32, true>(codes, a, st) : launch_row_c<DT_F32, false>(codes, a, st);
 }
 
-template <int DT, bool SYM, int CODES>
+// Block = TX column chunks (8 columns, 16 B each) x TY row slices.  Default 32 x 8 (512-B row
+// segments; 16 x 16 at g = 256 to bound registers), picked by tools/ab_col.py (profiles/r01_ab_col.jsonl:
+// 11008x4096 g=128 39.1 us vs 41.2 for the r1 8 x 32 shape, g=32 45.3 vs 67.7).  flags variant
+// 1 = 8 x 32, 2 = 32 x 8, 3 = 16 x 16.
+template <int DT, bool SYM, int CODES, int TX, int TY>
 hipError_t launch_col_t(const ColArgs& a, hipStream_t st) {
-  constexpr int TX = 8, TY = 32;
   dim3 grid((unsigned)((a.cols + 8 * TX - 1) / (8 * TX)), (unsigned)(a.rows / a.g));
-  switch (a.g) {
-    case 32: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 1>), grid, dim3(TX * TY), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 2>), grid, dim3(TX * TY), 0, st, a); break;
-    case 128: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 4>), grid, dim3(TX * TY), 0, st, a); break;
-    case 256: hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 8>), grid, dim3(TX * TY), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, dim3(TX * TY), 0, st, a); break;
-  }
+  static_assert(32 % TY == 0, "k_column_reg needs g % TY == 0 for g >= 32");
+  const dim3 blk(TX * TY);
+  if (a.g == 32) hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 32 / TY>), grid, blk, 0, st, a);
+  else if (a.g == 64) hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 64 / TY>), grid, blk, 0, st, a);
+  else if (a.g == 128) hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 128 / TY>), grid, blk, 0, st, a);
+  else if (a.g == 256) hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 256 / TY>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, blk, 0, st, a);
   return hipGetLastError();
 }
-template <int DT, bool SYM>
-hipError_t launch_col_c(int codes, const ColArgs& a, hipStream_t st) {
-  if (codes == 0) return launch_col_t<DT, SYM, 0>(a, st);
-  if (codes == 4) return launch_col_t<DT, SYM, 4>(a, st);
-  return launch_col_t<DT, SYM, 8>(a, st);
+template <int DT, bool SYM, int CODES>
+hipError_t launch_col_v(int variant, const ColArgs& a, hipStream_t st) {
+  if (variant == 1) return launch_col_t<DT, SYM, CODES, 8, 32>(a, st);
+  if (variant == 2) return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
+  if (variant == 3 || a.g == 256) return launch_col_t<DT, SYM, CODES, 16, 16>(a, st);  // 16 rows/thread at g=256
+  return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
 }
-hipError_t launch_col(int dt, bool sym, int codes, const ColArgs& a, hipStream_t st) {
-  if (dt == IWQ_F16) return sym ? launch_col_c<DT_F16, true>(codes, a, st) : launch_col_c<DT_F16, false>(codes, a, st);
-  if (dt == IWQ_BF16) return sym ? launch_col_c<DT_BF16, true>(codes, a, st) : launch_col_c<DT_BF16, false>(codes, a, st);
-  return sym ? launch_col_c<DT_F32, true>(codes, a, st) : launch_col_c<DT_F32, false>(codes, a, st);
+template <int DT, bool SYM>
+hipError_t launch_col_c(int codes, int variant, const ColArgs& a, hipStream_t st) {
+  if (codes == 0) return launch_col_v<DT, SYM, 0>(variant, a, st);
+  if (codes == 4) return launch_col_v<DT, SYM, 4>(variant, a, st);
+  return launch_col_v<DT, SYM, 8>(variant, a, st);
+}
+hipError_t launch_col(int dt, bool sym, int codes, int variant, const ColArgs& a, hipStream_t st) {
+  if (dt == IWQ_F16)
+    return sym ? launch_col_c<DT_F16, true>(codes, variant, a, st) : launch_col_c<DT_F16, false>(codes, variant, a, st);
+  if (dt == IWQ_BF16)
+    return sym ? launch_col_c<DT_BF16, true>(codes, variant, a, st) : launch_col_c<DT_BF16, false>(codes, variant, a, st);
+  return sym ? launch_col_c<DT_F32, true>(codes, variant, a, st) : launch_col_c<DT_F32, false>(codes, variant, a, st);
 }
 
 template <int DT, bool SYM>
@@ -1112,7 +1251,7 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     a.g = L;  // rows per group (L = group, or rows for per-channel)
     a.n_bits = n_bits;
     a.nan_flag = nan_flag;
-    IWQ_HIP(launch_col(dtype, sym, codes, a, s));
+    IWQ_HIP(launch_col(dtype, sym, codes, (int)((flags >> 16) & 0xFFu), a, s));
     return IWQ_OK;
   }
   // universal path
