@@ -207,6 +207,15 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
                    unsigned flags, void* stream);
 
+/*
+ * Packed codes -> fp16 W_deq [N, K] (contiguous: ld_out == K, 16-B aligned), bit-identical to the
+ * reference's dequantized weight RN16((q - z) * s): the prefill path for packed-only weights
+ * (dequantize once, then one library GEMM).  Same codes / scales / zeros / group conventions as
+ * iwq_w4a16_gemm; K % 32 == 0.
+ */
+int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros, int n_bits, int64_t group,
+                       int64_t N, int64_t K, void* out, int64_t ld_out, void* stream);
+
 /* Deterministic synthetic weights (oracle/synth.py bit-for-bit), written to [rows, cols] contiguous. */
 int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t index_offset, void* stream);
 

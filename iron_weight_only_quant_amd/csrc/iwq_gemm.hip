@@ -688,9 +688,82 @@ __global__ __launch_bounds__(BG_THR) void k_w4a16_big(GemmArgs a) {
   }
 }
 
+// Packed codes -> the fp16 dequantized weight W_deq [N, K] (contiguous), element for element the
+// reference's RN16((q - z) * s) (quant_linear.py:935-949): the prefill path for packed-only weights
+// (dequantize once into a scratch buffer, then one library GEMM), HBM-bound at 2 + 0.5 + 4/g B per
+// weight.  The weight is walked flat: a wave takes 2048 consecutive elements per step; lane l's
+// piece j (j < 4) is elements 512 j + 8 l .. +8, i.e. code dword 64 j + l, so every load
+// instruction reads 256 contiguous bytes and every 16-B store instruction writes 1 KiB contiguous
+// (a piece never straddles a row or a scale group: K % 32 == 0, g % 32 == 0).
+__global__ __launch_bounds__(256) void k_dequant_packed(GemmArgs a, int64_t total) {
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const IWQ_GLOBAL uint32_t* c32 = gp<uint32_t>(a.codes);
+  IWQ_GLOBAL h8* out = gp<h8>(a.y);
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2048; base < total; base += nwaves * 2048) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t e = base + 512 * j + 8 * lane;
+      w[j] = __builtin_nontemporal_load(c32 + (e < total ? e / 8 : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t e = base + 512 * j + 8 * lane;
+      if (e < total) {
+        const int64_t gi = a.gshift >= 0 ? (e >> a.gshift) : e / a.group;  // flat group index
+        const _Float16 sc = gp<_Float16>(a.scales)[gi];
+        const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[gi] : a.zsym;
+        const h2 sv = {sc, sc};
+        const h2 zz = {(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
+        __builtin_nontemporal_store(dequant8_nat(w[j], zz, sv, mask_s, magic_v), out + e / 8);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros, int n_bits, int64_t group,
+                       int64_t N, int64_t K, void* out, int64_t ld_out, void* stream) {
+  if (!codes || !scales || !out) return IWQ_ERR_ARG;
+  if (N <= 0 || K <= 0 || K % 32 != 0 || ld_out != K) return IWQ_ERR_SHAPE;
+  if (n_bits < 2 || n_bits > 4) return IWQ_ERR_BITS;
+  const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
+  if (g <= 0 || g % 32 != 0 || K % g != 0) return IWQ_ERR_GROUP;
+  if ((reinterpret_cast<uintptr_t>(codes) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u)) return IWQ_ERR_ARG;
+  GemmArgs a{};
+  a.codes = static_cast<const uint8_t*>(codes);
+  a.scales = static_cast<const _Float16*>(scales);
+  a.zeros = static_cast<const _Float16*>(zeros);
+  a.y = static_cast<_Float16*>(out);
+  a.K = (int)K;
+  a.N = (int)N;
+  a.group = (int)g;
+  a.gpr = (int)(K / g);
+  a.zsym = (float)(1 << (n_bits - 1));
+  a.gshift = (g & (g - 1)) == 0 ? __builtin_ctzll((unsigned long long)g) : -1;
+  const int64_t total = N * K;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  int64_t blocks = (total + 4 * 2048 - 1) / (4 * 2048);
+  if (blocks > (int64_t)cus * 8) blocks = (int64_t)cus * 8;
+  hipLaunchKernelGGL(k_dequant_packed, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), a,
+                     total);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    iwq::last_hip_error() = (int)e;
+    return IWQ_ERR_HIP;
+  }
+  return IWQ_OK;
+}
 
 int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,

@@ -327,6 +327,32 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     return y.reshape(*x.shape[:-1], N)
 
 
+def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor], n_bits: int,
+                   group: int, N: int, K: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed codes -> fp16 W_deq [N, K], bit-identical to the reference's dequantized weight."""
+    L.require_device(codes)
+    lib = L.load()
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float16, device=codes.device)
+    with torch.cuda.device(codes.device):
+        st = lib.iwq_dequant_packed(L.ptr(codes), L.ptr(scales), L.ptr(zeros), int(n_bits), int(group), int(N),
+                                    int(K), L.ptr(out), out.stride(0), L.stream_handle(codes.device))
+    _raise_for(st, "iwq_dequant_packed")
+    return out
+
+
+def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
+                 n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
+    decode batches (M <= GEMV_MAX_M), dequant-once + hipBLASLt (F.linear) above, where the library
+    GEMM on a freshly dequantized weight beats the fused MFMA kernel."""
+    K = x.shape[-1]
+    if x.numel() // K <= GEMV_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
+        return w4a16_gemm(x, codes, scales, zeros, n_bits, group, N, bias)
+    w = dequant_packed(codes, scales, zeros, n_bits, group, N, K)
+    return torch.nn.functional.linear(x, w, bias)
+
+
 class BatchPlan:
     """Device-resident work table for quantizing many weights in one launch (quant_wrapper.py:52-82).
 

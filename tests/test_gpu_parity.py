@@ -542,6 +542,24 @@ def test_quantlinear_fused_forward(K):
     torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
 
 
+@pytest.mark.parametrize("bits,group,sym", [(4, -2, False), (4, 128, False), (4, 128, True), (3, 64, False),
+                                            (2, 32, True), (4, 96, False)])
+def test_dequant_packed_bit_exact(K, bits, group, sym):
+    """Packed codes -> fp16 W_deq equals the fake-quant weight of the same quantization, bit for bit;
+    w4a16_linear (packed-only forward) matches F.linear on it at decode and prefill sizes."""
+    N, Kd = 384, 1536
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 91 + bits)
+    r = K.quantize_minmax(w, bits, group, sym, 0, want_codes=True)
+    deq = K.dequant_packed(r.codes, r.scales, r.zeros, bits, group, N, Kd)
+    assert torch.equal(deq.view(torch.int16), r.out.view(torch.int16))
+    bias = torch.randn(N, device=DEV).half()
+    for m in (1, 9, 600):
+        x = torch.randn(m, Kd, device=DEV).half()
+        y = K.w4a16_linear(x, r.codes, r.scales, r.zeros, bits, group, N, bias)
+        torch.testing.assert_close(y, torch.nn.functional.linear(x, r.out, bias), rtol=1e-2, atol=2e-2)
+
+
 def test_quantlinear_fused_forward_auto(K, monkeypatch):
     """fused_forward="auto": the packed-weight kernel for M <= 16 rows, F.linear above."""
     from iron_weight_only_quant_amd import quant_linear as QLm

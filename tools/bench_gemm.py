@@ -1,5 +1,6 @@
 """Config 3 measurement: fused INT4 dequant->GEMM forward (kernels.w4a16_gemm, MFMA) vs the
-reference forward F.linear(x, W_deq) (hipBLASLt on the fp16 dequantized weight), Llama-2-7B shapes.
+reference forward F.linear(x, W_deq) (hipBLASLt on the fp16 dequantized weight), Llama-2-7B shapes,
+plus the packed-only alternative dequant-once (iwq_dequant_packed) + hipBLASLt.
 
 Prints one JSON line per (shape, M) with TFLOP/s of both, the fraction of the 2.5 PF dense fp16
 MFMA peak (MI355X_MICROARCH.md) and the weight bytes each reads.  Timing: HIP events around R
@@ -79,6 +80,13 @@ def main():
             ref = lambda: torch.nn.functional.linear(x, r.out)
             ref()
             t_r = timed(ref, a.reps) if M >= 1024 else timed_graph(ref, 50)
+            # packed-only prefill alternative: dequantize once (iwq_dequant_packed) + hipBLASLt
+            dq = lambda: torch.nn.functional.linear(
+                x, kernels.dequant_packed(r.codes, r.scales, r.zeros, 4, a.group, N, K))
+            dq()
+            t_dq = timed(dq, a.reps) if M >= 1024 else timed_graph(dq, 50)
+            deq_only = lambda: kernels.dequant_packed(r.codes, r.scales, r.zeros, 4, a.group, N, K)
+            t_deq = timed_graph(deq_only, 20)
             for v in [int(t) for t in a.variants.split(",")]:
                 fl = kernels.gemm_variant_flags(v)
                 fused = lambda: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N, flags=fl)
@@ -94,6 +102,8 @@ def main():
                        "fused_weight_GBps": round(wbytes / t_f / 1e6, 1),
                        "hipblaslt_fp16_ms": round(t_r, 4), "hipblaslt_tflops": round(flops / t_r / 1e9, 1),
                        "speedup_vs_F_linear": round(t_r / t_f, 3),
+                       "dequant_plus_hipblaslt_ms": round(t_dq, 4), "dequant_only_ms": round(t_deq, 4),
+                       "dequant_GBps": round((wbytes + N * K * 2) / t_deq / 1e6, 1),
                        "weight_bytes_fused": wbytes,
                        "weight_bytes_fp16": int(N * K * 2), "max_abs_diff_vs_F_linear": err}
                 print(json.dumps(rec), flush=True)
