@@ -174,6 +174,18 @@ int iwq_fp4_grid_lut(const void* w, int64_t rows, int64_t cols, int64_t group, i
                      void* stream, const void* lut);
 
 /*
+ * Batched FP form (quantize_model over a whole model, one launch): fp16 weights, entries planned by
+ * iwq_batch_plan(h_entries, n, IWQ_F16, 8, group, &total_units) (out_codes must be NULL), decode
+ * table REQUIRED (iwq_fp_build_lut with the same codec / exp / mant / approximate parameters).
+ * group: power of two in [8, 512].  Per tensor the result equals iwq_quantize_fp_lut /
+ * iwq_quantize_fp_approx_lut (single-aligned) / iwq_fp4_grid_lut bit for bit.
+ */
+int iwq_quantize_fp_batched(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units, int codec,
+                            int exp_bits, int mant_bits, int64_t group, int symmetric, int hi_align_start,
+                            int hi_align_exp_field, int tail_pad_bits, const void* lut, uint32_t* nan_flag,
+                            unsigned flags, void* stream);
+
+/*
  * QuantLinear.quantize_weight, weight_format "bfp" (quant_linear.py:648-723): block floating point
  * with a shared per-group exponent (max fp16 exponent field of the group) and min(w_bit-1, 11)
  * mantissa bits incl. the leading one (round-half-up, saturating).  dtype F16 / BF16 / F32 (taken to

@@ -29,7 +29,7 @@ EXPORTS = (
     "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
     "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
     "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
-    "iwq_dequant_packed",
+    "iwq_dequant_packed", "iwq_quantize_fp_batched",
 )
 
 IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX = 0, 1, 2
@@ -105,6 +105,9 @@ def load():
         lib.iwq_fp4_grid_lut.restype = i32
         lib.iwq_quantize_fp_approx_lut.argtypes = lib.iwq_quantize_fp_approx.argtypes + [vp]
         lib.iwq_quantize_fp_approx_lut.restype = i32
+        lib.iwq_quantize_fp_batched.argtypes = [vp, ctypes.c_int32, i64, i32, i32, i32, i64, i32, i32, i32, i32, vp,
+                                                vp, u32, vp]
+        lib.iwq_quantize_fp_batched.restype = i32
         lib.iwq_dequant_packed.argtypes = [vp, vp, vp, i32, i64, i64, i64, vp, i64, vp]
         lib.iwq_dequant_packed.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]

@@ -53,6 +53,8 @@ struct FpArgs {
   uint32_t* nan_flag;
   const uint16_t* lut;  // decode table (iwq_fp_build_lut) or null: ALU codec
   int32_t lut_n8;       // table entries, rounded up to a multiple of 8
+  const iwq_batch_entry* entries;  // batched form (whole model): tensor table, else null
+  int32_t n_entries;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -267,7 +269,7 @@ __device__ __forceinline__ FpParams bcast_fp_params(const FpParams& p, int k) {
 // table (<= 48 KB for E4M3) once; finite groups take fp_pair_lut, the rest the exact ALU chain.
 // Group parameters are computed once per iteration of 4 units (g >= 32: lane l computes unit l % 4
 // of its group) and DPP-broadcast, as in k_group; GS = grid-stride walk (large single tensors).
-template <int CODEC, int G, bool SYM, bool GS>
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false>
 __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
@@ -296,6 +298,30 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   const _Float16 bnd = __builtin_bit_cast(_Float16, (uint16_t)lut_bound_bits(CODEC, a.f));
   const h2 bound2 = {bnd, bnd};
   bool any_nan = false;
+  // current tensor (batched: wave-uniform cursor over the table, entries ordered by unit_begin)
+  const char* tw = a.w;
+  char* tout = a.out;
+  void* tsc = a.scales;
+  void* tz = a.zeros;
+  int64_t tnumel = a.numel, tbeg = 0, tnext = INT64_MAX;
+  int32_t cur = -1;
+  auto seek = [&](int64_t u) {
+    if constexpr (BATCHED) {
+      if (cur < 0 || u >= tnext) {
+        const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(a.entries);
+        if (cur < 0) cur = 0;
+        while (cur + 1 < a.n_entries && u >= tab[cur + 1].unit_begin) ++cur;
+        cur = __builtin_amdgcn_readfirstlane(cur);
+        tw = static_cast<const char*>(tab[cur].w);
+        tout = static_cast<char*>(tab[cur].out_deq);
+        tsc = tab[cur].out_scales;
+        tz = tab[cur].out_zeros;
+        tnumel = tab[cur].rows * tab[cur].cols;
+        tbeg = tab[cur].unit_begin;
+        tnext = cur + 1 < a.n_entries ? tab[cur + 1].unit_begin : INT64_MAX;
+      }
+    }
+  };
   auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
     Vec8<DT_F16> o;
     bool nan8 = false;
@@ -311,23 +337,25 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
         o.set(i, F::from_f(y));
       }
     }
-    if (e0 < a.numel) {
+    if (e0 < tnumel) {
       any_nan |= nan8;
-      if (a.out) o.store(a.out + e0 * F::BYTES);
+      if (tout) o.store(tout + e0 * F::BYTES);
       if ((lane % LPG) == 0) {
-        if (a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
-        if (!SYM && CODEC == CODEC_FP && a.zeros) store_param<DT_F16>(a.zeros, e0 / G, p.z);
+        if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
+        if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);
       }
     }
   };
   while (u0 < cend) {
-    const int32_t nu = (int32_t)min((int64_t)UNROLL, cend - u0);
+    seek(u0);
+    const int32_t nu = (int32_t)min(min((int64_t)UNROLL, cend - u0), tnext - u0);
+    const int64_t eb = (u0 - tbeg) * UNIT + (int64_t)lane * 8;  // this lane's element in unit 0
     Vec8<DT_F16> v[UNROLL];
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
-      const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
-      const bool ok = (k < nu) && e < a.numel;
-      v[k].load(a.w + (ok ? e : 0) * F::BYTES);
+      const int64_t e = eb + (int64_t)k * UNIT;
+      const bool ok = (k < nu) && e < tnumel;
+      v[k].load(tw + (ok ? e : 0) * F::BYTES);
     }
     int32_t mn[UNROLL], mx[UNROLL];
 #pragma unroll
@@ -351,7 +379,7 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       if (k < nu) {
-        const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
+        const int64_t e0 = eb + (int64_t)k * UNIT;
         if (SHARE && shared_ok) {
           unit_out(k, e0, bcast_fp_params(ps, k), v[k], true);
         } else {
@@ -466,6 +494,35 @@ hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
   if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
   else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
   return hipGetLastError();
+}
+
+template <int CODEC, int G, bool SYM>
+hipError_t launch_fp_lut_batched_t(const FpArgs& a, hipStream_t st) {
+  auto kern = k_fp_group_lut<CODEC, G, SYM, false, true>;
+  const size_t lds = (size_t)a.lut_n8 * 2;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
+  constexpr int WPBL = LUT_BLOCK / WAVE;
+  int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
+  const int64_t cap = (int64_t)cu_count() * occ;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int CODEC, bool SYM>
+hipError_t launch_fp_lut_batched(int64_t g, const FpArgs& a, hipStream_t st) {
+  switch (g) {
+    case 8: return launch_fp_lut_batched_t<CODEC, 8, SYM>(a, st);
+    case 16: return launch_fp_lut_batched_t<CODEC, 16, SYM>(a, st);
+    case 32: return launch_fp_lut_batched_t<CODEC, 32, SYM>(a, st);
+    case 64: return launch_fp_lut_batched_t<CODEC, 64, SYM>(a, st);
+    case 128: return launch_fp_lut_batched_t<CODEC, 128, SYM>(a, st);
+    case 256: return launch_fp_lut_batched_t<CODEC, 256, SYM>(a, st);
+    case 512: return launch_fp_lut_batched_t<CODEC, 512, SYM>(a, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 template <int CODEC, bool SYM>
@@ -801,6 +858,40 @@ int iwq_quantize_fp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int
   return iwq_quantize_fp_lut(w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, symmetric, quant_dim, out_deq,
                              ld_out, out_codes, out_scales, out_zeros, workspace, workspace_bytes, nan_flag, flags,
                              stream, nullptr);
+}
+
+int iwq_quantize_fp_batched(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units, int codec,
+                            int exp_bits, int mant_bits, int64_t group, int symmetric, int hi_align_start,
+                            int hi_align_exp_field, int tail_pad_bits, const void* lut, uint32_t* nan_flag,
+                            unsigned flags, void* stream) {
+  (void)flags;
+  if (!d_entries || n_entries <= 0 || total_units <= 0 || !lut || !aligned16p(lut)) return IWQ_ERR_ARG;
+  if (codec != CODEC_FP && codec != CODEC_GRID && codec != CODEC_APX) return IWQ_ERR_ARG;
+  if (group < 8 || group > 512 || (group & (group - 1)) != 0) return IWQ_ERR_GROUP_MODE;
+  if (codec == CODEC_GRID) { exp_bits = 2; mant_bits = 1; }
+  FpSpec f{};
+  const int st = fp_spec(exp_bits, mant_bits, f);
+  if (st != IWQ_OK) return st;
+  f.hs = hi_align_start;
+  f.hf = hi_align_exp_field;
+  f.tp = tail_pad_bits;
+  FpArgs a{};
+  a.entries = d_entries;
+  a.n_entries = n_entries;
+  a.total_units = total_units;
+  a.f = f;
+  a.nan_flag = nan_flag;
+  a.lut = static_cast<const uint16_t*>(lut);
+  a.lut_n8 = (int32_t)((lut_bound_bits(codec, f) + 1 + 7) / 8 * 8);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool sym = codec != CODEC_FP || symmetric != 0;
+  hipError_t e;
+  if (codec == CODEC_GRID) e = launch_fp_lut_batched<CODEC_GRID, true>(group, a, s);
+  else if (codec == CODEC_APX) e = launch_fp_lut_batched<CODEC_APX, true>(group, a, s);
+  else if (sym) e = launch_fp_lut_batched<CODEC_FP, true>(group, a, s);
+  else e = launch_fp_lut_batched<CODEC_FP, false>(group, a, s);
+  IWQ_HIP_FP(e);
+  return IWQ_OK;
 }
 
 int iwq_fp4_grid_lut(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,

@@ -434,3 +434,62 @@ def selftest_division(device="cuda"):
     with torch.cuda.device(counts.device):
         L.check(lib.iwq_selftest_division(L.ptr(counts), L.stream_handle(counts.device)), "iwq_selftest_division")
     return tuple(int(x) for x in counts.cpu())
+
+
+class FpBatchPlan:
+    """Whole-model FP fake quantization in ONE launch (quantize_model's loop for weight_format
+    fp4/fp6/fp8, approximate single-aligned decode, or the E2M1 grid): fp16 contiguous weights,
+    power-of-two groups in [8, 512], decode table path (iwq_quantize_fp_batched).  Per tensor the
+    result is bit-identical to quantize_fp / quantize_fp_approx / fp4_grid."""
+
+    def __init__(self, weights: List[torch.Tensor], codec: int, exp_bits: int, mant_bits: int, group: int,
+                 symmetric: bool, hs: int = 0, hf: int = 0, tp: int = 0,
+                 outs: Optional[List[torch.Tensor]] = None):
+        if not weights:
+            raise ValueError("empty batch")
+        lib = L.load()
+        dev = weights[0].device
+        for w in weights:
+            L.require_device(w)
+            if w.device != dev or w.dtype != torch.float16 or w.dim() != 2 or not w.is_contiguous():
+                raise ValueError("batched FP weights must be contiguous 2-D fp16 tensors on one device")
+        if group not in FAST_GROUPS:
+            raise ValueError("batched FP path supports power-of-two groups 8..512")
+        self.device = dev
+        self.codec, self.exp_bits, self.mant_bits = int(codec), int(exp_bits), int(mant_bits)
+        self.group, self.symmetric = int(group), bool(symmetric) or codec != L.IWQ_CODEC_FP
+        self.hs, self.hf, self.tp = int(hs), int(hf), int(tp)
+        self.lut = _luts.get(dev, codec, exp_bits if codec != L.IWQ_CODEC_GRID else 0,
+                             mant_bits if codec != L.IWQ_CODEC_GRID else 0, hs, hf, tp)
+        if self.lut is None:
+            raise RuntimeError("decode table unavailable for this format (or building it inside a graph capture)")
+        self.weights = weights
+        self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
+        self.scales = [torch.empty(w.numel() // group, dtype=torch.float16, device=dev) for w in weights]
+        self.zeros = [torch.empty(w.numel() // group, dtype=torch.float16, device=dev) if not self.symmetric else None
+                      for w in weights]
+        n = len(weights)
+        table = (L.IwqBatchEntry * n)()
+        for i, w in enumerate(weights):
+            table[i].w = w.data_ptr()
+            table[i].out_deq = self.outs[i].data_ptr()
+            table[i].out_codes = None
+            table[i].out_scales = self.scales[i].data_ptr()
+            table[i].out_zeros = self.zeros[i].data_ptr() if self.zeros[i] is not None else None
+            table[i].rows, table[i].cols = w.shape
+        total = ctypes.c_int64(0)
+        _raise_for(lib.iwq_batch_plan(table, n, L.IWQ_F16, 8, self.group, ctypes.byref(total)), "iwq_batch_plan")
+        self.total_units = total.value
+        self.d_table = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
+        self.n = n
+        self.nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.numel = sum(w.numel() for w in weights)
+
+    def run(self, stream=None):
+        lib = L.load()
+        sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
+        with torch.cuda.device(self.device):
+            st = lib.iwq_quantize_fp_batched(L.ptr(self.d_table), self.n, self.total_units, self.codec,
+                                             self.exp_bits, self.mant_bits, self.group, int(self.symmetric),
+                                             self.hs, self.hf, self.tp, L.ptr(self.lut), L.ptr(self.nan_flag), 0, sh)
+        _raise_for(st, "iwq_quantize_fp_batched")

@@ -7,7 +7,8 @@ weight storage; weight-only runs need 0 < w_bit < 16 and a_bit None or >= 16 (:1
 MI355X-first difference: instead of quantizing layer after layer (one ~16-op ATen chain plus an
 empty_cache per layer, :52-82), all eligible layers that live on one GPU and share a dtype are
 quantized by ONE persistent multi-tensor launch (kernels.BatchPlan) when the group size is a
-power of two in [8, 512]; any other configuration uses one launch per layer.
+power of two in [8, 512] (INT: kernels.BatchPlan; FP4/FP6/FP8 and the single-aligned approximate
+decode on fp16 weights: kernels.FpBatchPlan); any other configuration uses one launch per layer.
 """
 import torch
 
@@ -83,9 +84,53 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
                 q.quantized.fill_(True)
                 _set_module(model, n, q)
                 done.add(n)
+    if (batched and w_format in ("fp4", "fp6", "fp8") and kw["quant_dim"] == 0 and g in kernels.FAST_GROUPS
+            and not (kw["approximate"] and kw["double_approximate"]) and layers):
+        _batched_fp(model, layers, kw, w_format, done)
     for n, m in layers:
         if n in done:
             continue
         q = QuantLinear.from_linear(m, **kw)
         _set_module(model, n, q)
     return model
+
+
+def _batched_fp(model, layers, kw, fmt, done):
+    """FP formats (and the single-aligned approximate decode) of every eligible fp16 layer on one
+    GPU in one launch (kernels.FpBatchPlan); buffers as QuantLinear's FP branches set them."""
+    from . import _lib as L
+    from .quant_linear import _fp_bits
+    e, m = _fp_bits(fmt)
+    g = kw["w_group_size"]
+    apx = bool(kw["approximate"])
+    if apx and fmt == "fp4" and e not in (1, 2):
+        return  # the per-layer path raises the reference's error
+    hs, hf, tp = ((kw[f"{fmt}_hi_align_start"], kw[f"{fmt}_hi_align_exp_field"], kw[f"{fmt}_tail_pad_bits"])
+                  if apx else (0, 0, 0))
+    codec = L.IWQ_CODEC_APX if apx else L.IWQ_CODEC_FP
+    sym = True if apx else bool(kw["symmetric"])
+    buckets = {}
+    for n, mod in layers:
+        w = mod.weight.data
+        if (w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous() and w.shape[1] % g == 0
+                and w.dtype == torch.float16 and w.data_ptr() % 16 == 0):
+            buckets.setdefault(w.device, []).append((n, mod))
+    for dev, items in buckets.items():
+        ws = [mod.weight.data for _, mod in items]
+        try:
+            plan = kernels.FpBatchPlan(ws, codec, e, m, g, sym, hs, hf, tp, outs=ws)
+        except (RuntimeError, ValueError, AssertionError):
+            continue  # e.g. E5M2 (fp_max overflows fp16): per-layer path raises like the reference
+        plan.run()
+        for i, (n, mod) in enumerate(items):
+            q = QuantLinear.from_linear(mod, quantize=False, **kw)
+            q.scales = plan.scales[i].view(-1, 1)
+            q.zeros = plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None
+            for other in ("fp4", "fp6", "fp8"):
+                if other != fmt:
+                    setattr(q, f"weight_{other}", None)
+            q.quantized.fill_(True)
+            if apx:
+                q.approximate = True
+            _set_module(model, n, q)
+            done.add(n)

@@ -273,6 +273,41 @@ def test_quantize_model_drop_in(K):
         torch.testing.assert_close(y, torch.nn.functional.linear(x, m.l0.weight, m.l0.bias))
 
 
+@pytest.mark.parametrize("fmt,sym,apx", [("fp8", False, False), ("fp8", True, False), ("fp6", False, False),
+                                         ("fp4", False, False), ("fp8", True, True), ("fp4", True, True)])
+def test_quantize_model_fp_batched(K, fmt, sym, apx):
+    """quantize_model with FP formats: the one-launch batched path (kernels.FpBatchPlan) leaves
+    every layer (weight, scales, zeros, buffers) bit-identical to the per-layer QuantLinear path."""
+    from types import SimpleNamespace
+
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+
+    torch.manual_seed(1)
+    specs = {"l0": (384, 256, True), "l1": (256, 384, False), "l2": (128, 512, True)}
+    originals = {n: (torch.randn(o, i) * 0.02).half() for n, (o, i, _) in specs.items()}
+    res = {}
+    for batched in (True, False):
+        m = torch.nn.Sequential()
+        for n, (o, i, b) in specs.items():
+            lin = torch.nn.Linear(i, o, bias=b).half().to(DEV)
+            lin.weight.data.copy_(originals[n])
+            m.add_module(n, lin)
+        args = SimpleNamespace(w_bit=8, a_bit=16, w_group_size=128, w_symmetric=sym, w_format=fmt, quant_dim=0,
+                               approximate=apx, double_approximate=False)
+        quantize_model(m, args, batched=batched, verbose=False)
+        res[batched] = m
+    for n in specs:
+        a, b = getattr(res[True], n), getattr(res[False], n)
+        assert isinstance(a, QuantLinear) and isinstance(b, QuantLinear)
+        assert torch.equal(a.weight.data.view(torch.int16), b.weight.data.view(torch.int16)), n
+        assert torch.equal(a.scales.view(torch.int16), b.scales.view(torch.int16)), n
+        assert (a.zeros is None) == (b.zeros is None), n
+        if a.zeros is not None:
+            assert torch.equal(a.zeros.view(torch.int16), b.zeros.view(torch.int16)), n
+        assert bool(a.quantized) and a.approximate == b.approximate
+
+
 def test_errors_match_reference(K):
     from iron_weight_only_quant_amd.quant_funcs import pseudo_quantize_tensor
     from iron_weight_only_quant_amd.quant_linear import QuantLinear
