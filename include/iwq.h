@@ -154,10 +154,12 @@ int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld
  * parameters) and read it through LDS instead of running the bit-level codec per element; lut NULL
  * is the plain entry point.  Packed codes (out_codes) always take the ALU codec.
  * codec: IWQ_CODEC_FP (iwq_quantize_fp), IWQ_CODEC_GRID (iwq_fp4_grid; exp/mant ignored),
- * IWQ_CODEC_APX (iwq_quantize_fp_approx, single-aligned decode).
+ * IWQ_CODEC_APX (iwq_quantize_fp_approx, single-aligned decode), IWQ_CODEC_APX_DOUBLE
+ * (iwq_quantize_fp_approx with double_approx: per-code words of the quad decoder; one pass for
+ * fp16, quant_dim 0, group 32 / 64 / 128 and a group count divisible by 4, else two passes).
  */
 #define IWQ_FP_LUT_BYTES 65536
-enum iwq_fp_codec { IWQ_CODEC_FP = 0, IWQ_CODEC_GRID = 1, IWQ_CODEC_APX = 2 };
+enum iwq_fp_codec { IWQ_CODEC_FP = 0, IWQ_CODEC_GRID = 1, IWQ_CODEC_APX = 2, IWQ_CODEC_APX_DOUBLE = 3 };
 int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start, int hi_align_exp_field,
                      int tail_pad_bits, void* lut, int64_t lut_bytes, void* stream);
 int iwq_quantize_fp_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,

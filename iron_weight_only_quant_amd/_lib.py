@@ -32,7 +32,7 @@ EXPORTS = (
     "iwq_dequant_packed", "iwq_quantize_fp_batched",
 )
 
-IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX = 0, 1, 2
+IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX, IWQ_CODEC_APX_DOUBLE = 0, 1, 2, 3
 IWQ_FP_LUT_BYTES = 65536
 
 

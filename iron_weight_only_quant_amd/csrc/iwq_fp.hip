@@ -39,7 +39,7 @@ constexpr int BLOCK = 256;
 constexpr int WPB = BLOCK / WAVE;
 constexpr int UNIT = WAVE * 8;
 
-enum : int { CODEC_FP = 0, CODEC_GRID = 1, CODEC_APX = 2 };
+enum : int { CODEC_FP = 0, CODEC_GRID = 1, CODEC_APX = 2, CODEC_APXD = 3 };
 
 struct FpArgs {
   const char* w;
@@ -76,6 +76,48 @@ __host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
   return codec == CODEC_GRID ? 0x4600u /* 6.0 */ : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f.fp_max16);
 }
 
+// Double-approximate decoder (quant_linear.py:288-363), split at the quad: everything it needs from
+// ONE code except its sign is a function of |t| -- mpad (int8 bits) | ae << 8 (4 bits: E <= 4 for
+// every format whose fp_max fits fp16) | (magnitude code == 0) << 12 | outlier << 14 |
+// (outlier && ae == max exponent) << 15 -- and is tabled like the other decodes (CODEC_APXD); the
+// quad statistics (outlier count, max ae, any max-exponent outlier) then combine four such words.
+// A code equal to 0 (|t| == 0, or a positive t whose magnitude code is 0) decodes to 0 outright
+// (the reference's zero mask); a sign-only code does NOT: its int8 mantissa arithmetic can still
+// give -1 after a rounding shift by 8 (ATen's int8 >> 8 == -1).
+__device__ __forceinline__ uint32_t apxd_info(uint32_t code, const FpSpec& f) {
+  const uint32_t c = code & ((1u << (f.E + f.M)) - 1u);  // magnitude bits (sign ignored)
+  const int ef = w8((int)((c >> f.M) & ((1u << f.E) - 1u)));
+  const int mf = w8((int)(c & ((1u << f.M) - 1u)));
+  const int ae = ef == 0 ? 1 : ef;
+  const int mfull = w8(lsh8(ef == 0 ? 0 : 1, f.M) | mf);
+  const int mpad = f.tp >= 0 ? lsh8(mfull, f.tp) : rrsh8(mfull, -f.tp);
+  const bool outl = ae < f.hs || ae > f.hf;
+  const int maxv = (1 << f.E) - 1;
+  return ((uint32_t)mpad & 0xFFu) | ((uint32_t)ae << 8) | (c == 0u ? 1u << 12 : 0u) | (outl ? 1u << 14 : 0u) |
+         ((outl && ae == maxv) ? 1u << 15 : 0u);
+}
+
+// one element's decoded value from its own info word and the quad's four info bytes (info >> 8)
+__device__ __forceinline__ float apxd_decode(uint32_t own, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
+                                             const FpSpec& f, int cap, float scale_m) {
+  const int maxv = (1 << f.E) - 1;
+  const uint32_t cnt = ((b0 >> 6) & 1u) + ((b1 >> 6) & 1u) + ((b2 >> 6) & 1u) + ((b3 >> 6) & 1u);
+  const int gmax = (int)max(max(b0 & 15u, b1 & 15u), max(b2 & 15u, b3 & 15u));
+  const bool has_max = ((b0 | b1 | b2 | b3) & 0x80u) != 0;
+  int tgt = cnt <= 1 ? w8(f.hf) : gmax;
+  if (has_max) tgt = w8(maxv);
+  const int ae = (int)((own >> 8) & 15u);
+  const int mpad = (int)(int8_t)(uint8_t)(own & 0xFFu);
+  const int sh = w8(tgt - ae);
+  const int mr = rrsh8(mpad, sh > 0 ? sh : 0);
+  const int nsh = w8(-sh);
+  int ml = lsh8(mpad, nsh > 0 ? nsh : 0);
+  ml = ml > cap ? cap : ml;
+  const int mal = sh >= 0 ? mr : ml;
+  const float p2 = (float)(_Float16)__builtin_ldexpf(1.0f, w8(tgt - f.bias));
+  return f16r(f16r((float)mal * scale_m) * p2);  // fp16 ops: mant / 2^(M+tail) * 2^(tgt-bias)
+}
+
 template <int CODEC>
 __global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut, int32_t n, int32_t n8) {
   __shared__ uint16_t tab_buf[120];
@@ -92,11 +134,14 @@ __global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut,
         d = __builtin_rintf(uv / sc) * sc;
       } else if constexpr (CODEC == CODEC_APX) {
         d = fp_decode_aligned(fp_encode(u, f, tabs), f);
+      } else if constexpr (CODEC == CODEC_APXD) {
+        d = 0.0f;
       } else {
         d = fp_decode(fp_encode(u, f, tabs), f);
       }
     }
-    lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
+    if constexpr (CODEC == CODEC_APXD) lut[i] = (uint16_t)apxd_info(i < n ? fp_encode((uint32_t)i, f, tabs) : 0u, f);
+    else lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
   }
 }
 
@@ -399,6 +444,130 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   fp_flag_nan(a.nan_flag, any_nan);
 }
 
+// Double-approximate decode in ONE pass (g in {32, 64, 128}, quant_dim 0, group count % 4 == 0):
+// a quad is 4 consecutive groups at one in-group position, i.e. lanes l, l^LPG, l^2LPG, l^3LPG of
+// the same 512-element unit at the same element slot (4 LPG <= 64).  Per element: symmetric FP
+// t = clamp(RN16(w / s)) (packed on finite groups), its info word from the LDS table (exact ALU
+// codec on non-finite groups), one info byte per element exchanged with the 3 partners (6
+// ds_bpermute per unit), then the quad decode and RN16(v * s) -- the reference's two passes
+// through a code buffer (and k_apx_double's scattered quad reads) in one streaming pass.
+template <int G, bool GS>
+__global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
+  using F = Fmt<DT_F16>;
+  static_assert(G == 32 || G == 64 || G == 128, "quad = 4 groups inside one 64-lane unit");
+  extern __shared__ u32x4 lut_dyn[];
+  __shared__ uint16_t tab_buf[120];
+  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_BLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
+  const Log2Tabs tabs = stage_log2_tables(tab_buf);
+  const __attribute__((address_space(3))) uint16_t* lut = (const __attribute__((address_space(3))) uint16_t*)lut_dyn;
+  constexpr int WPBL = LUT_BLOCK / WAVE;
+  constexpr int UNROLL = 4;
+  constexpr int LPG = G / 8;
+  const FpSpec& f = a.f;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * WPBL + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * WPBL;
+  int64_t u0, cend;
+  if constexpr (GS) {
+    u0 = wave * UNROLL;
+    cend = min(u0 + UNROLL, a.total_units);
+  } else {
+    int64_t per = (a.total_units + nwaves - 1) / nwaves;
+    per = (per + UNROLL - 1) / UNROLL * UNROLL;
+    u0 = wave * per;
+    cend = min(u0 + per, a.total_units);
+  }
+  const _Float16 bnd = (_Float16)f.fp_max16;
+  const h2 bound2 = {bnd, bnd};
+  const int capr = (1 << (f.M + 1)) - 1;
+  const int cap = w8(f.tp >= 0 ? (capr << f.tp) : (capr >> (-f.tp)));
+  const float scale_m = (float)(_Float16)__builtin_ldexpf(1.0f, -(f.M + f.tp));
+  bool any_nan = false;
+  while (u0 < cend) {
+    const int32_t nu = (int32_t)min((int64_t)UNROLL, cend - u0);
+    Vec8<DT_F16> v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
+      v[k].load(a.w + ((k < nu && e < a.numel) ? e : 0) * F::BYTES);
+    }
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      if (k < nu) {  // wave-uniform
+        const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
+        int32_t mn, mx;
+        minmax8<DT_F16, true>(v[k], mn, mx);
+        group_max<LPG>(mx);
+        const FpParams p = fp_group_params<CODEC_APX, true>(mn, mx, f);
+        uint32_t info[8], sgz[8];  // sgz: bit 0 = code sign, bit 1 = code == 0
+        if (p.fast) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f2 df = __builtin_convertvector(as_h2(v[k].u[j]), f2);
+            h2 t = __builtin_convertvector(pk_div_f16vals(df, p.rs, p.s), h2);
+            t = pk_max(pk_min(t, bound2), -bound2);
+            const uint32_t tb = as_u32(t);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t th = (tb >> (16 * h)) & 0xFFFFu, u = th & 0x7FFFu;
+              const uint32_t inf_ = lut[u];
+              const uint32_t sg = (th >> 15) & (u != 0u ? 1u : 0u);  // fp_encode: |t| == 0 -> code 0
+              info[2 * j + h] = inf_;
+              sgz[2 * j + h] = sg | ((((inf_ >> 12) & 1u) && !sg) ? 2u : 0u);
+            }
+          }
+        } else {  // non-finite group: the exact chain (fp_apx_elem's t), ALU codec
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float t = div16(F::to_f(v[k].get(i)), p.s, p.rs, false);
+            t = clamp_nan(t, -f.fp_max16, f.fp_max16);
+            const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
+            const uint32_t code = fp_encode(tb, f, tabs);
+            info[i] = apxd_info(code, f);
+            sgz[i] = ((code >> (f.E + f.M)) & 1u) | (code == 0u ? 2u : 0u);
+          }
+        }
+        uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          x0 |= ((info[i] >> 8) & 0xFFu) << (8 * i);
+          x1 |= ((info[4 + i] >> 8) & 0xFFu) << (8 * i);
+        }
+        const uint32_t a0 = (uint32_t)__shfl_xor((int)x0, LPG), a1 = (uint32_t)__shfl_xor((int)x1, LPG);
+        const uint32_t b0 = (uint32_t)__shfl_xor((int)x0, 2 * LPG), b1 = (uint32_t)__shfl_xor((int)x1, 2 * LPG);
+        const uint32_t c0 = (uint32_t)__shfl_xor((int)a0, 2 * LPG), c1 = (uint32_t)__shfl_xor((int)a1, 2 * LPG);
+        Vec8<DT_F16> o;
+        bool nan8 = false;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int sh8 = 8 * (i & 3);
+          const uint32_t q0 = ((i < 4 ? x0 : x1) >> sh8) & 0xFFu, q1 = ((i < 4 ? a0 : a1) >> sh8) & 0xFFu;
+          const uint32_t q2 = ((i < 4 ? b0 : b1) >> sh8) & 0xFFu, q3 = ((i < 4 ? c0 : c1) >> sh8) & 0xFFu;
+          float dv = apxd_decode(info[i], q0, q1, q2, q3, f, cap, scale_m);
+          if (sgz[i] & 1u) dv = -dv;
+          if (sgz[i] & 2u) dv = 0.0f;                          // zero code
+          const float y = (float)(_Float16)opaque(dv * p.s);  // RN16(decoded * scales)
+          nan8 |= (y != y);
+          o.set(i, F::from_f(y));
+        }
+        if (e0 < a.numel) {
+          any_nan |= nan8;
+          o.store(a.out + e0 * F::BYTES);
+          if ((lane % LPG) == 0 && a.scales) store_param<DT_F16>(a.scales, e0 / G, p.s);
+        }
+      }
+    }
+    u0 += nu;
+    if constexpr (GS) {
+      if (u0 >= cend) {
+        u0 += (nwaves - 1) * UNROLL;
+        cend = min(u0 + UNROLL, a.total_units);
+      }
+    }
+  }
+  fp_flag_nan(a.nan_flag, any_nan);
+}
+
 template <int CODEC, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_fp_apply(SegArgs a, FpSpec f) {
   using F = Fmt<DT_F16>;
@@ -537,6 +706,30 @@ hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
     case 512: return launch_fp_lut_t<CODEC, 512, SYM>(a, st);
   }
   return hipErrorInvalidValue;
+}
+
+template <int G>
+hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
+  auto kern = k_apx_double_lut<G, false>;
+  auto kern_gs = k_apx_double_lut<G, true>;
+  const size_t lds = (size_t)a.lut_n8 * 2;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
+  constexpr int WPBL = LUT_BLOCK / WAVE;
+  int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
+  const int64_t cap = (int64_t)cu_count() * occ;
+  const bool gs = a.total_units >= 2 * cap * WPBL * 4;
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_apx_double_lut(int64_t g, const FpArgs& a, hipStream_t st) {
+  if (g == 32) return launch_apx_double_lut_t<32>(a, st);
+  if (g == 64) return launch_apx_double_lut_t<64>(a, st);
+  return launch_apx_double_lut_t<128>(a, st);
 }
 
 hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpArgs& a, hipStream_t st) {
@@ -776,6 +969,28 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
   if (vc % group != 0) return IWQ_ERR_GROUP;
   const int64_t G = vr * vc / group;
   if ((G * group) % 4 != 0) return IWQ_ERR_SHAPE;  // quads of 4 (reference ValueError)
+  if (lut && dtype == IWQ_F16 && quant_dim == 0 && (group == 32 || group == 64 || group == 128) && (G & 3) == 0 &&
+      ld_w == cols && ld_out == cols && aligned16p(w) && aligned16p(out_deq) && aligned16p(lut) &&
+      !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+    FpSpec f{};
+    int st = fp_spec(exp_bits, mant_bits, f);
+    if (st != IWQ_OK) return st;
+    f.hs = hi_align_start;
+    f.hf = hi_align_exp_field;
+    f.tp = tail_pad_bits;
+    FpArgs a{};
+    a.w = static_cast<const char*>(w);
+    a.out = static_cast<char*>(out_deq);
+    a.scales = out_scales;
+    a.numel = rows * cols;
+    a.total_units = (a.numel + UNIT - 1) / UNIT;
+    a.f = f;
+    a.nan_flag = nan_flag;
+    a.lut = static_cast<const uint16_t*>(lut);
+    a.lut_n8 = (int32_t)((lut_bound_bits(CODEC_APXD, f) + 1 + 7) / 8 * 8);
+    IWQ_HIP_FP(launch_apx_double_lut(group, a, static_cast<hipStream_t>(stream)));
+    return IWQ_OK;
+  }
   const int64_t cb = apx_codes_bytes(rows, cols, exp_bits, mant_bits);
   if (!workspace || workspace_bytes < cb || !aligned16p(workspace)) return IWQ_ERR_WORKSPACE;
   uint8_t* codes = static_cast<uint8_t*>(workspace);
@@ -821,7 +1036,7 @@ int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld
 
 int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start, int hi_align_exp_field,
                      int tail_pad_bits, void* lut, int64_t lut_bytes, void* stream) {
-  if (codec != CODEC_FP && codec != CODEC_GRID && codec != CODEC_APX) return IWQ_ERR_ARG;
+  if (codec != CODEC_FP && codec != CODEC_GRID && codec != CODEC_APX && codec != CODEC_APXD) return IWQ_ERR_ARG;
   if (codec == CODEC_GRID) { exp_bits = 2; mant_bits = 1; }
   FpSpec f{};
   const int st = fp_spec(exp_bits, mant_bits, f);
@@ -837,6 +1052,7 @@ int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start,
   uint16_t* t = static_cast<uint16_t*>(lut);
   if (codec == CODEC_GRID) hipLaunchKernelGGL(k_fp_build_lut<CODEC_GRID>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
   else if (codec == CODEC_APX) hipLaunchKernelGGL(k_fp_build_lut<CODEC_APX>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
+  else if (codec == CODEC_APXD) hipLaunchKernelGGL(k_fp_build_lut<CODEC_APXD>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
   else hipLaunchKernelGGL(k_fp_build_lut<CODEC_FP>, dim3(blocks), dim3(BLOCK), 0, s, f, t, n, n8);
   IWQ_HIP_FP(hipGetLastError());
   return IWQ_OK;

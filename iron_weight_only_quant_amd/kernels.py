@@ -225,8 +225,8 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     wsb = int(lib.iwq_approx_workspace_bytes(rows, cols, int(exp_bits), int(mant_bits), int(group), int(quant_dim),
                                              int(bool(double_approx))))
     ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
-    lut = (_luts.get(dev, L.IWQ_CODEC_APX, exp_bits, mant_bits, hi_align_start, hi_align_exp_field, tail_pad_bits)
-           if use_lut and not double_approx else None)
+    lut = (_luts.get(dev, L.IWQ_CODEC_APX_DOUBLE if double_approx else L.IWQ_CODEC_APX, exp_bits, mant_bits,
+                     hi_align_start, hi_align_exp_field, tail_pad_bits) if use_lut else None)
     with torch.cuda.device(dev):
         st = lib.iwq_quantize_fp_approx_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
                                             int(mant_bits), int(group), int(quant_dim), int(hi_align_start),

@@ -438,18 +438,23 @@ def test_fp4_grid_exhaustive_lut(K):
 
 @pytest.mark.parametrize("hs,hf,tp", [(12, 15, 1), (4, 7, 2), (1, 3, 0), (2, 5, -1)])
 def test_fp_approx_exhaustive_lut(K, hs, hf, tp):
-    """Approximate (single-aligned) table path on every finite fp16 in [-fp_max, fp_max] at scale 1
-    vs the ALU path, E4M3 and E2M1."""
+    """Approximate table paths on every finite fp16 in [-fp_max, fp_max] at scale 1 vs the ALU path,
+    E4M3 and E2M1: single-aligned decode, and the one-pass double-approximate decode (rows shuffled
+    so each quad of groups mixes exponents) vs the two-pass reference-order kernel."""
     from oracle import fp_codec as C
     xs = np.arange(1 << 16, dtype=np.uint32).astype(np.uint16).view(np.float16)
     for e, m in ((4, 3), (2, 1)):
         _, fp_max = C.fp_params(e, m)
         vals = xs[np.isfinite(xs) & (np.abs(xs.astype(np.float32)) <= fp_max)]
         rows, _ = _scale_one_rows(vals, fp_max)
-        x = to_dev(rows, "float16")
-        a = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, False)
-        b = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, False, use_lut=False)
-        assert torch.equal(a.out.view(torch.int16), b.out.view(torch.int16)), (e, m, hs, hf, tp)
+        rows = np.concatenate([rows, np.zeros(((-rows.shape[0]) % 4, 128), np.float16)])  # quads of groups
+        rng = np.random.default_rng(e * 100 + hs)
+        x = to_dev(rows[rng.permutation(rows.shape[0])], "float16")  # mix exponents inside each quad
+        for double in (False, True):
+            a = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, double)
+            b = K.quantize_fp_approx(x, e, m, 128, 0, hs, hf, tp, double, use_lut=False)
+            assert torch.equal(a.out.view(torch.int16), b.out.view(torch.int16)), (e, m, hs, hf, tp, double)
+            assert torch.equal(a.scales.view(torch.int16), b.scales.view(torch.int16)), (e, m, hs, hf, tp, double)
 
 
 @pytest.mark.parametrize("flags", FLAG_SETS)

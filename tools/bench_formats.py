@@ -82,9 +82,9 @@ def main():
         ("bfp_w4_g128", lambda w, out: K.quantize_bfp(w, 4, g, out=out), 4 * n),
         ("bfp_w8_g32", lambda w, out: K.quantize_bfp(w, 8, 32, out=out), 4 * n),
         ("approx_fp8_g128", lambda w, out: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, False, out=out), 4 * n + 2 * G),
-        # double: FP pass writes codes (1 B), decode pass reads codes + scales, writes dequant
+        # double: one pass (k_apx_double_lut, g in {32, 64, 128}): read w, write dequant + scales
         ("approx_fp8_g128_double", lambda w, out: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, True, out=out),
-         2 * n + n + n + 2 * n + 2 * G + 2 * G),
+         4 * n + 2 * G),
     ]
     only = set(a.only.split(",")) if a.only else None
     for name, f1, algo in cases:
