@@ -76,38 +76,52 @@ __host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
   return codec == CODEC_GRID ? 0x4600u /* 6.0 */ : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f.fp_max16);
 }
 
-// Double-approximate decoder (quant_linear.py:288-363), split at the quad: everything it needs from
-// ONE code except its sign is a function of |t| -- mpad (int8 bits) | ae << 8 (4 bits: E <= 4 for
-// every format whose fp_max fits fp16) | (magnitude code == 0) << 12 | outlier << 14 |
-// (outlier && ae == max exponent) << 15 -- and is tabled like the other decodes (CODEC_APXD); the
-// quad statistics (outlier count, max ae, any max-exponent outlier) then combine four such words.
-// A code equal to 0 (|t| == 0, or a positive t whose magnitude code is 0) decodes to 0 outright
-// (the reference's zero mask); a sign-only code does NOT: its int8 mantissa arithmetic can still
-// give -1 after a rounding shift by 8 (ATen's int8 >> 8 == -1).
-__device__ __forceinline__ uint32_t apxd_info(uint32_t code, const FpSpec& f) {
-  const uint32_t c = code & ((1u << (f.E + f.M)) - 1u);  // magnitude bits (sign ignored)
+// Double-approximate decoder (quant_linear.py:288-363), split at the quad.  Per code (sign aside)
+// everything the quad statistics need is a function of |t|: the INFO word = magnitude code (7 bits)
+// | ae << 8 (4 bits: E <= 4 for every format whose fp_max fits fp16) | (magnitude code == 0) << 12
+// | outlier << 14 | (outlier && ae == max exponent) << 15, tabled per |t| (CODEC_APXD, table 1).
+// The decoded value then depends only on (magnitude code, quad target exponent tgt in [0, 15]):
+// table 2 (128 x 16 fp16, after table 1) holds RN16(RN16(mal * 2^-(M+tail)) * 2^(tgt-bias)) with the
+// reference's int8 mantissa arithmetic.  A code equal to 0 (|t| == 0, or a positive t whose
+// magnitude code is 0) decodes to 0 outright (the reference's zero mask); a sign-only code does NOT:
+// its int8 mantissa arithmetic can still give -1 after a rounding shift by 8 (ATen's int8 >> 8 == -1).
+constexpr int APXD_T2 = 128 * 16;  // entries of table 2
+
+__device__ __forceinline__ void apxd_fields(uint32_t c, const FpSpec& f, int& ae, int& mpad) {
   const int ef = w8((int)((c >> f.M) & ((1u << f.E) - 1u)));
   const int mf = w8((int)(c & ((1u << f.M) - 1u)));
-  const int ae = ef == 0 ? 1 : ef;
+  ae = ef == 0 ? 1 : ef;
   const int mfull = w8(lsh8(ef == 0 ? 0 : 1, f.M) | mf);
-  const int mpad = f.tp >= 0 ? lsh8(mfull, f.tp) : rrsh8(mfull, -f.tp);
+  mpad = f.tp >= 0 ? lsh8(mfull, f.tp) : rrsh8(mfull, -f.tp);
+}
+
+__device__ __forceinline__ uint32_t apxd_info(uint32_t code, const FpSpec& f) {
+  const uint32_t c = code & ((1u << (f.E + f.M)) - 1u);  // magnitude bits (sign ignored)
+  int ae, mpad;
+  apxd_fields(c, f, ae, mpad);
   const bool outl = ae < f.hs || ae > f.hf;
   const int maxv = (1 << f.E) - 1;
-  return ((uint32_t)mpad & 0xFFu) | ((uint32_t)ae << 8) | (c == 0u ? 1u << 12 : 0u) | (outl ? 1u << 14 : 0u) |
+  return c | ((uint32_t)ae << 8) | (c == 0u ? 1u << 12 : 0u) | (outl ? 1u << 14 : 0u) |
          ((outl && ae == maxv) ? 1u << 15 : 0u);
 }
 
-// one element's decoded value from its own info word and the quad's four info bytes (info >> 8)
-__device__ __forceinline__ float apxd_decode(uint32_t own, uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3,
-                                             const FpSpec& f, int cap, float scale_m) {
-  const int maxv = (1 << f.E) - 1;
+// the quad's target exponent from its four info bytes (info >> 8)
+__device__ __forceinline__ int apxd_tgt(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3, const FpSpec& f) {
   const uint32_t cnt = ((b0 >> 6) & 1u) + ((b1 >> 6) & 1u) + ((b2 >> 6) & 1u) + ((b3 >> 6) & 1u);
   const int gmax = (int)max(max(b0 & 15u, b1 & 15u), max(b2 & 15u, b3 & 15u));
   const bool has_max = ((b0 | b1 | b2 | b3) & 0x80u) != 0;
   int tgt = cnt <= 1 ? w8(f.hf) : gmax;
-  if (has_max) tgt = w8(maxv);
-  const int ae = (int)((own >> 8) & 15u);
-  const int mpad = (int)(int8_t)(uint8_t)(own & 0xFFu);
+  if (has_max) tgt = w8((1 << f.E) - 1);
+  return tgt;
+}
+
+// decoded value (before the code's sign) of magnitude code c at target exponent tgt (table 2)
+__device__ __forceinline__ float apxd_value(uint32_t c, int tgt, const FpSpec& f) {
+  int ae, mpad;
+  apxd_fields(c, f, ae, mpad);
+  const int capr = (1 << (f.M + 1)) - 1;
+  const int cap = w8(f.tp >= 0 ? (capr << f.tp) : (capr >> (-f.tp)));
+  const float scale_m = (float)(_Float16)__builtin_ldexpf(1.0f, -(f.M + f.tp));
   const int sh = w8(tgt - ae);
   const int mr = rrsh8(mpad, sh > 0 ? sh : 0);
   const int nsh = w8(-sh);
@@ -142,6 +156,13 @@ __global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut,
     }
     if constexpr (CODEC == CODEC_APXD) lut[i] = (uint16_t)apxd_info(i < n ? fp_encode((uint32_t)i, f, tabs) : 0u, f);
     else lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
+  }
+  if constexpr (CODEC == CODEC_APXD) {  // table 2: (magnitude code, tgt) -> value, after table 1
+    for (int32_t i = blockIdx.x * BLOCK + threadIdx.x; i < APXD_T2; i += gridDim.x * BLOCK) {
+      const uint32_t c = (uint32_t)i >> 4;
+      const float v = c < (1u << (f.E + f.M)) ? apxd_value(c, i & 15, f) : 0.0f;
+      lut[n8 + i] = (uint16_t)Fmt<DT_F16>::from_f(v);
+    }
   }
 }
 
@@ -457,9 +478,10 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
   static_assert(G == 32 || G == 64 || G == 128, "quad = 4 groups inside one 64-lane unit");
   extern __shared__ u32x4 lut_dyn[];
   __shared__ uint16_t tab_buf[120];
-  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_BLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
+  for (int32_t i = threadIdx.x; i < (a.lut_n8 + APXD_T2) / 8; i += LUT_BLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
   const Log2Tabs tabs = stage_log2_tables(tab_buf);
   const __attribute__((address_space(3))) uint16_t* lut = (const __attribute__((address_space(3))) uint16_t*)lut_dyn;
+  const __attribute__((address_space(3))) _Float16* t2 = (const __attribute__((address_space(3))) _Float16*)(lut + a.lut_n8);
   constexpr int WPBL = LUT_BLOCK / WAVE;
   constexpr int UNROLL = 4;
   constexpr int LPG = G / 8;
@@ -479,9 +501,6 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
   }
   const _Float16 bnd = (_Float16)f.fp_max16;
   const h2 bound2 = {bnd, bnd};
-  const int capr = (1 << (f.M + 1)) - 1;
-  const int cap = w8(f.tp >= 0 ? (capr << f.tp) : (capr >> (-f.tp)));
-  const float scale_m = (float)(_Float16)__builtin_ldexpf(1.0f, -(f.M + f.tp));
   bool any_nan = false;
   while (u0 < cend) {
     const int32_t nu = (int32_t)min((int64_t)UNROLL, cend - u0);
@@ -543,7 +562,8 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
           const int sh8 = 8 * (i & 3);
           const uint32_t q0 = ((i < 4 ? x0 : x1) >> sh8) & 0xFFu, q1 = ((i < 4 ? a0 : a1) >> sh8) & 0xFFu;
           const uint32_t q2 = ((i < 4 ? b0 : b1) >> sh8) & 0xFFu, q3 = ((i < 4 ? c0 : c1) >> sh8) & 0xFFu;
-          float dv = apxd_decode(info[i], q0, q1, q2, q3, f, cap, scale_m);
+          const int tgt = apxd_tgt(q0, q1, q2, q3, f);  // in [0, 15] (launcher: 0 <= hf <= 15)
+          float dv = (float)t2[((info[i] & 0x7Fu) << 4) | (uint32_t)tgt];
           if (sgz[i] & 1u) dv = -dv;
           if (sgz[i] & 2u) dv = 0.0f;                          // zero code
           const float y = (float)(_Float16)opaque(dv * p.s);  // RN16(decoded * scales)
@@ -712,7 +732,7 @@ template <int G>
 hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
   auto kern = k_apx_double_lut<G, false>;
   auto kern_gs = k_apx_double_lut<G, true>;
-  const size_t lds = (size_t)a.lut_n8 * 2;
+  const size_t lds = (size_t)(a.lut_n8 + APXD_T2) * 2;
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
   constexpr int WPBL = LUT_BLOCK / WAVE;
@@ -970,6 +990,7 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
   const int64_t G = vr * vc / group;
   if ((G * group) % 4 != 0) return IWQ_ERR_SHAPE;  // quads of 4 (reference ValueError)
   if (lut && dtype == IWQ_F16 && quant_dim == 0 && (group == 32 || group == 64 || group == 128) && (G & 3) == 0 &&
+      hi_align_exp_field >= 0 && hi_align_exp_field <= 15 && exp_bits <= 4 &&
       ld_w == cols && ld_out == cols && aligned16p(w) && aligned16p(out_deq) && aligned16p(lut) &&
       !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     FpSpec f{};
@@ -1046,7 +1067,8 @@ int iwq_fp_build_lut(int codec, int exp_bits, int mant_bits, int hi_align_start,
   f.tp = tail_pad_bits;
   const int32_t n = (int32_t)lut_bound_bits(codec, f) + 1;
   const int32_t n8 = (n + 7) / 8 * 8;
-  if (!lut || !aligned16p(lut) || lut_bytes < (int64_t)n8 * 2 || n8 > LUT_MAX) return IWQ_ERR_WORKSPACE;
+  const int64_t need = ((int64_t)n8 + (codec == CODEC_APXD ? APXD_T2 : 0)) * 2;
+  if (!lut || !aligned16p(lut) || lut_bytes < need || n8 > LUT_MAX) return IWQ_ERR_WORKSPACE;
   const unsigned blocks = (unsigned)((n8 + BLOCK - 1) / BLOCK);
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint16_t* t = static_cast<uint16_t*>(lut);
