@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "weights quantized GB/s + PPL delta, Llama-2-7B 4-bit g=128 at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+MODEL_NAME = {"llama2-7b": "Llama-2-7B", "llama2-70b": "Llama-2-70B", "opt-125m": "OPT-125M"}
 
 
 
@@ -46,6 +47,9 @@ def parse():
                          "llama2-70b: the 560 weights are bin-packed over the ranks (strong scaling, configs[3])")
     ap.add_argument("--gather", action="store_true",
                     help="also time the all_gather of packed codes+scales to rank 0 (RCCL), reported separately")
+    ap.add_argument("--scatter", action="store_true",
+                    help="strong scaling of the chosen model: its weights start on rank 0 and are scattered to "
+                         "their owners over RCCL point-to-point first (timed separately as scatter_ms, never in value)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppl", action="store_true", help="skip the PPL-harness plumbing run (random-init OPT-125M)")
@@ -123,6 +127,40 @@ def make_weights(model, rank, world):
     return ws, names, shapes
 
 
+def scatter_weights(model, rank, world):
+    """--scatter (strong scaling): the whole model's fp16 weights start on rank 0 (one flat buffer
+    per destination rank, synthetic) and are sent to their owners over RCCL point-to-point (all
+    sends in flight together: rank 0's xGMI links to every other GPU run in parallel), timed alone
+    (max over ranks).  Returns this rank's weights as views into its received buffer."""
+    from iron_weight_only_quant_amd import kernels, shard
+    shapes = shard.model_linear_shapes(model)
+    bins = shard.plan_shards(shapes, world)
+    layouts = [shard.bin_layout(shapes, b) for b in bins]
+    index = {n: i for i, (n, _) in enumerate(shapes)}
+    sends, recv = None, None
+    if rank == 0:
+        sends = []
+        for lay, tot in layouts:
+            flat = torch.empty(tot, dtype=torch.float16, device="cuda")
+            for name, off, (r, c) in lay:
+                kernels.fill_synthetic(flat[off: off + r * c].view(r, c), seed=index[name])
+            sends.append(flat)
+    else:
+        recv = torch.empty(layouts[rank][1], dtype=torch.float16, device="cuda")
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    mine = shard.scatter_from_rank0(sends, recv)
+    torch.cuda.synchronize()
+    barrier(world)
+    ms = max_over_ranks((time.perf_counter() - t0) * 1e3, world)
+    if rank == 0:
+        sends = [mine]  # drop the other ranks' copies on rank 0
+    views = shard.views_of(mine, layouts[rank][0])
+    names = [n for n, _, _ in layouts[rank][0]]
+    return [views[n] for n in names], names, shapes, round(ms, 3)
+
+
 def ppl_plumbing(bits, group, symmetric, chunks=8, seqlen=2048):
     """Second half of the metric, as far as it can be measured offline: the SequentialPPLEvaluator
     arithmetic (main.py:42-140) before and after quantize_model on a RANDOM-INIT OPT-125M-shaped
@@ -176,7 +214,9 @@ def time_gather(plan, names, all_shapes, args, ws_n):
     """All_gather of the packed results (codes + scales/zeros) to rank 0 over RCCL, timed alone."""
     from iron_weight_only_quant_amd import shard
     import torch.distributed as dist
-    res = shard.ShardResult(names, plan.codes, plan.scales, plan.zeros)
+    order = sorted(range(len(names)), key=lambda i: names[i])  # gather_to_rank0 unpacks in name order
+    res = shard.ShardResult([names[i] for i in order], [plan.codes[i] for i in order],
+                            [plan.scales[i] for i in order], [plan.zeros[i] for i in order])
     bins = shard.plan_shards(all_shapes, ws_n)
     names_per_rank = [[all_shapes[i][0] for i in b] for b in bins]
     shp = dict(all_shapes)
@@ -304,10 +344,14 @@ def main():
     ws_n, rank, _ = init_dist(args)
     from iron_weight_only_quant_amd import kernels
 
-    strong = args.model == "llama2-70b"
+    strong = args.model == "llama2-70b" or args.scatter  # --scatter: the model is partitioned, not replicated
     if strong:
         args.inplace = True  # 70B fp16 = 137 GB: in place (QuantLinear semantics) so N=1 fits in 288 GB
-    weights, names, all_shapes = make_weights(args.model, rank, ws_n)
+    scatter_ms = None
+    if args.scatter and ws_n > 1:
+        weights, names, all_shapes, scatter_ms = scatter_weights(args.model, rank, ws_n)
+    else:
+        weights, names, all_shapes = make_weights(args.model, rank, ws_n)
     numel = sum(w.numel() for w in weights)
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric,
                              outs=weights if args.inplace else None, want_codes=args.gather)
@@ -381,8 +425,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ws_n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": (f"Llama-2-70B 560 Linear weights bin-packed over {ws_n} GPU(s) "
-                                    if strong else f"Llama-2-7B all {len(weights)} Linear weights per GPU ")
+            "config": {"workload": (f"{MODEL_NAME[args.model]} {len(all_shapes)} Linear weights bin-packed over "
+                                    f"{ws_n} GPU(s) " if strong else
+                                    f"{MODEL_NAME[args.model]} all {len(weights)} Linear weights per GPU ")
                                    + f"({total_numel} fp16 weights total), INT{args.bits} g={args.group} "
                                    f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
                                    f"{'in-place' if args.inplace else 'out-of-place'} dequant + scales/zeros, "
@@ -398,6 +443,7 @@ def main():
             "ppl_delta": None,
             "ppl_plumbing": ppl,
             "gather_ms": gather_ms,
+            "scatter_ms": scatter_ms,
         }
         print(json.dumps(rec), flush=True)
     if ws_n > 1:

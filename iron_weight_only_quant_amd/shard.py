@@ -4,9 +4,11 @@ The reference quantizes layer after layer on whichever GPU accelerate placed the
 (utils.py:43 device_map="balanced", quant_wrapper.py:52-82) — one GPU busy at a time.  Here
 every Linear weight is an independent unit of work, so the set is bin-packed by bytes over the
 ranks (one process per GPU) and each rank quantizes its shard with ONE batched launch; there is no
-exchange in the data path.  Optionally the packed results (int codes + fp16 scales/zeros, ~1/4 of
-the fp16 bytes) are gathered to rank 0 with a single torch.distributed collective (RCCL over xGMI
-on MI355X, gloo in the CPU tests).
+exchange in the data path.  Optionally the fp16 weights start on rank 0 and are scattered to the
+ranks that own them (`scatter_from_rank0`: one point-to-point send per destination, all in flight
+together, so rank 0's xGMI links to the other GPUs run in parallel), and the packed results (int
+codes + fp16 scales/zeros, ~1/4 of the fp16 bytes) are gathered back to rank 0 with a single
+torch.distributed collective (RCCL over xGMI on MI355X, gloo in the CPU tests).
 """
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -133,3 +135,45 @@ def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bi
                 off += G * esz
             result[name] = (codes, scales, zeros)
     return result
+
+
+def bin_layout(shapes: Sequence[Tuple[str, Tuple[int, int]]], bin_: List[int]):
+    """Flat layout of one rank's weights: [(name, element offset, (rows, cols))], total elements.
+    Tensors are placed back to back in name order, each start rounded to 8 elements (16 B)."""
+    items, off = [], 0
+    for i in sorted(bin_, key=lambda i: shapes[i][0]):
+        name, (r, c) = shapes[i]
+        items.append((name, off, (r, c)))
+        off += (r * c + 7) // 8 * 8
+    return items, off
+
+
+def views_of(flat: torch.Tensor, layout) -> Dict[str, torch.Tensor]:
+    """{name: [rows, cols] view} into a rank's flat weight buffer (no copies)."""
+    return {name: flat[off: off + r * c].view(r, c) for name, off, (r, c) in layout}
+
+
+def scatter_from_rank0(send_flats: Optional[List[torch.Tensor]], recv_flat: Optional[torch.Tensor], pg=None):
+    """Rank 0 holds every rank's flat weight buffer (send_flats[r]); every other rank receives its
+    own into recv_flat.  One isend per destination, issued together (batch_isend_irecv), so on an
+    xGMI node rank 0 drives its links to the 7 other GPUs concurrently.  Returns this rank's flat
+    buffer (rank 0: send_flats[0], no copy)."""
+    import torch.distributed as dist
+    rank = dist.get_rank(pg)
+    world = dist.get_world_size(pg)
+    # gloo (CPU tests / 1-GPU rehearsal) has no device-memory point-to-point: stage through the host
+    staged = dist.get_backend(pg) == "gloo" and any(
+        t is not None and t.is_cuda for t in ([recv_flat] + list(send_flats or [])))
+    host = (lambda t: t.cpu()) if staged else (lambda t: t)
+    if rank == 0:
+        ops = [dist.P2POp(dist.isend, host(send_flats[r]), r, group=pg) for r in range(1, world)]
+        rbuf = None
+    else:
+        rbuf = torch.empty(recv_flat.shape, dtype=recv_flat.dtype) if staged else recv_flat
+        ops = [dist.P2POp(dist.irecv, rbuf, 0, group=pg)]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if rank != 0 and staged:
+        recv_flat.copy_(rbuf)
+    return send_flats[0] if rank == 0 else recv_flat

@@ -96,3 +96,54 @@ def test_gloo_world2_gather_matches_single_process(sym):
         assert np.array_equal(scales.view(np.uint16), r.scales.reshape(-1).view(np.uint16))
         if not sym:
             assert np.array_equal(zeros.view(np.uint16), r.zeros.reshape(-1).view(np.uint16))
+
+
+def _scatter_worker(rank, world, port, out_q):
+    import torch.distributed as dist
+    from iron_weight_only_quant_amd import shard
+    from oracle.synth import synth
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shapes = _small_model()
+        bins = shard.plan_shards(shapes, world)
+        layouts = [shard.bin_layout(shapes, b) for b in bins]
+        sends, recv = None, None
+        if rank == 0:  # rank 0 holds the whole model, one flat buffer per destination rank
+            sends = []
+            for lay, tot in layouts:
+                flat = torch.zeros(tot, dtype=torch.float16)
+                for name, off, (r, c) in lay:
+                    i = [n for n, _ in shapes].index(name)
+                    flat[off: off + r * c] = torch.from_numpy(synth(500 + i, (r, c), "float16").reshape(-1))
+                sends.append(flat)
+        else:
+            recv = torch.empty(layouts[rank][1], dtype=torch.float16)
+        mine = shard.scatter_from_rank0(sends, recv)
+        got = {k: v.numpy().copy() for k, v in shard.views_of(mine, layouts[rank][0]).items()}
+        out_q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_scatter_from_rank0():
+    """Every rank receives exactly its bin's weights, bit for bit, from rank 0."""
+    from oracle.synth import synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shapes = _small_model()
+    from iron_weight_only_quant_amd import shard
+    bins = shard.plan_shards(shapes, 2)
+    for r in range(2):
+        assert set(res[r]) == {shapes[i][0] for i in bins[r]}
+        for name, arr in res[r].items():
+            i = [n for n, _ in shapes].index(name)
+            assert np.array_equal(arr.view(np.uint16), synth(500 + i, shapes[i][1], "float16").view(np.uint16))

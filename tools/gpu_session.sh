@@ -69,6 +69,7 @@ if [[ $WHAT == *dist2* ]]; then
   export IWQ_DIST_BACKEND=gloo
   step dist2_7b 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
   step dist2_70b 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --model llama2-70b --steps 3 --warmup 1
+  step dist2_7b_sg 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --model llama2-7b --steps 3 --warmup 1 --scatter --gather --no-shapes
   unset IWQ_DIST_BACKEND
 fi
 if [[ $WHAT == *pmc* ]]; then
