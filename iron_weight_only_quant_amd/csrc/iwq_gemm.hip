@@ -438,6 +438,146 @@ void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
   }
 }
 
+// Persistent form of k_w4a16_gemv: the grid is the resident set of workgroups and each one walks
+// column groups c = blockIdx.x, blockIdx.x + gridDim.x, ...  X is staged into LDS ONCE per
+// workgroup, and each wave's code ring runs across column-group boundaries (the first PF steps of
+// group i+1 are in flight while group i's partial tiles are summed), so there is neither a
+// second-round tail (70B gate: 1792 groups over 1024 slots) nor a per-workgroup restart.
+template <int PF, int S, int T, bool XLDS>
+__global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv_p(GemmArgs a, int ngroups) {
+  constexpr int WPB = S * T;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile = wid % T, ks = wid / T;
+  const int q = lane >> 4, r16 = lane & 15;
+  const int nks = a.K / BK;
+  const int nj = nks > ks ? (nks - ks + S - 1) / S : 0;  // steps of this wave per column group
+  const int ngi = ngroups > (int)blockIdx.x ? (ngroups - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int total = ngi * nj;                            // ring length of this wave
+  const int64_t crow = a.K / 2;
+  const int arow = r16 < a.M ? r16 : a.M - 1;
+  const int xpitch = a.K * 2 + 16;
+  const int xbytes = XLDS ? (a.M * xpitch + 15) / 16 * 16 : 0;
+  float* red = reinterpret_cast<float*>(dsm + xbytes);   // [WPB][256] partial tiles
+  const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
+  const h2 k1024 = h2{(_Float16)1024.0f, (_Float16)1024.0f}, k64 = h2{(_Float16)64.0f, (_Float16)64.0f};
+  u32x4 bc[PF];
+  _Float16 sv[PF], zv[PF];
+  u32x4 xa[XLDS ? 1 : PF][4];
+  auto col_of = [&](int g) { return ((int)blockIdx.x + (g / nj) * (int)gridDim.x) * T * 16 + tile * 16 + r16; };
+  auto load = [&](int g, int u) {
+    const int kt = ks + (g % nj) * S;
+    const int n = col_of(g);
+    bc[u] = __builtin_nontemporal_load(gp<u32x4>(a.codes + (int64_t)n * crow + q * 16 + kt * (BK / 2)));
+    const int kk = kt * BK + 32 * q;
+    const int64_t gi = (int64_t)n * a.gpr + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group);
+    sv[u] = gp<_Float16>(a.scales)[gi];
+    zv[u] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
+    if constexpr (!XLDS) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < total) load(u, u);
+
+  if constexpr (XLDS) {
+    const int cpr = a.K / 8;
+    for (int m = 0; m < a.M; ++m) {
+      const _Float16* xr = a.x + (int64_t)m * a.lda;
+      for (int c = threadIdx.x; c < cpr; c += WPB * 64) {
+        const u32x4 d = *gp<u32x4>(xr + 8 * c);
+        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+      }
+    }
+    __syncthreads();
+  }
+  const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+  const DqConst dq;
+  // sum the WPB partial tiles of column group cg and store; every wave of the workgroup calls this
+  // exactly once per column group (2 barriers), waves without k-steps (nj == 0) included
+  auto flush = [&](const f4& acc, int cg) {
+    *reinterpret_cast<f4*>(red + wid * 256 + lane * 4) = acc;
+    __syncthreads();
+    for (int o = threadIdx.x; o < T * 256; o += WPB * 64) {
+      const int t = o >> 8, e = o & 255;  // e = lane' * 4 + reg of the C layout
+      const int ln = e >> 2, reg = e & 3;
+      const int row = 4 * (ln >> 4) + reg, col = (cg * T + t) * 16 + (ln & 15);
+      if (row < a.M) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < S; ++k) v += red[(k * T + t) * 256 + e];
+        if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
+        gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+      }
+    }
+    __syncthreads();
+  };
+  if (nj == 0) {
+    for (int gi = 0; gi < ngi; ++gi) flush((f4){0.f, 0.f, 0.f, 0.f}, (int)blockIdx.x + gi * (int)gridDim.x);
+    return;
+  }
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < total; g0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int g = g0 + u;
+      if (g >= total) break;
+      const int kt = ks + (g % nj) * S;
+      const h2 s2 = h2{sv[u], sv[u]};
+      const h2 z2 = h2{zv[u], zv[u]};
+      const h2 z1024 = z2 + k1024, z64 = z2 + k64;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        h8 af;
+        if constexpr (XLDS) {
+          af = *reinterpret_cast<const h8*>(xsrow + kt * (BK * 2) + 16 * s);
+        } else {
+          const u32x4 x4 = xa[u][s];
+          const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
+                            perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
+          af = __builtin_bit_cast(h8, pa);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dequant8(bc[u][s], z1024, z64, s2, dq), acc, 0, 0, 0);
+      }
+      if (g + PF < total) load(g + PF, u);
+      if ((g % nj) == nj - 1) {  // this wave's last step of the column group
+        flush(acc, (int)blockIdx.x + (g / nj) * (int)gridDim.x);
+        acc = (f4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+}
+
+template <int PF, int S, int T>
+void launch_gemv_p(const GemmArgs& a, hipStream_t st) {
+  const int64_t xbytes = ((int64_t)a.M * (a.K * 2 + 16) + 15) / 16 * 16;
+  const bool xlds = xbytes <= XLDS_MAX;
+  const size_t lds = (xlds ? (size_t)xbytes : 0) + (size_t)S * T * 256 * 4;
+  const int ngroups = a.N / (16 * T);
+  int dev = 0, cus = 256, occ = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (xlds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_w4a16_gemv_p<PF, S, T, true>, S * T * 64, lds) !=
+            hipSuccess || occ <= 0)
+      occ = 1;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_w4a16_gemv_p<PF, S, T, false>, S * T * 64, lds) !=
+            hipSuccess || occ <= 0)
+      occ = 1;
+  }
+  int blocks = cus * occ;
+  if (blocks > ngroups) blocks = ngroups;
+  if (xlds) hipLaunchKernelGGL((k_w4a16_gemv_p<PF, S, T, true>), dim3(blocks), dim3(S * T * 64), lds, st, a, ngroups);
+  else hipLaunchKernelGGL((k_w4a16_gemv_p<PF, S, T, false>), dim3(blocks), dim3(S * T * 64), lds, st, a, ngroups);
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_w4a16_big: prefill (large M), per-channel scales.  256x256 output tile per 512-thread
 // workgroup (8 waves as 2 (M) x 4 (N), 128x64 per wave = 8x4 MFMA tiles), K in steps of 64.
@@ -814,6 +954,13 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 101: launch_gemv<4, 8, 1, 1>(a, st, true); break;
       case 12: launch_gemv<2, 4, 1>(a, st, true); break;
       case 13: launch_gemv<2, 16, 1>(a, st, true); break;
+      // persistent variants (k_w4a16_gemv_p): measured 0-20 % SLOWER than the default on every Llama
+      // decode shape (profiles/r01_gemv_persistent.jsonl) -- the per-group flush barriers stall the
+      // code ring more than the second-round tail costs; kept for A/B
+      case 14: launch_gemv_p<2, 8, 1>(a, st); break;
+      case 15: launch_gemv_p<4, 8, 1>(a, st); break;
+      case 16: launch_gemv_p<2, 4, 1>(a, st); break;
+      case 17: launch_gemv_p<4, 4, 1>(a, st); break;
       default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
     }
   } else if (N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 && !(flags & IWQ_FLAG_FORCE_GENERIC) &&

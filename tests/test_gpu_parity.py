@@ -547,13 +547,33 @@ def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     # default (decode kernel for M <= 16), the tiled prefill kernel, and every decode variant
-    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 14) if M <= 16):
+    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 18) if M <= 16):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b, flags=flags)
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (flags, float(err.max()))
     # and against the reference forward semantics: F.linear on the dequantized fp16 weight
     y2 = torch.nn.functional.linear(x, r.out, b)
     assert float((y.float() - y2.float()).abs().max()) <= 4 * float(err.max()) + 2e-3
+
+
+@pytest.mark.parametrize("Kd", [256, 1152, 4096])
+@pytest.mark.parametrize("M", [1, 16])
+def test_gemv_persistent_many_groups(K, Kd, M):
+    """Persistent decode GEMV with more column groups than resident workgroups (each workgroup walks
+    several groups), k-split waves with unequal step counts (Kd = 1152: 9 steps over 8 waves) and
+    waves without any step (Kd = 256): every variant vs an fp32 GEMM on the fake-quant weight."""
+    N = 24576
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 77)
+    r = K.quantize_minmax(w, 4, 128, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (0, 14, 15, 16, 17):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, 128, N, b, flags=K.gemm_variant_flags(v))
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (v, float(err.max()))
 
 
 def test_w4a16_gemm_identity_layout(K):
@@ -565,7 +585,7 @@ def test_w4a16_gemm_identity_layout(K):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
     for m in (1, 5, 16):  # decode kernels: rows of the identity pick weight columns exactly
-        for v in range(0, 14):
+        for v in range(0, 18):
             y = K.w4a16_gemm(x[:m].contiguous(), r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
             assert torch.equal(y, r.out.t()[:m].contiguous()), (m, v)
 
