@@ -68,6 +68,8 @@ enum iwq_status {
 /* flags */
 #define IWQ_FLAG_FORCE_GENERIC 0x1u  /* use the universal segmented path (testing / A-B)            */
 #define IWQ_FLAG_BATCH_CODES 0x100u  /* batched entry: every entry carries out_codes              */
+#define IWQ_FLAG_TILED_CODES 0x200u  /* iwq_w4a16_gemm: codes are in the decode tile layout
+                                        (iwq_tile_codes); M <= 16 only                            */
 /* bits 16..23: kernel tuning variant of the batched fp16/g128/asym kernel (0 = default; A/B only) */
 #define IWQ_FLAG_VARIANT(v) (((unsigned)(v) & 0xFFu) << 16)
 
@@ -220,6 +222,14 @@ int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int p
 int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
                    unsigned flags, void* stream);
+
+/*
+ * Row-major packed 4-bit codes [N, K/2] -> the decode tile layout read by iwq_w4a16_gemm with
+ * IWQ_FLAG_TILED_CODES: for each 16-row tile t and 128-k step kt a contiguous 1 KiB block at
+ * byte (t * K/128 + kt) * 1024, byte 16 l + i of it = row 16 t + (l % 16), code byte
+ * 64 kt + 16 (l / 16) + i.  N % 16 == 0, K % 128 == 0; out holds N * K / 2 bytes.
+ */
+int iwq_tile_codes(const void* codes, int64_t N, int64_t K, void* out, void* stream);
 
 /*
  * Packed codes -> fp16 W_deq [N, K] (contiguous: ld_out == K, 16-B aligned), bit-identical to the

@@ -312,7 +312,10 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
 // ---------------------------------------------------------------------------------------------
 constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X image (2+ workgroups per CU)
 
-template <int PF, int S, int T, bool XLDS, int PROBE = 0>
+// TILED: codes in the decode tile layout (iwq_tile_codes): the 1 KiB a wave loads for one 128-k
+// step of its 16 columns is contiguous (lane l = 16 q + r at byte 16 l), instead of 16 column rows x
+// 64 B at a K/2 stride -- one DRAM-friendly 1 KiB burst per load instruction.
+template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false>
 __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   constexpr int WPB = S * T;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
@@ -326,7 +329,8 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   const int64_t crow = a.K / 2;
   const int arow = r16 < a.M ? r16 : a.M - 1;
   const int xpitch = a.K * 2 + 16;                       // LDS row pitch (bytes), +16 vs bank conflicts
-  const uint8_t* cbase = a.codes + (int64_t)n * crow + q * 16;
+  const uint8_t* cbase = TILED ? a.codes + (int64_t)(blockIdx.x * T + tile) * nks * 1024 + lane * 16
+                               : a.codes + (int64_t)n * crow + q * 16;
   const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
   const bool perch = a.gpr == 1;                          // one scale/zero per column: hoisted
 
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   u32x4 xa[XLDS ? 1 : PF][4];
   auto load = [&](int j, int u) {
     const int kt = ks + j * S;
-    bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * (BK / 2)));
+    bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * (TILED ? 1024 : BK / 2)));
     if (!perch) {
       const int kk = kt * BK + 32 * q;
       const int64_t gi = (int64_t)n * a.gpr + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group);
@@ -425,16 +429,29 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   }
 }
 
-template <int PF, int S, int T, int PROBE = 0>
+template <int PF, int S, int T, int PROBE = 0, bool TILED = false>
 void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * T));
   const size_t red = (size_t)S * T * 256 * 4;
   if (allow_lds && xbytes <= XLDS_MAX) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
-    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), lds, st, a);
   } else {
-    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE>), dim3(blocks), dim3(S * T * 64), red, st, a);
+    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), red, st, a);
+  }
+}
+
+// row-major packed codes [N, K/2] -> decode tile layout: block (t, kt) of 1 KiB at (t * K/128 + kt) KiB,
+// byte 16 l + i = row 16 t + (l & 15), code byte 64 kt + 16 (l >> 4) + i.  One thread per 16 B.
+__global__ __launch_bounds__(256) void k_tile_codes(const uint8_t* codes, uint8_t* out, int64_t K, int64_t nchunks) {
+  const int64_t nks = K / BK;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
+    const int64_t blk = i >> 6, l = i & 63;
+    const int64_t t = blk / nks, kt = blk - t * nks;
+    const int64_t row = 16 * t + (l & 15);
+    const u32x4 v = *gp<u32x4>(codes + row * (K / 2) + 64 * kt + 16 * (l >> 4));
+    *gp<u32x4>(out + i * 16) = v;
   }
 }
 
@@ -869,6 +886,23 @@ __global__ __launch_bounds__(256) void k_dequant_packed(GemmArgs a, int64_t tota
 
 extern "C" {
 
+int iwq_tile_codes(const void* codes, int64_t N, int64_t K, void* out, void* stream) {
+  if (!codes || !out) return IWQ_ERR_ARG;
+  if (N <= 0 || K <= 0 || N % 16 != 0 || K % BK != 0) return IWQ_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(codes) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u)) return IWQ_ERR_ARG;
+  const int64_t nchunks = N * (K / 2) / 16;
+  int64_t blocks = (nchunks + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_tile_codes, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(codes), static_cast<uint8_t*>(out), K, nchunks);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    iwq::last_hip_error() = (int)e;
+    return IWQ_ERR_HIP;
+  }
+  return IWQ_OK;
+}
+
 int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros, int n_bits, int64_t group,
                        int64_t N, int64_t K, void* out, int64_t ld_out, void* stream) {
   if (!codes || !scales || !out) return IWQ_ERR_ARG;
@@ -934,7 +968,11 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
   a.gshift = (g & (g - 1)) == 0 ? __builtin_ctzll((unsigned long long)g) : -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const unsigned variant = (flags >> 16) & 0xFFu;
-  if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+  if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
+    if (M > 16) return IWQ_ERR_ARG;
+    if (variant == 1) launch_gemv<4, 8, 1, 0, true>(a, st, true);
+    else launch_gemv<2, 8, 1, 0, true>(a, st, true);
+  } else if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     switch (variant) {
       case 1:  // previous decode kernel (A/B reference)
         if (K >= 4096) hipLaunchKernelGGL(k_w4a16_decode<8>, dim3((unsigned)(N / 16)), dim3(512), 0, st, a);

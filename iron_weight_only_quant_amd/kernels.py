@@ -309,8 +309,12 @@ def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: in
 
 
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
-               n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0) -> torch.Tensor:
-    """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA)."""
+               n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
+               tiled: bool = False) -> torch.Tensor:
+    """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA).
+    tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only."""
+    if tiled:
+        flags |= L.IWQ_FLAG_TILED_CODES
     L.require_device(x)
     lib = L.load()
     K = x.shape[-1]
@@ -325,6 +329,18 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
                                 L.stream_handle(x.device))
     _raise_for(st, "iwq_w4a16_gemm")
     return y.reshape(*x.shape[:-1], N)
+
+
+def tile_codes(codes: torch.Tensor, N: int, K: int) -> torch.Tensor:
+    """Row-major packed 4-bit codes -> the decode tile layout (iwq_tile_codes): each 1 KiB a GEMV
+    wave loads is contiguous.  Use with w4a16_gemm(..., tiled=True) for M <= 16."""
+    L.require_device(codes)
+    lib = L.load()
+    out = torch.empty(N * K // 2, dtype=torch.uint8, device=codes.device)
+    with torch.cuda.device(codes.device):
+        st = lib.iwq_tile_codes(L.ptr(codes), int(N), int(K), L.ptr(out), L.stream_handle(codes.device))
+    _raise_for(st, "iwq_tile_codes")
+    return out
 
 
 def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor], n_bits: int,
@@ -342,12 +358,16 @@ def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[to
 
 
 def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
-                 n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None,
+                 tiled_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
-    decode batches (M <= GEMV_MAX_M), dequant-once + hipBLASLt (F.linear) above, where the library
-    GEMM on a freshly dequantized weight beats the fused MFMA kernel."""
+    decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), dequant-once
+    + hipBLASLt (F.linear) above, where the library GEMM on a freshly dequantized weight beats the
+    fused MFMA kernel."""
     K = x.shape[-1]
     if x.numel() // K <= GEMV_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
+        if tiled_codes is not None:
+            return w4a16_gemm(x, tiled_codes, scales, zeros, n_bits, group, N, bias, tiled=True)
         return w4a16_gemm(x, codes, scales, zeros, n_bits, group, N, bias)
     w = dequant_packed(codes, scales, zeros, n_bits, group, N, K)
     return torch.nn.functional.linear(x, w, bias)

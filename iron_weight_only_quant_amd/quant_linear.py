@@ -93,7 +93,7 @@ class QuantLinear(nn.Module):
         # the reference's buffers (quant_linear.py:451-458), registered without the per-name checks
         self._buffers.update(quantized=torch.tensor(False), scales=None, zeros=None, weight_fp4=None,
                              weight_fp6=None, weight_fp8=None, weight_bfp_mantissa=None,
-                             weight_bfp_exponent=None, qweight=None)
+                             weight_bfp_exponent=None, qweight=None, qweight_tiled=None)
         if _init_weight:
             self.reset_parameters()
 
@@ -134,6 +134,11 @@ class QuantLinear(nn.Module):
             self.scales = res.scales.view(-1, 1)
             self.zeros = res.zeros.view(-1, 1) if res.zeros is not None else None
             self.qweight = res.codes
+            self.qweight_tiled = None
+            if (self.fused_forward == "auto" and res.codes is not None and self.quant_dim == 0
+                    and self.w_bit <= 4 and w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0):
+                # decode batches read the codes in the GEMV tile layout (1 KiB contiguous per load)
+                self.qweight_tiled = kernels.tile_codes(res.codes, w.shape[0], w.shape[1])
             self.weight_fp4 = None
             self.weight_fp6 = None
             self.weight_fp8 = None
@@ -220,6 +225,13 @@ class QuantLinear(nn.Module):
         fused = self.fused_forward
         if fused == "auto":
             fused = input.numel() // max(1, self.in_features) <= kernels.GEMV_MAX_M
+            if (fused and self.qweight_tiled is not None and self.weight_format == "int"
+                    and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
+                                                     self.w_group_size)
+                    and (self.bias is None or self.bias.dtype == torch.float16)):
+                return kernels.w4a16_gemm(input, self.qweight_tiled, self.scales.view(-1),
+                                          None if self.zeros is None else self.zeros.view(-1), self.w_bit,
+                                          self.w_group_size, self.out_features, self.bias, tiled=True)
         if (fused and self.weight_format == "int" and self.quant_dim == 0 and self.qweight is not None
                 and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
                                                  self.w_group_size)

@@ -576,6 +576,26 @@ def test_gemv_persistent_many_groups(K, Kd, M):
         assert bool((err <= tol).all()), (v, float(err.max()))
 
 
+@pytest.mark.parametrize("group", [-2, 128])
+def test_gemv_tiled_layout_identical(K, group):
+    """The decode tile layout changes only where the codes are read from: outputs are bit-identical
+    to the row-major kernel (same arithmetic, same order), for M = 1, 7, 16."""
+    N, Kd = 384, 4352
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 55)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    tiled = K.tile_codes(r.codes, N, Kd)
+    assert tiled.numel() == r.codes.numel()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    for m in (1, 7, 16):
+        x = (torch.randn(m, Kd, device=DEV) * 0.5).half()
+        y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
+        y1 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True)
+        assert torch.equal(y0.view(torch.int16), y1.view(torch.int16)), m
+    with pytest.raises(Exception):
+        K.w4a16_gemm(torch.randn(32, Kd, device=DEV).half(), tiled, r.scales, r.zeros, 4, group, N, tiled=True)
+
+
 def test_w4a16_gemm_identity_layout(K):
     """A = I with an asymmetric weight: catches any transposed or permuted output/operand mapping."""
     N, Kd = 128, 128
@@ -628,6 +648,7 @@ def test_quantlinear_fused_forward_auto(K, monkeypatch):
     monkeypatch.setattr(QLm.kernels, "w4a16_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
     lin = torch.nn.Linear(512, 256, bias=True).half().to(DEV)
     q = QLm.QuantLinear.from_linear(lin, w_bit=4, w_group_size=128, symmetric=False, fused_forward="auto")
+    assert q.qweight_tiled is not None and q.qweight_tiled.numel() == q.qweight.numel()
     for shape, fused in (((1, 512), True), ((2, 8, 512), True), ((4, 64, 512), False)):
         calls.clear()
         x = torch.randn(*shape, device=DEV).half()

@@ -96,7 +96,15 @@ def main():
                 t_f = timed(fused, a.reps) if M >= 1024 else timed_graph(fused, 50)
                 flops = 2.0 * M * N * K
                 wbytes = int(r.codes.numel() + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0))
+                t_tiled = None
+                if M <= 16:
+                    tiled = kernels.tile_codes(r.codes, N, K)
+                    ft = lambda: kernels.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, a.group, N, flags=fl, tiled=True)
+                    ft()
+                    t_tiled = timed_graph(ft, 50)
                 rec = {"shape": name, "M": M, "N": N, "K": K, "group": a.group, "variant": v,
+                       "tiled_ms": round(t_tiled, 4) if t_tiled else None,
+                       "tiled_weight_GBps": round(int(r.codes.numel() + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0)) / t_tiled / 1e6, 1) if t_tiled else None,
                        "fused_ms": round(t_f, 4), "fused_tflops": round(flops / t_f / 1e9, 1),
                        "fused_frac_peak": round(flops / t_f / 1e9 / PEAK_TFLOPS, 4),
                        "fused_weight_GBps": round(wbytes / t_f / 1e6, 1),
