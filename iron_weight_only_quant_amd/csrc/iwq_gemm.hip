@@ -970,8 +970,23 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
   const unsigned variant = (flags >> 16) & 0xFFu;
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
     if (M > 16) return IWQ_ERR_ARG;
-    if (variant == 1) launch_gemv<4, 8, 1, 0, true>(a, st, true);
-    else launch_gemv<2, 8, 1, 0, true>(a, st, true);
+    switch (variant) {  // same shapes as the row-major variants of the same number (A/B)
+      case 1:
+      case 2: launch_gemv<4, 8, 1, 0, true>(a, st, true); break;
+      case 4: launch_gemv<4, 4, 2, 0, true>(a, st, true); break;
+      case 5: launch_gemv<4, 4, 4, 0, true>(a, st, true); break;
+      case 7: launch_gemv<6, 4, 2, 0, true>(a, st, true); break;
+      case 8: launch_gemv<4, 16, 1, 0, true>(a, st, true); break;
+      case 9: launch_gemv<8, 4, 1, 0, true>(a, st, true); break;
+      case 10: launch_gemv<4, 2, 4, 0, true>(a, st, true); break;
+      case 12: launch_gemv<2, 4, 1, 0, true>(a, st, true); break;
+      case 13: launch_gemv<2, 16, 1, 0, true>(a, st, true); break;
+      case 18: launch_gemv<3, 8, 1, 0, true>(a, st, true); break;
+      case 19: launch_gemv<8, 8, 1, 0, true>(a, st, true); break;
+      case 20: launch_gemv<2, 8, 2, 0, true>(a, st, true); break;
+      case 100: launch_gemv<2, 8, 1, 1, true>(a, st, true); break;  // probe: no dequant
+      default: launch_gemv<2, 8, 1, 0, true>(a, st, true); break;
+    }
   } else if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     switch (variant) {
       case 1:  // previous decode kernel (A/B reference)

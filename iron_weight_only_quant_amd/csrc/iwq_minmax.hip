@@ -732,7 +732,7 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
 //                    derives the tensor's scale / zero point and quantizes its share
 // 6 B per fp16 element of HBM traffic (read, read, write) instead of the segmented path's scalar walk.
 // =============================================================================================
-template <int DT, bool SYM>
+template <int DT, bool SYM, bool NTL>
 __global__ __launch_bounds__(BLOCK) void k_tensor_reduce(const char* w, int64_t nunits, int32_t* partial) {
   using F = Fmt<DT>;
   constexpr int UN = 4;
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_reduce(const char* w, int64_t 
 #pragma unroll
     for (int k = 0; k < UN; ++k) {
       const int64_t u = u0 + k * nthreads;
-      v[k].load(w + (u < nunits ? u : 0) * 8 * F::BYTES);
+      v[k].template load<NTL>(w + (u < nunits ? u : 0) * 8 * F::BYTES);
     }
 #pragma unroll
     for (int k = 0; k < UN; ++k) {
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_reduce(const char* w, int64_t 
   }
 }
 
-template <int DT, bool SYM, int CODES>
+template <int DT, bool SYM, int CODES, bool NTL, bool REV>
 __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out, uint8_t* codes, void* scales,
                                                         void* zeros, int64_t nunits, const int32_t* partial,
                                                         int nparts, int n_bits, uint32_t* nan_flag) {
@@ -792,9 +792,10 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
   }
   bool any_nan = false;
   const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
-  for (int64_t u = (int64_t)blockIdx.x * BLOCK + threadIdx.x; u < nunits; u += nthreads) {
+  for (int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x; t < nunits; t += nthreads) {
+    const int64_t u = REV ? nunits - 1 - t : t;  // REV: the units the reduce read last (MALL) first
     Vec8<DT> v, o;
-    v.load(w + u * 8 * F::BYTES);
+    v.template load<NTL>(w + u * 8 * F::BYTES);
     uint32_t c[4];
     any_nan |= quant8<DT, SYM>(v, p, n_bits, o, c);
     if (out) o.store(out + u * 8 * F::BYTES);
@@ -899,12 +900,13 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
 // Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
 // selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
 template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true, bool GS = false>
-hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st) {
+hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st, int max_blocks_per_cu = 8) {
   static int cache[64] = {0};
   auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS, SHARED, GS>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-  const int64_t cap = (int64_t)device_cu_count() * resident_blocks_per_cu(kern, cache);
+  const int per_cu = resident_blocks_per_cu(kern, cache);
+  const int64_t cap = (int64_t)device_cu_count() * (per_cu < max_blocks_per_cu ? per_cu : max_blocks_per_cu);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
@@ -957,6 +959,10 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 6: return launch_variant_t<4, true, true, true, true, true>(a, st);    // grid-stride + prefetch
     case 7: return launch_variant_t<2, true, true, true, true, true>(a, st);    // grid-stride, UNROLL 2, prefetch
     case 8: return launch_variant_t<1, true, true, true, true, true>(a, st);    // grid-stride, UNROLL 1, prefetch
+    case 9: return launch_variant_t<4, false, true, true>(a, st, 7);            // default kernel, 7 waves/SIMD
+    case 10: return launch_variant_t<4, false, true, true>(a, st, 6);           // default kernel, 6 waves/SIMD
+    case 11: return launch_variant_t<4, false, true, true>(a, st, 4);           // default kernel, 4 waves/SIMD
+    case 12: return launch_variant_t<4, false, true, true>(a, st, 8);           // default kernel (same as 0)
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
@@ -1102,41 +1108,56 @@ hipError_t launch_seg(int dt, bool sym, const SegArgs& a, hipStream_t st) {
 
 constexpr int TENSOR_PARTS_MAX = 4096;
 
+// Per-tensor variants (flags bits 16..23; profiles/r01_ab_tensor.jsonl):
+//   0/2: temporal loads in both passes (default: cold 11008x4096 51.1 -> 49.0 us, 4096^2 22.6 -> 20.0 us)
+//   1: non-temporal loads in both passes (the previous default)
+//   3: temporal loads, apply walks the tensor backwards (the most recently read units first): no gain
+template <int DT, bool SYM, int CODES, bool NTL, bool REV>
+void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nunits,
+                        int64_t blocks, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+  hipLaunchKernelGGL((k_tensor_reduce<DT, SYM, NTL>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
+                     static_cast<const char*>(w), nunits, ws);
+  hipLaunchKernelGGL((k_tensor_apply<DT, SYM, CODES, NTL, REV>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
+                     static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales,
+                     zeros, nunits, ws, (int)blocks, n_bits, nan_flag);
+}
+
 template <int DT, bool SYM, int CODES>
 hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
-                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int variant) {
   const int64_t nunits = numel / 8;
   int64_t blocks = (int64_t)device_cu_count() * 8;
   const int64_t need = (nunits + BLOCK - 1) / BLOCK;
   if (blocks > need) blocks = need;
   if (blocks > TENSOR_PARTS_MAX) blocks = TENSOR_PARTS_MAX;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL((k_tensor_reduce<DT, SYM>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
-                     static_cast<const char*>(w), nunits, ws);
-  hipLaunchKernelGGL((k_tensor_apply<DT, SYM, CODES>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
-                     static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales,
-                     zeros, nunits, ws, (int)blocks, n_bits, nan_flag);
+  if (variant == 1)
+    launch_tensor_pair<DT, SYM, CODES, true, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
+  else if (variant == 3)
+    launch_tensor_pair<DT, SYM, CODES, false, true>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
+  else
+    launch_tensor_pair<DT, SYM, CODES, false, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   return hipGetLastError();
 }
 
 template <int DT, bool SYM>
 hipError_t launch_tensor_c(int codes, const void* w, void* out, void* cd, void* sc, void* zr, int64_t numel,
-                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
-  if (codes == 0) return launch_tensor_t<DT, SYM, 0>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
-  if (codes == 4) return launch_tensor_t<DT, SYM, 4>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
-  return launch_tensor_t<DT, SYM, 8>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int v) {
+  if (codes == 0) return launch_tensor_t<DT, SYM, 0>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
+  if (codes == 4) return launch_tensor_t<DT, SYM, 4>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
+  return launch_tensor_t<DT, SYM, 8>(w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
 }
 
 hipError_t launch_tensor(int dt, bool sym, int codes, const void* w, void* out, void* cd, void* sc, void* zr,
-                         int64_t numel, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
+                         int64_t numel, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int v) {
   if (dt == IWQ_F16)
-    return sym ? launch_tensor_c<DT_F16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
-               : launch_tensor_c<DT_F16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+    return sym ? launch_tensor_c<DT_F16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v)
+               : launch_tensor_c<DT_F16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
   if (dt == IWQ_BF16)
-    return sym ? launch_tensor_c<DT_BF16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
-               : launch_tensor_c<DT_BF16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
-  return sym ? launch_tensor_c<DT_F32, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st)
-             : launch_tensor_c<DT_F32, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st);
+    return sym ? launch_tensor_c<DT_BF16, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v)
+               : launch_tensor_c<DT_BF16, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
+  return sym ? launch_tensor_c<DT_F32, true>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v)
+             : launch_tensor_c<DT_F32, false>(codes, w, out, cd, sc, zr, numel, ws, n_bits, nan_flag, st, v);
 }
 
 int group_geometry(int64_t rows, int64_t cols, int64_t group, int quant_dim, int64_t& L, int64_t& G) {
@@ -1216,7 +1237,8 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     const int64_t need = iwq_workspace_bytes(rows, cols, group, quant_dim);
     if (!workspace || workspace_bytes < need || !aligned16(workspace)) return IWQ_ERR_WORKSPACE;
     IWQ_HIP(launch_tensor(dtype, sym, codes, w, out_deq, out_codes, out_scales, sym ? nullptr : out_zeros,
-                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s));
+                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s,
+                          (int)((flags >> 16) & 0xFFu)));
     return IWQ_OK;
   }
   if (!generic && quant_dim == 0 && group != IWQ_GROUP_PER_TENSOR && L % 8 == 0 && L <= ROW_MAX_L && al && fastbits) {

@@ -310,9 +310,10 @@ def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: in
 
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
-               tiled: bool = False) -> torch.Tensor:
+               tiled: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA).
-    tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only."""
+    tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only.
+    out: optional contiguous fp16 [M, N] destination (rows of x flattened)."""
     if tiled:
         flags |= L.IWQ_FLAG_TILED_CODES
     L.require_device(x)
@@ -322,7 +323,13 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     if x2.stride(-1) != 1 or x2.data_ptr() % 16 or x2.stride(0) % 8:
         x2 = x2.contiguous()
     M = x2.shape[0]
-    y = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    if out is None:
+        y = torch.empty((M, N), dtype=torch.float16, device=x.device)
+    else:
+        if (out.dtype != torch.float16 or out.device != x.device or not out.is_contiguous()
+                or out.numel() != M * N):
+            raise ValueError("w4a16_gemm: out must be a contiguous fp16 tensor of M*N elements on x's device")
+        y = out.view(M, N)
     with torch.cuda.device(x.device):
         st = lib.iwq_w4a16_gemm(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                 int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, int(flags),

@@ -594,6 +594,17 @@ def test_gemv_tiled_layout_identical(K, group):
         assert torch.equal(y0.view(torch.int16), y1.view(torch.int16)), m
     with pytest.raises(Exception):
         K.w4a16_gemm(torch.randn(32, Kd, device=DEV).half(), tiled, r.scales, r.zeros, 4, group, N, tiled=True)
+    # tiled A/B variants: same S (k-split) => same summation order as the row-major variant of that
+    # number (18-20 have the default's S = 8); out= writes in place
+    x = (torch.randn(5, Kd, device=DEV) * 0.5).half()
+    y = torch.empty(5, N, dtype=torch.float16, device=DEV)
+    for v in (1, 2, 4, 5, 7, 8, 9, 10, 12, 13, 18, 19, 20):
+        rv = v if v in (2, 4, 5, 7, 8, 9, 10, 12, 13) else (2 if v == 1 else 0)
+        y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(rv))
+        y1 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v),
+                          tiled=True, out=y)
+        assert y1.data_ptr() == y.data_ptr()
+        assert torch.equal(y0.view(torch.int16), y.view(torch.int16)), v
 
 
 def test_w4a16_gemm_identity_layout(K):
@@ -668,7 +679,8 @@ def test_per_tensor_fast_path(K, dtype):
     xd = to_dev(x, dtype)
     for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
-        for flags in FLAG_SETS:
+        # + per-tensor kernel-pair variants 1 (non-temporal) and 3 (apply walks backwards)
+        for flags in FLAG_SETS + [K.gemm_variant_flags(1), K.gemm_variant_flags(3)]:
             r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
             assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
             assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)

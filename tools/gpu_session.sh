@@ -38,6 +38,9 @@ fi
 if [[ $WHAT == *b70* ]]; then
   step bench70b 900 python bench.py --model llama2-70b --steps 5 --warmup 2 --cpu-seconds 8
 fi
+if [[ $WHAT == *gemvcold* ]]; then
+  step gemv_cold 600 python tools/bench_gemv_cold.py ${GEMV_ARGS:-}
+fi
 if [[ $WHAT == *gemm* ]]; then
   step bench_gemm 600 python tools/bench_gemm.py ${GEMM_ARGS:-}
 fi
