@@ -429,6 +429,159 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   }
 }
 
+// k_w4a16_gemv_ct: the same weight stream for 4 <= M <= 16, where X, not the codes, dominates the
+// on-chip traffic: k_w4a16_gemv reads (or stages) X once per 16-column tile, M * 256 B per 1 KiB of
+// codes (M = 16: 4x the code bytes from L2).  Here each wave applies one A fragment to CT column
+// tiles (CT code loads per k-step, CT accumulators), so X traffic per code byte drops CT-fold.
+// Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits.
+template <int PF, int S, int CT, bool XLDS, bool TILED>
+__global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int lane = threadIdx.x & 63;
+  const int ks = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int tile0 = blockIdx.x * CT;
+  const int nks = a.K / BK;
+  const int nj = nks > ks ? (nks - ks + S - 1) / S : 0;
+  const int64_t crow = a.K / 2;
+  const int arow = r16 < a.M ? r16 : a.M - 1;
+  const int xpitch = a.K * 2 + 16;
+  const int64_t tstride = TILED ? (int64_t)nks * 1024 : 16 * crow;  // code bytes between column tiles
+  const uint8_t* cbase = TILED ? a.codes + (int64_t)tile0 * tstride + lane * 16
+                               : a.codes + (int64_t)(tile0 * 16 + r16) * crow + q * 16;
+  const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
+  const bool perch = a.gpr == 1;
+
+  _Float16 sc0[CT], zz0[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int n = (tile0 + c) * 16 + r16;
+    sc0[c] = perch ? gp<_Float16>(a.scales)[n] : (_Float16)0.f;
+    zz0[c] = perch ? (a.zeros ? gp<_Float16>(a.zeros)[n] : (_Float16)a.zsym) : (_Float16)0.f;
+  }
+  const h2 k1024 = h2{(_Float16)1024.0f, (_Float16)1024.0f}, k64 = h2{(_Float16)64.0f, (_Float16)64.0f};
+  u32x4 bc[PF][CT];
+  _Float16 sv[PF][CT], zv[PF][CT];
+  u32x4 xa[XLDS ? 1 : PF][4];
+  auto load = [&](int j, int u) {
+    const int kt = ks + j * S;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+      bc[u][c] = __builtin_nontemporal_load(gp<u32x4>(cbase + c * tstride + kt * (TILED ? 1024 : BK / 2)));
+    if (!perch) {
+      const int kk = kt * BK + 32 * q;
+      const int gk = a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int64_t gi = (int64_t)((tile0 + c) * 16 + r16) * a.gpr + gk;
+        sv[u][c] = gp<_Float16>(a.scales)[gi];
+        zv[u][c] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
+      }
+    }
+    if constexpr (!XLDS) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nj) load(u, u);
+
+  if constexpr (XLDS) {
+    const int cpr = a.K / 8;
+    for (int m = 0; m < a.M; ++m) {
+      const _Float16* xr = a.x + (int64_t)m * a.lda;
+      for (int c = threadIdx.x; c < cpr; c += S * 64) {
+        const u32x4 d = *gp<u32x4>(xr + 8 * c);
+        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+      }
+    }
+    __syncthreads();
+  }
+  const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+  const DqConst dq;
+
+  f4 acc[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) acc[c] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nj; j0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int j = j0 + u;
+      if (j >= nj) break;
+      const int kt = ks + j * S;
+      h2 s2[CT], z1024[CT], z64[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        s2[c] = perch ? h2{sc0[c], sc0[c]} : h2{sv[u][c], sv[u][c]};
+        const h2 z2 = perch ? h2{zz0[c], zz0[c]} : h2{zv[u][c], zv[u][c]};
+        z1024[c] = z2 + k1024;
+        z64[c] = z2 + k64;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        h8 af;
+        if constexpr (XLDS) {
+          af = *reinterpret_cast<const h8*>(xsrow + kt * (BK * 2) + 16 * s);
+        } else {
+          const u32x4 x4 = xa[u][s];
+          const u32x4 pa = {perm(x4.z, x4.x, 0x05040100u), perm(x4.z, x4.x, 0x07060302u),
+                            perm(x4.w, x4.y, 0x05040100u), perm(x4.w, x4.y, 0x07060302u)};
+          af = __builtin_bit_cast(h8, pa);
+        }
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
+                                                          acc[c], 0, 0, 0);
+      }
+      if (j + PF < nj) load(j + PF, u);
+    }
+  }
+  if constexpr (XLDS) __syncthreads();
+  float* red = reinterpret_cast<float*>(dsm);  // [S][CT][256]
+#pragma unroll
+  for (int c = 0; c < CT; ++c) *reinterpret_cast<f4*>(red + (ks * CT + c) * 256 + lane * 4) = acc[c];
+  __syncthreads();
+  for (int o = threadIdx.x; o < CT * 256; o += S * 64) {
+    const int c = o >> 8, e = o & 255;
+    const int ln = e >> 2, reg = e & 3;
+    const int row = 4 * (ln >> 4) + reg, col = (tile0 + c) * 16 + (ln & 15);
+    if (row < a.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) v += red[(k * CT + c) * 256 + e];
+      if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
+      gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+    }
+  }
+}
+
+// Column tiles per wave for the decode default (cold sweep, profiles/r01_gemv_ct.jsonl): X traffic
+// only matters from M = 4 on, and a CT-fold smaller grid must still cover the chip: CT = 4 when that
+// leaves >= 256 workgroups (or >= 160 at M >= 8: 7B gate/up), CT = 2 for >= 256 workgroups once M*K
+// is large (70B down, K = 28672); else the one-tile kernel.  70B gate M = 16: 58.5 -> 30.7 us.
+inline int gemv_auto_ct(int64_t M, int64_t N, int64_t K) {
+  if (M < 4) return 1;
+  if (N / 64 >= 256 || (M >= 8 && N / 64 >= 160)) return 4;
+  if (N / 32 >= 256 && M * K >= 65536) return 2;
+  return 1;
+}
+
+template <int PF, int S, int CT, bool TILED>
+void launch_gemv_ct(const GemmArgs& a, hipStream_t st) {
+  const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
+  const unsigned blocks = (unsigned)(a.N / (16 * CT));
+  const size_t red = (size_t)S * CT * 256 * 4;
+  if (xbytes <= XLDS_MAX) {
+    const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED>), dim3(blocks), dim3(S * 64), lds, st, a);
+  } else {
+    hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED>), dim3(blocks), dim3(S * 64), red, st, a);
+  }
+}
+
 template <int PF, int S, int T, int PROBE = 0, bool TILED = false>
 void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
@@ -984,8 +1137,16 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       case 18: launch_gemv<3, 8, 1, 0, true>(a, st, true); break;
       case 19: launch_gemv<8, 8, 1, 0, true>(a, st, true); break;
       case 20: launch_gemv<2, 8, 2, 0, true>(a, st, true); break;
+      case 21: launch_gemv_ct<2, 8, 2, true>(a, st); break;
+      case 22: launch_gemv_ct<2, 8, 4, true>(a, st); break;
+      case 23: launch_gemv_ct<3, 8, 2, true>(a, st); break;
+      case 24: launch_gemv_ct<1, 8, 4, true>(a, st); break;
       case 100: launch_gemv<2, 8, 1, 1, true>(a, st, true); break;  // probe: no dequant
-      default: launch_gemv<2, 8, 1, 0, true>(a, st, true); break;
+      default:
+        if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
+        else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
+        else launch_gemv<2, 8, 1, 0, true>(a, st, true);
+        break;
     }
   } else if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     switch (variant) {
@@ -1010,11 +1171,19 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       // persistent variants (k_w4a16_gemv_p): measured 0-20 % SLOWER than the default on every Llama
       // decode shape (profiles/r01_gemv_persistent.jsonl) -- the per-group flush barriers stall the
       // code ring more than the second-round tail costs; kept for A/B
+      case 21: launch_gemv_ct<2, 8, 2, false>(a, st); break;
+      case 22: launch_gemv_ct<2, 8, 4, false>(a, st); break;
+      case 23: launch_gemv_ct<3, 8, 2, false>(a, st); break;
+      case 24: launch_gemv_ct<1, 8, 4, false>(a, st); break;
       case 14: launch_gemv_p<2, 8, 1>(a, st); break;
       case 15: launch_gemv_p<4, 8, 1>(a, st); break;
       case 16: launch_gemv_p<2, 4, 1>(a, st); break;
       case 17: launch_gemv_p<4, 4, 1>(a, st); break;
-      default: launch_gemv<2, 8, 1>(a, st, true); break;  // best or within 5 % of best, M in {1,4,16} (r01 sweep)
+      default:  // best or within 5 % of best, M in {1,4,16} (r01 sweep); column tiles for M >= 4
+        if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, false>(a, st);
+        else if (ct == 2) launch_gemv_ct<3, 8, 2, false>(a, st);
+        else launch_gemv<2, 8, 1>(a, st, true);
+        break;
     }
   } else if (N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              (a.gpr == 1 || a.group % 64 == 0)) {

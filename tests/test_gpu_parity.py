@@ -598,13 +598,29 @@ def test_gemv_tiled_layout_identical(K, group):
     # number (18-20 have the default's S = 8); out= writes in place
     x = (torch.randn(5, Kd, device=DEV) * 0.5).half()
     y = torch.empty(5, N, dtype=torch.float16, device=DEV)
-    for v in (1, 2, 4, 5, 7, 8, 9, 10, 12, 13, 18, 19, 20):
+    for v in (1, 2, 4, 5, 7, 8, 9, 10, 12, 13, 18, 19, 20, 21, 22, 23, 24):
         rv = v if v in (2, 4, 5, 7, 8, 9, 10, 12, 13) else (2 if v == 1 else 0)
         y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(rv))
         y1 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v),
                           tiled=True, out=y)
         assert y1.data_ptr() == y.data_ptr()
         assert torch.equal(y0.view(torch.int16), y.view(torch.int16)), v
+        if v >= 21:  # column-tile kernels on row-major codes: same bits too
+            y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+            assert torch.equal(y0.view(torch.int16), y2.view(torch.int16)), v
+    # a grid wide enough that the default takes the column-tile kernel (N/64 >= 256 -> 4 tiles per
+    # wave at M >= 4): same bits as the one-tile kernel with the same k-split (variant 18)
+    N2, K2 = 16384, 512
+    w2 = torch.empty(N2, K2, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w2, 56)
+    r2 = K.quantize_minmax(w2, 4, group, False, 0, want_codes=True)
+    t2 = K.tile_codes(r2.codes, N2, K2)
+    for m in (1, 4, 9, 16):
+        x = (torch.randn(m, K2, device=DEV) * 0.5).half()
+        ref = K.w4a16_gemm(x, r2.codes, r2.scales, r2.zeros, 4, group, N2, flags=K.gemm_variant_flags(18))
+        for codes, tl in ((r2.codes, False), (t2, True)):
+            y = K.w4a16_gemm(x, codes, r2.scales, r2.zeros, 4, group, N2, tiled=tl)
+            assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), (m, tl)
 
 
 def test_w4a16_gemm_identity_layout(K):
@@ -616,7 +632,7 @@ def test_w4a16_gemm_identity_layout(K):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
     for m in (1, 5, 16):  # decode kernels: rows of the identity pick weight columns exactly
-        for v in range(0, 18):
+        for v in list(range(0, 18)) + [21, 22, 23, 24]:
             y = K.w4a16_gemm(x[:m].contiguous(), r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
             assert torch.equal(y, r.out.t()[:m].contiguous()), (m, v)
 
