@@ -594,7 +594,7 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
   constexpr int NC = TX * 8;  // columns per block
   __shared__ int32_t s_mn[TY][NC];
   __shared__ int32_t s_mx[TY][NC];
-  __shared__ int32_t f_mn[NC], f_mx[NC];
+  __shared__ GroupParams f_p[NC];
   const int tx = threadIdx.x % TX;
   const int ty = threadIdx.x / TX;
   const int64_t c0 = ((int64_t)blockIdx.x * TX + tx) * 8;
@@ -656,29 +656,27 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) { s_mn[ty][tx * 8 + i] = mn[i]; s_mx[ty][tx * 8 + i] = mx[i]; }
   __syncthreads();
+  // one thread per column folds the TY partials AND derives the group's parameters once (not once
+  // per row slice: 8x less parameter math at TY = 8), shared through LDS
   if (threadIdx.x < NC) {
     int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
 #pragma unroll 8
     for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][threadIdx.x]); a_mx = max(a_mx, s_mx[y][threadIdx.x]); }
-    f_mn[threadIdx.x] = a_mn;
-    f_mx[threadIdx.x] = a_mx;
+    const GroupParams q = params_from_keys<DT, SYM>(a_mn, a_mx, a.n_bits, rmax_for(a.n_bits, SYM));
+    f_p[threadIdx.x] = q;
+    const int64_t col = (int64_t)blockIdx.x * NC + threadIdx.x;
+    if (col < a.cols) {
+      const int64_t gidx = col * (a.rows / a.g) + jr;
+      if (a.scales) store_param<DT>(a.scales, gidx, q.s);
+      if (!SYM && a.zeros) store_param<DT>(a.zeros, gidx, q.z);
+    }
   }
   __syncthreads();
-  const float rmax = rmax_for(a.n_bits, SYM);
   GroupParams p[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) p[i] = params_from_keys<DT, SYM>(f_mn[tx * 8 + i], f_mx[tx * 8 + i], a.n_bits, rmax);
+  for (int i = 0; i < 8; ++i) p[i] = f_p[tx * 8 + i];
   bool any_nan = false;
   if (cvalid) {
-    if (ty == 0) {
-      const int64_t ng = a.rows / a.g;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int64_t gidx = (c0 + i) * ng + jr;
-        if (a.scales) store_param<DT>(a.scales, gidx, p[i].s);
-        if (!SYM && a.zeros) store_param<DT>(a.zeros, gidx, p[i].z);
-      }
-    }
     const uint32_t off = SYM ? (1u << (a.n_bits - 1)) : 0u;
     if constexpr (DT == DT_F16) {
       // all 8 columns of this thread on the fast path: packed pairs with per-half group operands

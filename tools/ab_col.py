@@ -29,6 +29,12 @@ def main():
     n = a.rows * a.cols
     algo = 4 * n + 4 * (n // a.group)
     ref = K.quantize_minmax(ws[0], 4, a.group, False, 1).out
+    import time
+    t_end = time.time() + 1.0  # clock ramp: ~1 s of untimed launches before the first timing
+    while time.time() < t_end:
+        for w, o in zip(ws, outs):
+            K.quantize_minmax(w, 4, a.group, False, 1, out=o)
+    torch.cuda.synchronize()
     for v in (0, 1, 2, 3):
         flags = K.gemm_variant_flags(v)
         r = K.quantize_minmax(ws[0], 4, a.group, False, 1, flags=flags).out
