@@ -85,7 +85,7 @@ __host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
 // reference's int8 mantissa arithmetic.  A code equal to 0 (|t| == 0, or a positive t whose
 // magnitude code is 0) decodes to 0 outright (the reference's zero mask); a sign-only code does NOT:
 // its int8 mantissa arithmetic can still give -1 after a rounding shift by 8 (ATen's int8 >> 8 == -1).
-constexpr int APXD_T2 = 128 * 16;  // entries of table 2
+constexpr int APXD_T2 = 16 * 256;  // entries of table 2: index (tgt << 8) | magnitude code
 
 __device__ __forceinline__ void apxd_fields(uint32_t c, const FpSpec& f, int& ae, int& mpad) {
   const int ef = w8((int)((c >> f.M) & ((1u << f.E) - 1u)));
@@ -113,6 +113,29 @@ __device__ __forceinline__ int apxd_tgt(uint32_t b0, uint32_t b1, uint32_t b2, u
   int tgt = cnt <= 1 ? w8(f.hf) : gmax;
   if (has_max) tgt = w8((1 << f.E) - 1);
   return tgt;
+}
+
+// apxd_tgt on 4 elements at once: bytes of x / a / b / c are the info bytes of the quad members
+// (own, partner 1, 2, 3) of 4 elements; returns their 4 target exponents, one per byte.
+__device__ __forceinline__ uint32_t apxd_tgt4(uint32_t x, uint32_t a, uint32_t b, uint32_t c, const FpSpec& f) {
+  // outlier count << 5 per byte (<= 0x80: no carry between bytes); > 1 <=> bit 6 or bit 7
+  const uint32_t cnt5 = ((x >> 1) & 0x20202020u) + ((a >> 1) & 0x20202020u) + ((b >> 1) & 0x20202020u) +
+                        ((c >> 1) & 0x20202020u);
+  const uint32_t gt1 = (cnt5 | (cnt5 << 1)) & 0x80808080u;
+  const uint32_t hm = (x | a | b | c) & 0x80808080u;            // a member is an outlier at the max exponent
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  auto mx16 = [](uint32_t p, uint32_t q) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, q)));
+  };
+  const uint32_t ev = mx16(mx16(x & 0x000F000Fu, a & 0x000F000Fu), mx16(b & 0x000F000Fu, c & 0x000F000Fu));
+  const uint32_t od = mx16(mx16(x & 0x0F000F00u, a & 0x0F000F00u), mx16(b & 0x0F000F00u, c & 0x0F000F00u));
+  const uint32_t gmax = ev | od;                                // max ae of the quad, per byte
+  const uint32_t mg = (gt1 - (gt1 >> 7)) | gt1;                 // 0xFF where count > 1
+  const uint32_t mh = (hm - (hm >> 7)) | hm;                    // 0xFF where has_max
+  const uint32_t hfw = 0x01010101u * ((uint32_t)w8(f.hf) & 0xFFu);
+  const uint32_t maxw = 0x01010101u * ((uint32_t)w8((1 << f.E) - 1) & 0xFFu);
+  const uint32_t t = (gmax & mg) | (hfw & ~mg);
+  return (maxw & mh) | (t & ~mh);
 }
 
 // decoded value (before the code's sign) of magnitude code c at target exponent tgt (table 2)
@@ -157,10 +180,11 @@ __global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut,
     if constexpr (CODEC == CODEC_APXD) lut[i] = (uint16_t)apxd_info(i < n ? fp_encode((uint32_t)i, f, tabs) : 0u, f);
     else lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
   }
-  if constexpr (CODEC == CODEC_APXD) {  // table 2: (magnitude code, tgt) -> value, after table 1
+  if constexpr (CODEC == CODEC_APXD) {  // table 2: (tgt, magnitude code) -> value, after table 1;
+                                        // codes >= 2^(E+M) (incl. the zero-code column 0x80) -> +0
     for (int32_t i = blockIdx.x * BLOCK + threadIdx.x; i < APXD_T2; i += gridDim.x * BLOCK) {
-      const uint32_t c = (uint32_t)i >> 4;
-      const float v = c < (1u << (f.E + f.M)) ? apxd_value(c, i & 15, f) : 0.0f;
+      const uint32_t c = (uint32_t)i & 0xFFu;
+      const float v = c < (1u << (f.E + f.M)) ? apxd_value(c, i >> 8, f) : 0.0f;
       lut[n8 + i] = (uint16_t)Fmt<DT_F16>::from_f(v);
     }
   }
@@ -510,32 +534,47 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
       const int64_t e = (u0 + k) * UNIT + (int64_t)lane * 8;
       v[k].load(a.w + ((k < nu && e < a.numel) ? e : 0) * F::BYTES);
     }
+    int32_t mn[UNROLL], mx[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      minmax8<DT_F16, true>(v[k], mn[k], mx[k]);
+      group_max<LPG>(mx[k]);
+    }
+    // shared group parameters (as k_fp_group_lut): lane l derives unit (l % 4) of its own group, the
+    // quad's lanes (same group, g >= 32) broadcast them by DPP when every unit's group is finite
+    const int kk = lane & (UNROLL - 1);
+    int32_t smn = mn[0], smx = mx[0];
+#pragma unroll
+    for (int k = 1; k < UNROLL; ++k) {
+      if (kk == k) { smn = mn[k]; smx = mx[k]; }
+    }
+    const FpParams ps = fp_group_params<CODEC_APX, true>(smn, smx, f);
+    const bool shared_ok = __ballot(kk < nu && !ps.fast) == 0;
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       if (k < nu) {  // wave-uniform
         const int64_t e0 = (u0 + k) * UNIT + (int64_t)lane * 8;
-        int32_t mn, mx;
-        minmax8<DT_F16, true>(v[k], mn, mx);
-        group_max<LPG>(mx);
-        const FpParams p = fp_group_params<CODEC_APX, true>(mn, mx, f);
-        uint32_t info[8], sgz[8];  // sgz: bit 0 = code sign, bit 1 = code == 0
+        const FpParams p = shared_ok ? bcast_fp_params(ps, k) : fp_group_params<CODEC_APX, true>(mn[k], mx[k], f);
+        // t = clamp(RN16(w / s)); info words (table 1 on finite groups, the exact chain + ALU codec
+        // otherwise); the quad exchange runs OUTSIDE the branch: partners may take the other path
+        uint32_t info[8], sgn[4];  // sgn: finite groups: code-sign bits per pair; else bit 2i+1 = sign,
+                                   // bit 2i = zero code of element i
         if (p.fast) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const f2 df = __builtin_convertvector(as_h2(v[k].u[j]), f2);
             h2 t = __builtin_convertvector(pk_div_f16vals(df, p.rs, p.s), h2);
             t = pk_max(pk_min(t, bound2), -bound2);
-            const uint32_t tb = as_u32(t);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const uint32_t th = (tb >> (16 * h)) & 0xFFFFu, u = th & 0x7FFFu;
-              const uint32_t inf_ = lut[u];
-              const uint32_t sg = (th >> 15) & (u != 0u ? 1u : 0u);  // fp_encode: |t| == 0 -> code 0
-              info[2 * j + h] = inf_;
-              sgz[2 * j + h] = sg | ((((inf_ >> 12) & 1u) && !sg) ? 2u : 0u);
-            }
+            const uint32_t tb = as_u32(t), mag = tb & 0x7FFF7FFFu;
+            sgn[j] = tb & (mag + 0x7FFF7FFFu) & 0x80008000u;  // fp_encode: |t| == 0 -> code 0
+            // zero code (magnitude 0, no sign: the reference masks it to 0) -> magnitude byte | 0x80,
+            // a table-2 column of zeros (entry (tgt, 0) is not 0 for every tgt: int8 shift wrap)
+            const uint32_t i0 = lut[mag & 0xFFFFu], i1 = lut[mag >> 16];
+            info[2 * j] = i0 | ((i0 >> 5) & ~(sgn[j] >> 8) & 0x80u);
+            info[2 * j + 1] = i1 | ((i1 >> 5) & ~(sgn[j] >> 24) & 0x80u);
           }
-        } else {  // non-finite group: the exact chain (fp_apx_elem's t), ALU codec
+        } else {
+          sgn[0] = 0;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             float t = div16(F::to_f(v[k].get(i)), p.s, p.rs, false);
@@ -543,32 +582,43 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             const uint32_t tb = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)t);
             const uint32_t code = fp_encode(tb, f, tabs);
             info[i] = apxd_info(code, f);
-            sgz[i] = ((code >> (f.E + f.M)) & 1u) | (code == 0u ? 2u : 0u);
+            sgn[0] |= (((code >> (f.E + f.M)) & 1u) << (2 * i + 1)) | ((code == 0u ? 1u : 0u) << (2 * i));
           }
         }
-        uint32_t x0 = 0, x1 = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          x0 |= ((info[i] >> 8) & 0xFFu) << (8 * i);
-          x1 |= ((info[4 + i] >> 8) & 0xFFu) << (8 * i);
-        }
+        // info byte 1 (ae | zero << 4 | outlier << 6 | outlier-at-max << 7) of 4 elements per word
+        const uint32_t x0 = __builtin_amdgcn_perm(info[1], info[0], 0x0C0C0501u) |
+                            __builtin_amdgcn_perm(info[3], info[2], 0x05010C0Cu);
+        const uint32_t x1 = __builtin_amdgcn_perm(info[5], info[4], 0x0C0C0501u) |
+                            __builtin_amdgcn_perm(info[7], info[6], 0x05010C0Cu);
         const uint32_t a0 = (uint32_t)__shfl_xor((int)x0, LPG), a1 = (uint32_t)__shfl_xor((int)x1, LPG);
         const uint32_t b0 = (uint32_t)__shfl_xor((int)x0, 2 * LPG), b1 = (uint32_t)__shfl_xor((int)x1, 2 * LPG);
         const uint32_t c0 = (uint32_t)__shfl_xor((int)a0, 2 * LPG), c1 = (uint32_t)__shfl_xor((int)a1, 2 * LPG);
+        const uint32_t tw0 = apxd_tgt4(x0, a0, b0, c0, f), tw1 = apxd_tgt4(x1, a1, b1, c1, f);
         Vec8<DT_F16> o;
         bool nan8 = false;
+        if (p.fast) {
+          const h2 s2 = {(_Float16)p.s, (_Float16)p.s};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int sh8 = 8 * (i & 3);
-          const uint32_t q0 = ((i < 4 ? x0 : x1) >> sh8) & 0xFFu, q1 = ((i < 4 ? a0 : a1) >> sh8) & 0xFFu;
-          const uint32_t q2 = ((i < 4 ? b0 : b1) >> sh8) & 0xFFu, q3 = ((i < 4 ? c0 : c1) >> sh8) & 0xFFu;
-          const int tgt = apxd_tgt(q0, q1, q2, q3, f);  // in [0, 15] (launcher: 0 <= hf <= 15)
-          float dv = (float)t2[((info[i] & 0x7Fu) << 4) | (uint32_t)tgt];
-          if (sgz[i] & 1u) dv = -dv;
-          if (sgz[i] & 2u) dv = 0.0f;                          // zero code
-          const float y = (float)(_Float16)opaque(dv * p.s);  // RN16(decoded * scales)
-          nan8 |= (y != y);
-          o.set(i, F::from_f(y));
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t tw = j < 2 ? tw0 : tw1;
+            // table-2 index (tgt << 8) | c: byte 0 = c (| 0x80: zero code), byte 1 = this element's tgt
+            const uint32_t i0 = __builtin_amdgcn_perm(tw, info[2 * j], 0x0C0C0400u + ((uint32_t)(2 * (j & 1)) << 8));
+            const uint32_t i1 = __builtin_amdgcn_perm(tw, info[2 * j + 1], 0x0C0C0400u + ((uint32_t)(2 * (j & 1) + 1) << 8));
+            const uint32_t vv = ((uint32_t)__builtin_bit_cast(uint16_t, t2[i0]) |
+                                 ((uint32_t)__builtin_bit_cast(uint16_t, t2[i1]) << 16)) ^ sgn[j];
+            o.u[j] = as_u32(as_h2(vv) * s2);  // RN16(decoded * scales): exact product, one rounding
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const uint32_t tgt = ((i < 4 ? tw0 : tw1) >> (8 * (i & 3))) & 0xFFu;  // in [0, 15]
+            float dv = (float)t2[(tgt << 8) | (info[i] & 0x7Fu)];
+            if ((sgn[0] >> (2 * i + 1)) & 1u) dv = -dv;
+            if ((sgn[0] >> (2 * i)) & 1u) dv = 0.0f;             // zero code
+            const float y = (float)(_Float16)opaque(dv * p.s);  // RN16(decoded * scales)
+            nan8 |= (y != y);
+            o.set(i, F::from_f(y));
+          }
         }
         if (e0 < a.numel) {
           any_nan |= nan8;
