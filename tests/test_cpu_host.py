@@ -68,6 +68,24 @@ def test_host_validation_without_gpu(lib):
     assert call(dummy, 8, 128, 128, 0, 9, 128, 0, 0, None, 128, dummy, None, None, None, 0, None, 0, None) == 7
 
 
+def test_decode_entries_host_validation(lib):
+    """iwq_tile_codes / iwq_w4a16_gemm / iwq_dequant_packed reject bad geometry on the host (no launch)."""
+    from iron_weight_only_quant_amd import _lib as L
+    vp = ctypes.c_void_p
+    d = vp(4096)
+    assert lib.iwq_tile_codes(None, 16, 128, d, None) == 9          # IWQ_ERR_ARG
+    assert lib.iwq_tile_codes(d, 15, 128, d, None) == 1             # N % 16 (IWQ_ERR_SHAPE)
+    assert lib.iwq_tile_codes(d, 16, 100, d, None) == 1             # K % 128
+    assert lib.iwq_tile_codes(vp(4104), 16, 128, d, None) == 9      # 16-B alignment
+    gemm = lib.iwq_w4a16_gemm
+    # tile layout is a decode-only (M <= 16) format
+    assert gemm(d, 17, 256, 256, d, d, d, 4, 128, 128, None, d, 128, L.IWQ_FLAG_TILED_CODES, None) == 9
+    assert gemm(d, 1, 256, 256, d, d, d, 4, 128, 100, None, d, 100, 0, None) == 1      # N % 128
+    assert gemm(d, 1, 256, 256, d, d, d, 4, 96, 128, None, d, 128, 0, None) == 2       # K % group
+    assert gemm(d, 1, 256, 256, d, d, d, 5, 128, 128, None, d, 128, 0, None) == 4     # n_bits
+    assert lib.iwq_dequant_packed(d, d, d, 4, 128, 128, 100, d, 100, None) != 0
+
+
 def test_batch_plan_host(lib):
     from iron_weight_only_quant_amd._lib import IwqBatchEntry
     t = (IwqBatchEntry * 3)()
