@@ -608,6 +608,13 @@ def test_gemv_tiled_layout_identical(K, group):
         if v >= 21:  # column-tile kernels on row-major codes: same bits too
             y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
             assert torch.equal(y0.view(torch.int16), y2.view(torch.int16)), v
+            # M = 16: X (139 KB) exceeds the LDS image budget -> the register-X form of both kernels
+            x16 = (torch.randn(16, Kd, device=DEV) * 0.5).half()
+            z0 = K.w4a16_gemm(x16, r.codes, r.scales, r.zeros, 4, group, N, b)
+            for codes, tl in ((r.codes, False), (tiled, True)):
+                z1 = K.w4a16_gemm(x16, codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v),
+                                  tiled=tl)
+                assert torch.equal(z0.view(torch.int16), z1.view(torch.int16)), (v, tl)
     # a grid wide enough that the default takes the column-tile kernel (N/64 >= 256 -> 4 tiles per
     # wave at M >= 4): same bits as the one-tile kernel with the same k-split (variant 18)
     N2, K2 = 16384, 512
