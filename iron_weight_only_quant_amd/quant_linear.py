@@ -266,9 +266,10 @@ class QuantLinear(nn.Module):
                 fp6_tail_pad_bits=fp6_tail_pad_bits, fp4_hi_align_start=fp4_hi_align_start,
                 fp4_hi_align_exp_field=fp4_hi_align_exp_field, fp4_tail_pad_bits=fp4_tail_pad_bits,
                 keep_codes=keep_codes, fused_forward=fused_forward, _init_weight=False)
-        q.weight = nn.Parameter(linear_layer.weight.data.detach(), requires_grad=False)
+        # aliases the original storage (quant_linear.py:1021-1024); straight into _parameters
+        q._parameters["weight"] = nn.Parameter(linear_layer.weight.data.detach(), requires_grad=False)
         if linear_layer.bias is not None:
-            q.bias = nn.Parameter(linear_layer.bias.data.detach(), requires_grad=False)
+            q._parameters["bias"] = nn.Parameter(linear_layer.bias.data.detach(), requires_grad=False)
         if quantize:
             q.quantize_weight()
         return q

@@ -25,7 +25,10 @@ def _set_module(model, name, new):
     path = name.split(".")
     for p in path[:-1]:
         parent = getattr(parent, p)
-    setattr(parent, path[-1], new)
+    if path[-1] in parent._modules:  # replacing a registered child: skip nn.Module.__setattr__'s checks
+        parent._modules[path[-1]] = new
+    else:
+        setattr(parent, path[-1], new)
 
 
 def _qkw(args, w_format):
@@ -79,8 +82,8 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
             plan.run()
             for i, (n, m) in enumerate(items):
                 q = QuantLinear.from_linear(m, quantize=False, **kw)
-                q.scales = plan.scales[i].view(-1, 1)
-                q.zeros = plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None
+                q._buffers.update(scales=plan.scales[i].view(-1, 1),
+                                  zeros=plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None)
                 q.quantized.fill_(True)
                 _set_module(model, n, q)
                 done.add(n)
@@ -124,13 +127,11 @@ def _batched_fp(model, layers, kw, fmt, done):
         plan.run()
         for i, (n, mod) in enumerate(items):
             q = QuantLinear.from_linear(mod, quantize=False, **kw)
-            q.scales = plan.scales[i].view(-1, 1)
-            q.zeros = plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None
-            for other in ("fp4", "fp6", "fp8"):
-                if other != fmt:
-                    setattr(q, f"weight_{other}", None)
+            # weight_fp4/6/8 stay None (set so by __init__, as the FP branches leave them)
+            q._buffers.update(scales=plan.scales[i].view(-1, 1),
+                              zeros=plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None)
             q.quantized.fill_(True)
             if apx:
-                q.approximate = True
+                q.__dict__["approximate"] = True
             _set_module(model, n, q)
             done.add(n)

@@ -5,6 +5,7 @@ host work included (module swap, buffers), batched (one launch per format) vs pe
 Prints one JSON line per (format, mode): wall ms from the call to a device sync, and the kernel-only
 share measured separately (bench_model_formats.py)."""
 import argparse
+import gc
 import json
 import os
 import sys
@@ -44,18 +45,22 @@ def main():
     from iron_weight_only_quant_amd.quant_wrapper import quantize_model
     for fmt in a.formats.split(","):
         for batched in (True, False):
-            m = build(a.model)
-            args = SimpleNamespace(w_bit=4 if fmt == "int" else 8, a_bit=16, w_group_size=128, w_symmetric=False,
-                                   w_format=fmt, quant_dim=0)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            quantize_model(m, args, batched=batched, verbose=False)
-            torch.cuda.synchronize()
-            ms = (time.perf_counter() - t0) * 1e3
-            print(json.dumps({"model": a.model, "format": fmt, "batched": batched, "wall_ms": round(ms, 2)}),
-                  flush=True)
-            del m
-            torch.cuda.empty_cache()
+            for rep in range(2):  # rep 0 includes the first launch of each kernel (code-object load)
+                m = build(a.model)
+                args = SimpleNamespace(w_bit=4 if fmt == "int" else 8, a_bit=16, w_group_size=128,
+                                       w_symmetric=False, w_format=fmt, quant_dim=0)
+                torch.cuda.synchronize()
+                gc.collect()  # no collector pause left over from the previous model inside the timing
+                t0 = time.perf_counter()
+                quantize_model(m, args, batched=batched, verbose=False)
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                print(json.dumps({"model": a.model, "format": fmt, "batched": batched, "rep": rep,
+                                  "host_ms": round((t1 - t0) * 1e3, 2), "wall_ms": round((t2 - t0) * 1e3, 2)}),
+                      flush=True)
+                del m
+                torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
