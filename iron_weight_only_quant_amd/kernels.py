@@ -405,9 +405,9 @@ class BatchPlan:
         self.n_bits, self.group, self.symmetric = int(n_bits), int(group), bool(symmetric)
         self.weights = weights
         self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
-        self.scales = [torch.empty(w.numel() // group, dtype=dt, device=dev) if want_scales else None for w in weights]
-        self.zeros = [torch.empty(w.numel() // group, dtype=dt, device=dev) if (want_scales and not symmetric) else None
-                      for w in weights]
+        self.scales = _param_views(weights, group, dt, dev) if want_scales else [None] * len(weights)
+        self.zeros = (_param_views(weights, group, dt, dev) if (want_scales and not symmetric)
+                      else [None] * len(weights))
         self.codes = [torch.empty(codes_nbytes(w.shape[0], w.shape[1], n_bits), dtype=torch.uint8, device=dev)
                       if want_codes else None for w in weights]
         self.want_codes = want_codes
@@ -463,6 +463,13 @@ def selftest_division(device="cuda"):
     return tuple(int(x) for x in counts.cpu())
 
 
+def _param_views(weights, group, dtype, dev):
+    """Per-tensor [G] parameter vectors as views of ONE allocation (one caching-allocator call
+    instead of one per layer: 224 / 560 for a 7B / 70B model); each view is contiguous."""
+    sizes = [w.numel() // group for w in weights]
+    return list(torch.empty(sum(sizes), dtype=dtype, device=dev).split(sizes))
+
+
 class FpBatchPlan:
     """Whole-model FP fake quantization in ONE launch (quantize_model's loop for weight_format
     fp4/fp6/fp8, approximate single-aligned decode, or the E2M1 grid): fp16 contiguous weights,
@@ -492,9 +499,9 @@ class FpBatchPlan:
             raise RuntimeError("decode table unavailable for this format (or building it inside a graph capture)")
         self.weights = weights
         self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
-        self.scales = [torch.empty(w.numel() // group, dtype=torch.float16, device=dev) for w in weights]
-        self.zeros = [torch.empty(w.numel() // group, dtype=torch.float16, device=dev) if not self.symmetric else None
-                      for w in weights]
+        self.scales = _param_views(weights, group, torch.float16, dev)
+        self.zeros = (_param_views(weights, group, torch.float16, dev) if not self.symmetric
+                      else [None] * len(weights))
         n = len(weights)
         table = (L.IwqBatchEntry * n)()
         for i, w in enumerate(weights):
