@@ -271,6 +271,21 @@ def test_quantize_model_drop_in(K):
         x = torch.randn(2, 5, 256, dtype=torch.float16, device=DEV)
         y = m.l0(x)
         torch.testing.assert_close(y, torch.nn.functional.linear(x, m.l0.weight, m.l0.bias))
+        # state_dict round trip (batched scales/zeros are views of one allocation): same keys as the
+        # reference's buffers, independent saved copies, loadable into a fresh quantized module
+        sd = m.state_dict()
+        for n in ("l0", "l1"):
+            assert {f"{n}.scales", f"{n}.zeros", f"{n}.quantized"} <= set(sd), n
+            assert sd[f"{n}.scales"].shape == (specs[n][0] * specs[n][1] // 128, 1)
+        import io
+        buf = io.BytesIO()
+        torch.save(sd, buf)
+        buf.seek(0)
+        sd2 = torch.load(buf, weights_only=True)
+        q2 = QuantLinear.from_linear(torch.nn.Linear(384, 256, bias=False).half().to(DEV), w_bit=4,
+                                     w_group_size=128, symmetric=False)
+        q2.load_state_dict({k[3:]: v for k, v in sd2.items() if k.startswith("l1.")})
+        assert torch.equal(q2.scales, m.l1.scales) and torch.equal(q2.weight, m.l1.weight)
 
 
 @pytest.mark.parametrize("fmt,sym,apx", [("fp8", False, False), ("fp8", True, False), ("fp6", False, False),
