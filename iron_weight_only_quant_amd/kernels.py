@@ -116,13 +116,20 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
             raise ValueError("packed codes need n_bits <= 8")
         codes = torch.empty(codes_nbytes(rows, cols, n_bits), dtype=torch.uint8, device=dev)
     nan_flag = _flags.take(dev)
-    wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
-    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev) if wsb > 0 else None
-    with torch.cuda.device(dev):
-        st = lib.iwq_quantize_minmax(
-            L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group), int(bool(symmetric)),
-            int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols), L.ptr(codes), L.ptr(scales),
-            L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev))
+
+    def call(ws, wsb):
+        with torch.cuda.device(dev):
+            return lib.iwq_quantize_minmax(
+                L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group),
+                int(bool(symmetric)), int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols),
+                L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags),
+                L.stream_handle(dev))
+    # the specialised kernels need no workspace; the C-ABI checks for one before launching anything,
+    # so only the per-tensor and universal paths pay for the allocation (and a second call)
+    st = call(None, 0)
+    if st == L.IWQ_ERR_WORKSPACE:
+        wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
+        st = call(torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev), wsb)
     _raise_for(st, "iwq_quantize_minmax")
     return QuantResult(out, scales, zeros, codes, nan_flag)
 

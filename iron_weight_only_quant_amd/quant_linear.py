@@ -131,17 +131,16 @@ class QuantLinear(nn.Module):
                                           want_codes=self.keep_codes and self.w_bit <= 8)
             if res.out is not w:
                 w.copy_(res.out)
-            self.scales = res.scales.view(-1, 1)
-            self.zeros = res.zeros.view(-1, 1) if res.zeros is not None else None
-            self.qweight = res.codes
-            self.qweight_tiled = None
+            tiled = None
             if (self.fused_forward == "auto" and res.codes is not None and self.quant_dim == 0
                     and self.w_bit <= 4 and w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0):
                 # decode batches read the codes in the GEMV tile layout (1 KiB contiguous per load)
-                self.qweight_tiled = kernels.tile_codes(res.codes, w.shape[0], w.shape[1])
-            self.weight_fp4 = None
-            self.weight_fp6 = None
-            self.weight_fp8 = None
+                tiled = kernels.tile_codes(res.codes, w.shape[0], w.shape[1])
+            # registered buffers (see __init__), written without nn.Module.__setattr__'s per-name checks
+            self._buffers.update(scales=res.scales.view(-1, 1),
+                                 zeros=res.zeros.view(-1, 1) if res.zeros is not None else None,
+                                 qweight=res.codes, qweight_tiled=tiled,
+                                 weight_fp4=None, weight_fp6=None, weight_fp8=None)
             self.quantized.fill_(True)
 
     def quantize_weight_approximate(self):
