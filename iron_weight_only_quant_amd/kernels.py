@@ -192,14 +192,19 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     codes = torch.empty(fp_code_nbytes(rows, cols, exp_bits, mant_bits), dtype=torch.uint8, device=dev) \
         if want_codes else None
     nan_flag = _flags.take(dev)
-    wsb = ((8 * G + 255) // 256) * 256
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     lut = _luts.get(dev, L.IWQ_CODEC_FP, exp_bits, mant_bits) if use_lut else None
-    with torch.cuda.device(dev):
-        st = lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits), int(mant_bits),
-                                     int(group), int(bool(symmetric)), int(quant_dim), L.ptr(out), out.stride(0),
-                                     L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag),
-                                     int(flags), L.stream_handle(dev), L.ptr(lut))
+
+    def call(ws, wsb):
+        with torch.cuda.device(dev):
+            return lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
+                                           int(mant_bits), int(group), int(bool(symmetric)), int(quant_dim),
+                                           L.ptr(out), out.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
+                                           L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev),
+                                           L.ptr(lut))
+    st = call(None, 0)  # the specialised kernel needs no workspace (checked before any launch)
+    if st == L.IWQ_ERR_WORKSPACE:
+        wsb = ((8 * G + 255) // 256) * 256
+        st = call(torch.empty(wsb, dtype=torch.uint8, device=dev), wsb)
     _raise_for(st, "iwq_quantize_fp")
     return QuantResult(out, scales, zeros, codes, nan_flag)
 

@@ -203,12 +203,10 @@ class QuantLinear(nn.Module):
                                   want_codes=self.keep_codes)
         if res.out is not w:
             w.copy_(res.out)
-        self.scales = res.scales.view(-1, 1)
-        self.zeros = res.zeros.view(-1, 1) if res.zeros is not None else None
-        self.qweight = res.codes
-        for other in ("fp4", "fp6", "fp8"):
-            if other != self.weight_format:
-                setattr(self, f"weight_{other}", None)
+        upd = dict(scales=res.scales.view(-1, 1), zeros=res.zeros.view(-1, 1) if res.zeros is not None else None,
+                   qweight=res.codes)
+        upd.update({f"weight_{o}": None for o in ("fp4", "fp6", "fp8") if o != self.weight_format})
+        self._buffers.update(upd)  # registered buffers (see __init__)
         self.quantized.fill_(True)
 
     def forward(self, input):
