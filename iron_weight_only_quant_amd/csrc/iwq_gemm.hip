@@ -562,10 +562,20 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
 // only matters from M = 4 on, and a CT-fold smaller grid must still cover the chip: CT = 4 when that
 // leaves >= 256 workgroups (or >= 160 at M >= 8: 7B gate/up), CT = 2 for >= 256 workgroups once M*K
 // is large (70B down, K = 28672); else the one-tile kernel.  70B gate M = 16: 58.5 -> 30.7 us.
+// Long reductions at M < 4 (7B down K = 11008, 70B down K = 28672): a 16-way k-split (S = 16) keeps
+// twice the waves streaming (cold: 9.4 -> 7.5 us, 26.6 -> 24.2 us); at K <= 8192 the extra partial
+// sums cost more than they hide (q/gate/70B gate 4-8 % slower).  Different k-split = different fp32
+// summation order than S = 8 (deterministic either way).
+inline bool gemv_long_k(int64_t M, int64_t K) { return M < 4 && K >= 10240; }
+
+// M = 3 counts as well (70B gate: staging 49 KB of X per 16-column workgroup, 29.1 us vs 26.8 at
+// M = 4 with 4 tiles), and M = 2 once X no longer fits the LDS image (70B down, K = 28672: 34.8 ->
+// 28.3 us).
 inline int gemv_auto_ct(int64_t M, int64_t N, int64_t K) {
-  if (M < 4) return 1;
+  const bool xlds = M * (2 * K + 16) <= XLDS_MAX;
+  if (M < 3 && xlds) return 1;
   if (N / 64 >= 256 || (M >= 8 && N / 64 >= 160)) return 4;
-  if (N / 32 >= 256 && M * K >= 65536) return 2;
+  if (N / 32 >= 256 && (M * K >= 65536 || !xlds)) return 2;
   return 1;
 }
 
@@ -1145,6 +1155,7 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
+        else if (gemv_long_k(M, K)) launch_gemv<2, 16, 1, 0, true>(a, st, true);
         else launch_gemv<2, 8, 1, 0, true>(a, st, true);
         break;
     }
@@ -1182,6 +1193,7 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       default:  // best or within 5 % of best, M in {1,4,16} (r01 sweep); column tiles for M >= 4
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, false>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, false>(a, st);
+        else if (gemv_long_k(M, K)) launch_gemv<2, 16, 1>(a, st, true);
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }

@@ -637,6 +637,33 @@ def test_gemv_tiled_layout_identical(K, group):
     K.fill_synthetic(w2, 56)
     r2 = K.quantize_minmax(w2, 4, group, False, 0, want_codes=True)
     t2 = K.tile_codes(r2.codes, N2, K2)
+    # long K at M < 4: the default takes the 16-way k-split (variant 13's kernel)
+    N3, K3 = 256, 10240
+    w3 = torch.empty(N3, K3, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w3, 57)
+    r3 = K.quantize_minmax(w3, 4, group, False, 0, want_codes=True)
+    t3 = K.tile_codes(r3.codes, N3, K3)
+    for m in (1, 3):
+        x = (torch.randn(m, K3, device=DEV) * 0.5).half()
+        for codes, tl in ((r3.codes, False), (t3, True)):
+            ref = K.w4a16_gemm(x, codes, r3.scales, r3.zeros, 4, group, N3, flags=K.gemm_variant_flags(13), tiled=tl)
+            y = K.w4a16_gemm(x, codes, r3.scales, r3.zeros, 4, group, N3, tiled=tl)
+            assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), (m, tl)
+            want = x.float() @ r3.out.float().t()
+            torch.testing.assert_close(y.float(), want, rtol=2e-2, atol=2e-2)
+    # M = 2 with X over the LDS budget (K = 16384): two column tiles per wave, same bits as variant 18
+    N4, K4 = 8192, 16384
+    w4 = torch.empty(N4, K4, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w4, 58)
+    r4 = K.quantize_minmax(w4, 4, group, False, 0, want_codes=True)
+    del w4
+    t4 = K.tile_codes(r4.codes, N4, K4)
+    x = (torch.randn(2, K4, device=DEV) * 0.5).half()
+    for codes, tl in ((r4.codes, False), (t4, True)):
+        ref = K.w4a16_gemm(x, codes, r4.scales, r4.zeros, 4, group, N4, flags=K.gemm_variant_flags(18), tiled=tl)
+        y = K.w4a16_gemm(x, codes, r4.scales, r4.zeros, 4, group, N4, tiled=tl)
+        assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), tl
+    del r4, t4
     for m in (1, 4, 9, 16):
         x = (torch.randn(m, K2, device=DEV) * 0.5).half()
         ref = K.w4a16_gemm(x, r2.codes, r2.scales, r2.zeros, 4, group, N2, flags=K.gemm_variant_flags(18))
