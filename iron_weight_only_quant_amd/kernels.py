@@ -118,7 +118,7 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
     nan_flag = _flags.take(dev)
 
     def call(ws, wsb):
-        with torch.cuda.device(dev):
+        with L.on_device(dev):
             return lib.iwq_quantize_minmax(
                 L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group),
                 int(bool(symmetric)), int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols),
@@ -152,7 +152,7 @@ class _LutCache:
         if torch.cuda.is_current_stream_capturing():
             return None
         t = torch.empty(L.IWQ_FP_LUT_BYTES, dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with L.on_device(dev):
             st = L.load().iwq_fp_build_lut(int(codec), int(exp_bits), int(mant_bits), int(hs), int(hf), int(tp),
                                            L.ptr(t), t.numel(), L.stream_handle(dev))
         if st != L.IWQ_OK:  # a format the table path does not cover: plain codec
@@ -195,7 +195,7 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     lut = _luts.get(dev, L.IWQ_CODEC_FP, exp_bits, mant_bits) if use_lut else None
 
     def call(ws, wsb):
-        with torch.cuda.device(dev):
+        with L.on_device(dev):
             return lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
                                            int(mant_bits), int(group), int(bool(symmetric)), int(quant_dim),
                                            L.ptr(out), out.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
@@ -239,7 +239,7 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
     lut = (_luts.get(dev, L.IWQ_CODEC_APX_DOUBLE if double_approx else L.IWQ_CODEC_APX, exp_bits, mant_bits,
                      hi_align_start, hi_align_exp_field, tail_pad_bits) if use_lut else None)
-    with torch.cuda.device(dev):
+    with L.on_device(dev):
         st = lib.iwq_quantize_fp_approx_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
                                             int(mant_bits), int(group), int(quant_dim), int(hi_align_start),
                                             int(hi_align_exp_field), int(tail_pad_bits), int(bool(double_approx)),
@@ -269,7 +269,7 @@ def quantize_bfp(w: torch.Tensor, w_bit: int, group: int, quant_dim: int = 0, ou
     group_geometry(rows, cols, group, quant_dim)
     if out is None:
         out = torch.empty((rows, cols), dtype=w.dtype, device=w.device)
-    with torch.cuda.device(w.device):
+    with L.on_device(w.device):
         st = lib.iwq_quantize_bfp(L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(w_bit), int(group),
                                   int(quant_dim), L.ptr(out), out.stride(0), int(flags), L.stream_handle(w.device))
     _raise_for(st, "iwq_quantize_bfp")
@@ -298,7 +298,7 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     lut = _luts.get(dev, L.IWQ_CODEC_GRID) if use_lut else None
-    with torch.cuda.device(dev):
+    with L.on_device(dev):
         st = lib.iwq_fp4_grid_lut(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out),
                                   L.ptr(scales), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev),
                                   L.ptr(lut))
@@ -342,7 +342,7 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
                 or out.numel() != M * N):
             raise ValueError("w4a16_gemm: out must be a contiguous fp16 tensor of M*N elements on x's device")
         y = out.view(M, N)
-    with torch.cuda.device(x.device):
+    with L.on_device(x.device):
         st = lib.iwq_w4a16_gemm(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                 int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, int(flags),
                                 L.stream_handle(x.device))
@@ -356,7 +356,7 @@ def tile_codes(codes: torch.Tensor, N: int, K: int) -> torch.Tensor:
     L.require_device(codes)
     lib = L.load()
     out = torch.empty(N * K // 2, dtype=torch.uint8, device=codes.device)
-    with torch.cuda.device(codes.device):
+    with L.on_device(codes.device):
         st = lib.iwq_tile_codes(L.ptr(codes), int(N), int(K), L.ptr(out), L.stream_handle(codes.device))
     _raise_for(st, "iwq_tile_codes")
     return out
@@ -369,7 +369,7 @@ def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[to
     lib = L.load()
     if out is None:
         out = torch.empty((N, K), dtype=torch.float16, device=codes.device)
-    with torch.cuda.device(codes.device):
+    with L.on_device(codes.device):
         st = lib.iwq_dequant_packed(L.ptr(codes), L.ptr(scales), L.ptr(zeros), int(n_bits), int(group), int(N),
                                     int(K), L.ptr(out), out.stride(0), L.stream_handle(codes.device))
     _raise_for(st, "iwq_dequant_packed")
@@ -446,7 +446,7 @@ class BatchPlan:
         lib = L.load()
         flags = (L.IWQ_FLAG_BATCH_CODES if self.want_codes else 0) | ((int(variant) & 0xFF) << 16)
         sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
-        with torch.cuda.device(self.device):
+        with L.on_device(self.device):
             st = lib.iwq_quantize_minmax_batched(L.ptr(self.d_table), self.n, self.total_units,
                                                  L.DTYPE_CODE[self.dtype], self.n_bits, self.group,
                                                  int(self.symmetric), L.ptr(self.nan_flag), flags, sh)
@@ -458,7 +458,7 @@ def fill_synthetic(t: torch.Tensor, seed: int, index_offset: int = 0):
     L.require_device(t)
     assert t.is_contiguous() and t.dtype in L.DTYPE_CODE
     lib = L.load()
-    with torch.cuda.device(t.device):
+    with L.on_device(t.device):
         st = lib.iwq_fill_synthetic(L.ptr(t), t.numel(), L.DTYPE_CODE[t.dtype], int(seed), int(index_offset),
                                     L.stream_handle(t.device))
     L.check(st, "iwq_fill_synthetic")
@@ -470,7 +470,7 @@ def selftest_division(device="cuda"):
     fast division vs IEEE division, exhaustive over fp16 operands."""
     lib = L.load()
     counts = torch.zeros(3, dtype=torch.int64, device=device)
-    with torch.cuda.device(counts.device):
+    with L.on_device(counts.device):
         L.check(lib.iwq_selftest_division(L.ptr(counts), L.stream_handle(counts.device)), "iwq_selftest_division")
     return tuple(int(x) for x in counts.cpu())
 
@@ -534,7 +534,7 @@ class FpBatchPlan:
     def run(self, stream=None):
         lib = L.load()
         sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
-        with torch.cuda.device(self.device):
+        with L.on_device(self.device):
             st = lib.iwq_quantize_fp_batched(L.ptr(self.d_table), self.n, self.total_units, self.codec,
                                              self.exp_bits, self.mant_bits, self.group, int(self.symmetric),
                                              self.hs, self.hf, self.tp, L.ptr(self.lut), L.ptr(self.nan_flag), 0, sh)
