@@ -766,7 +766,7 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_reduce(const char* w, int64_t 
   }
 }
 
-template <int DT, bool SYM, int CODES, bool NTL, bool REV>
+template <int DT, bool SYM, int CODES, bool NTL, bool REV, int UN = 1>
 __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out, uint8_t* codes, void* scales,
                                                         void* zeros, int64_t nunits, const int32_t* partial,
                                                         int nparts, int n_bits, uint32_t* nan_flag) {
@@ -790,14 +790,27 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
   }
   bool any_nan = false;
   const int64_t nthreads = (int64_t)gridDim.x * BLOCK;
-  for (int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x; t < nunits; t += nthreads) {
-    const int64_t u = REV ? nunits - 1 - t : t;  // REV: the units the reduce read last (MALL) first
-    Vec8<DT> v, o;
-    v.template load<NTL>(w + u * 8 * F::BYTES);
-    uint32_t c[4];
-    any_nan |= quant8<DT, SYM>(v, p, n_bits, o, c);
-    if (out) o.store(out + u * 8 * F::BYTES);
-    if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+  // UN units per thread per iteration, all loads issued before the first store (UN > 1)
+  for (int64_t t0 = (int64_t)blockIdx.x * BLOCK + threadIdx.x; t0 < nunits; t0 += nthreads * UN) {
+    Vec8<DT> v[UN];
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t t = t0 + k * nthreads;
+      const int64_t u = REV ? nunits - 1 - t : t;  // REV: the units the reduce read last (MALL) first
+      v[k].template load<NTL>(w + (t < nunits ? u : 0) * 8 * F::BYTES);
+    }
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t t = t0 + k * nthreads;
+      if (t < nunits) {
+        const int64_t u = REV ? nunits - 1 - t : t;
+        Vec8<DT> o;
+        uint32_t c[4];
+        any_nan |= quant8<DT, SYM>(v[k], p, n_bits, o, c);
+        if (out) o.store(out + u * 8 * F::BYTES);
+        if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+      }
+    }
   }
   flag_nan(nan_flag, any_nan);
 }
@@ -1110,12 +1123,13 @@ constexpr int TENSOR_PARTS_MAX = 4096;
 //   0/2: temporal loads in both passes (default: cold 11008x4096 51.1 -> 49.0 us, 4096^2 22.6 -> 20.0 us)
 //   1: non-temporal loads in both passes (the previous default)
 //   3: temporal loads, apply walks the tensor backwards (the most recently read units first): no gain
-template <int DT, bool SYM, int CODES, bool NTL, bool REV>
+//   4 / 5: apply with 4 / 2 units in flight per thread: within +-2.5 % (profiles/r01_ab_tensor_unroll.jsonl)
+template <int DT, bool SYM, int CODES, bool NTL, bool REV, int UN = 1>
 void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nunits,
                         int64_t blocks, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st) {
   hipLaunchKernelGGL((k_tensor_reduce<DT, SYM, NTL>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
                      static_cast<const char*>(w), nunits, ws);
-  hipLaunchKernelGGL((k_tensor_apply<DT, SYM, CODES, NTL, REV>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
+  hipLaunchKernelGGL((k_tensor_apply<DT, SYM, CODES, NTL, REV, UN>), dim3((unsigned)blocks), dim3(BLOCK), 0, st,
                      static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales,
                      zeros, nunits, ws, (int)blocks, n_bits, nan_flag);
 }
@@ -1133,6 +1147,10 @@ hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, 
     launch_tensor_pair<DT, SYM, CODES, true, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   else if (variant == 3)
     launch_tensor_pair<DT, SYM, CODES, false, true>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
+  else if (variant == 4)
+    launch_tensor_pair<DT, SYM, CODES, false, false, 4>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
+  else if (variant == 5)
+    launch_tensor_pair<DT, SYM, CODES, false, false, 2>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   else
     launch_tensor_pair<DT, SYM, CODES, false, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   return hipGetLastError();
