@@ -658,13 +658,13 @@ __global__ __launch_bounds__(TX * TY) void k_column_reg(ColArgs a) {
   __syncthreads();
   // one thread per column folds the TY partials AND derives the group's parameters once (not once
   // per row slice: 8x less parameter math at TY = 8), shared through LDS
-  if (threadIdx.x < NC) {
+  for (int cc = threadIdx.x; cc < NC; cc += TX * TY) {  // NC > threads for the 64 x 4 shape
     int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
 #pragma unroll 8
-    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][threadIdx.x]); a_mx = max(a_mx, s_mx[y][threadIdx.x]); }
+    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][cc]); a_mx = max(a_mx, s_mx[y][cc]); }
     const GroupParams q = params_from_keys<DT, SYM>(a_mn, a_mx, a.n_bits, rmax_for(a.n_bits, SYM));
-    f_p[threadIdx.x] = q;
-    const int64_t col = (int64_t)blockIdx.x * NC + threadIdx.x;
+    f_p[cc] = q;
+    const int64_t col = (int64_t)blockIdx.x * NC + cc;
     if (col < a.cols) {
       const int64_t gidx = col * (a.rows / a.g) + jr;
       if (a.scales) store_param<DT>(a.scales, gidx, q.s);
@@ -1076,8 +1076,22 @@ hipError_t launch_col_t(const ColArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((k_column<DT, SYM, CODES, TX, TY>), grid, blk, 0, st, a);
   return hipGetLastError();
 }
+// 64 column chunks x 4 row slices (1 KiB row segments; g / 4 rows per thread): short groups only
+template <int DT, bool SYM, int CODES>
+hipError_t launch_col_wide(const ColArgs& a, hipStream_t st) {
+  constexpr int TX = 64, TY = 4;
+  dim3 grid((unsigned)((a.cols + 8 * TX - 1) / (8 * TX)), (unsigned)(a.rows / a.g));
+  if (a.g == 32) hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 8>), grid, dim3(TX * TY), 0, st, a);
+  else hipLaunchKernelGGL((k_column_reg<DT, SYM, CODES, TX, TY, 16>), grid, dim3(TX * TY), 0, st, a);
+  return hipGetLastError();
+}
 template <int DT, bool SYM, int CODES>
 hipError_t launch_col_v(int variant, const ColArgs& a, hipStream_t st) {
+  if constexpr (DT == DT_F16) {  // g = 32: 1 KiB row segments win (cold 11008x4096 44.7 -> 41.0 us);
+                                 // g = 64: 37.7 -> 39.4 us, so only as variant 4 (r01_ab_col_wide.jsonl)
+    if ((variant == 4 && a.g == 64) || ((variant == 0 || variant == 4) && a.g == 32))
+      return launch_col_wide<DT, SYM, CODES>(a, st);
+  }
   if (variant == 1) return launch_col_t<DT, SYM, CODES, 8, 32>(a, st);
   if (variant == 2) return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
   if (variant == 3 || a.g == 256) return launch_col_t<DT, SYM, CODES, 16, 16>(a, st);  // 16 rows/thread at g=256

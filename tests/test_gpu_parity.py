@@ -767,7 +767,7 @@ def test_quant_dim1_register_kernel(K, dtype):
     for g in (32, 64, 128, 256):
         for bits, sym in ((4, False), (8, True), (3, False)):
             exp = O.quantlinear_int(x, bits, g, sym, 1, dtype)
-            for flags in FLAG_SETS:
+            for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4)]:
                 r = K.quantize_minmax(xd, bits, g, sym, 1, want_codes=True, flags=flags)
                 assert bits_equal(to_np(r.out), exp.dequant), (g, bits, sym, flags)
                 assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (g, bits, sym, flags)
