@@ -115,6 +115,14 @@ __device__ __forceinline__ int apxd_tgt(uint32_t b0, uint32_t b1, uint32_t b2, u
   return tgt;
 }
 
+// value of lane (lane ^ M): ds_swizzle in bit-mask mode (no address VGPR) inside 32-lane halves,
+// ds_bpermute (__shfl_xor) across them
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+  if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);
+  else return (uint32_t)__shfl_xor((int)v, M);
+}
+
 // apxd_tgt on 4 elements at once: bytes of x / a / b / c are the info bytes of the quad members
 // (own, partner 1, 2, 3) of 4 elements; returns their 4 target exponents, one per byte.
 __device__ __forceinline__ uint32_t apxd_tgt4(uint32_t x, uint32_t a, uint32_t b, uint32_t c, const FpSpec& f) {
@@ -590,9 +598,9 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
                             __builtin_amdgcn_perm(info[3], info[2], 0x05010C0Cu);
         const uint32_t x1 = __builtin_amdgcn_perm(info[5], info[4], 0x0C0C0501u) |
                             __builtin_amdgcn_perm(info[7], info[6], 0x05010C0Cu);
-        const uint32_t a0 = (uint32_t)__shfl_xor((int)x0, LPG), a1 = (uint32_t)__shfl_xor((int)x1, LPG);
-        const uint32_t b0 = (uint32_t)__shfl_xor((int)x0, 2 * LPG), b1 = (uint32_t)__shfl_xor((int)x1, 2 * LPG);
-        const uint32_t c0 = (uint32_t)__shfl_xor((int)a0, 2 * LPG), c1 = (uint32_t)__shfl_xor((int)a1, 2 * LPG);
+        const uint32_t a0 = lane_xor<LPG>(x0), a1 = lane_xor<LPG>(x1);
+        const uint32_t b0 = lane_xor<2 * LPG>(x0), b1 = lane_xor<2 * LPG>(x1);
+        const uint32_t c0 = lane_xor<2 * LPG>(a0), c1 = lane_xor<2 * LPG>(a1);
         const uint32_t tw0 = apxd_tgt4(x0, a0, b0, c0, f), tw1 = apxd_tgt4(x1, a1, b1, c1, f);
         Vec8<DT_F16> o;
         bool nan8 = false;
