@@ -42,6 +42,11 @@ class _FlagPool:
         key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
         buf = self.buf.get(key)
         i = self.next.get(key, 0)
+        if (buf is None or i >= self.SIZE) and dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # never create or re-zero the shared pool inside a graph capture (its memory would come
+            # from the graph's private pool and the zero-fill would only be recorded): a per-call
+            # flag whose zero-fill is part of the captured graph instead
+            return torch.zeros(1, dtype=torch.int32, device=dev)
         if buf is None or i >= self.SIZE:
             if buf is None:
                 buf = torch.zeros(self.SIZE, dtype=torch.int32, device=dev)
@@ -320,6 +325,33 @@ def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: in
             and g > 0 and g % 32 == 0 and K % g == 0)
 
 
+def _check_packed(what, dev, codes, scales, zeros, n_bits, group, N, K, bias=None):
+    """Host-side validation of a packed 4-bit weight before its pointers reach a kernel: codes
+    [N*K/2] uint8, scales (and zeros) [N*K/g] fp16, all on `dev` and contiguous.  A tensor of the
+    wrong size or layout (e.g. quant_dim=1 codes) raises here instead of reading out of bounds."""
+    if not 2 <= n_bits <= 4:
+        raise ValueError(f"{what}: packed 4-bit codes need 2 <= n_bits <= 4")
+    g = K if group == -2 else group
+    if g <= 0 or K % g != 0:
+        raise ValueError(f"{what}: group {group} does not divide K={K}")
+    G = N * (K // g)
+
+    def chk(name, t, numel, dtype):
+        if t.device != dev:
+            raise ValueError(f"{what}: {name} is on {t.device}, expected {dev}")
+        if t.dtype != dtype:
+            raise TypeError(f"{what}: {name} must be {dtype}, got {t.dtype}")
+        if not t.is_contiguous() or t.numel() != numel:
+            raise ValueError(f"{what}: {name} must be contiguous with {numel} elements, got "
+                             f"{tuple(t.shape)}")
+    chk("codes", codes, N * K // 2, torch.uint8)
+    chk("scales", scales, G, torch.float16)
+    if zeros is not None:
+        chk("zeros", zeros, G, torch.float16)
+    if bias is not None:
+        chk("bias", bias, N, torch.float16)
+
+
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
                tiled: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -329,8 +361,11 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     if tiled:
         flags |= L.IWQ_FLAG_TILED_CODES
     L.require_device(x)
-    lib = L.load()
+    if x.dtype != torch.float16:
+        raise TypeError(f"w4a16_gemm: x must be float16, got {x.dtype}")
     K = x.shape[-1]
+    _check_packed("w4a16_gemm", x.device, codes, scales, zeros, n_bits, group, N, K, bias)
+    lib = L.load()
     x2 = x.reshape(-1, K)
     if x2.stride(-1) != 1 or x2.data_ptr() % 16 or x2.stride(0) % 8:
         x2 = x2.contiguous()
@@ -354,6 +389,8 @@ def tile_codes(codes: torch.Tensor, N: int, K: int) -> torch.Tensor:
     """Row-major packed 4-bit codes -> the decode tile layout (iwq_tile_codes): each 1 KiB a GEMV
     wave loads is contiguous.  Use with w4a16_gemm(..., tiled=True) for M <= 16."""
     L.require_device(codes)
+    if codes.dtype != torch.uint8 or not codes.is_contiguous() or codes.numel() != N * K // 2:
+        raise ValueError(f"tile_codes: codes must be contiguous uint8 with N*K/2 = {N * K // 2} elements")
     lib = L.load()
     out = torch.empty(N * K // 2, dtype=torch.uint8, device=codes.device)
     with L.on_device(codes.device):
@@ -366,9 +403,13 @@ def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[to
                    group: int, N: int, K: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Packed codes -> fp16 W_deq [N, K], bit-identical to the reference's dequantized weight."""
     L.require_device(codes)
+    _check_packed("dequant_packed", codes.device, codes, scales, zeros, n_bits, group, N, K)
     lib = L.load()
     if out is None:
         out = torch.empty((N, K), dtype=torch.float16, device=codes.device)
+    elif (out.dtype != torch.float16 or out.device != codes.device or out.shape != (N, K)
+          or out.stride(1) != 1):
+        raise ValueError("dequant_packed: out must be an fp16 [N, K] tensor with unit column stride")
     with L.on_device(codes.device):
         st = lib.iwq_dequant_packed(L.ptr(codes), L.ptr(scales), L.ptr(zeros), int(n_bits), int(group), int(N),
                                     int(K), L.ptr(out), out.stride(0), L.stream_handle(codes.device))

@@ -94,8 +94,17 @@ class QuantLinear(nn.Module):
         self._buffers.update(quantized=torch.tensor(False), scales=None, zeros=None, weight_fp4=None,
                              weight_fp6=None, weight_fp8=None, weight_bfp_mantissa=None,
                              weight_bfp_exponent=None, qweight=None, qweight_tiled=None)
+        # the packed codes are a derived cache of (weight, scales, zeros), not part of the reference's
+        # state: kept out of state_dict (a strict load of a reference checkpoint must match), and
+        # dropped whenever a state_dict is loaded so the forward never runs on stale codes
+        self._non_persistent_buffers_set.update(("qweight", "qweight_tiled"))
+        self.register_load_state_dict_post_hook(QuantLinear._drop_codes_after_load)
         if _init_weight:
             self.reset_parameters()
+
+    @staticmethod
+    def _drop_codes_after_load(module, incompatible_keys):
+        module._buffers.update(qweight=None, qweight_tiled=None)
 
     def reset_parameters(self):
         nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
@@ -222,17 +231,11 @@ class QuantLinear(nn.Module):
         fused = self.fused_forward
         if fused == "auto":
             fused = input.numel() // max(1, self.in_features) <= kernels.GEMV_MAX_M
-            if (fused and self.qweight_tiled is not None and self.weight_format == "int"
-                    and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
-                                                     self.w_group_size)
-                    and (self.bias is None or self.bias.dtype == torch.float16)):
+            if fused and self.qweight_tiled is not None and self._fused_ok(input):
                 return kernels.w4a16_gemm(input, self.qweight_tiled, self.scales.view(-1),
                                           None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                           self.w_group_size, self.out_features, self.bias, tiled=True)
-        if (fused and self.weight_format == "int" and self.quant_dim == 0 and self.qweight is not None
-                and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
-                                                 self.w_group_size)
-                and (self.bias is None or self.bias.dtype == torch.float16)):
+        if fused and self.qweight is not None and self._fused_ok(input):
             return kernels.w4a16_gemm(input, self.qweight, self.scales.view(-1),
                                       None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                       self.w_group_size, self.out_features, self.bias)
@@ -242,6 +245,17 @@ class QuantLinear(nn.Module):
         if input.dim() > 2:
             out = out.reshape(original_input_shape[:-1] + (self.out_features,))
         return out
+
+    def _fused_ok(self, input):
+        """The packed-code kernels read fp16 codes' parameters and fp16 activations: any other
+        storage dtype (bf16/fp32 weights -> bf16/fp32 scales) takes the reference's
+        F.linear(input, weight.to(input.dtype)) path instead of misreading the parameter bits."""
+        return (self.weight_format == "int" and self.quant_dim == 0
+                and self.scales is not None and self.scales.dtype == torch.float16
+                and (self.zeros is None or self.zeros.dtype == torch.float16)
+                and (self.bias is None or self.bias.dtype == torch.float16)
+                and kernels.w4a16_gemm_supported(input, self.out_features, self.in_features, self.w_bit,
+                                                 self.w_group_size))
 
     @classmethod
     def from_linear(cls, linear_layer, w_bit=4, w_group_size=128, symmetric=False, mode=0,

@@ -49,6 +49,28 @@ def _qkw(args, w_format):
     )
 
 
+def _tied(layers):
+    """Names of layers whose weight bytes overlap those of an EARLIER layer (tied weights: two
+    Linear modules over one storage).  Such a pair must not be two entries of one in-place launch
+    (a data race); the reference quantizes them one after the other, the later one on the earlier
+    one's dequantized output, which the per-layer loop after the batch replays in layer order.
+    One sort + sweep over byte intervals, so untied models pay O(n log n) host time."""
+    iv = []
+    for i, (n, m) in enumerate(layers):
+        w = m.weight.data
+        if w.numel():
+            lo = w.data_ptr()
+            iv.append((str(w.device), lo, lo + w.numel() * w.element_size(), i))
+    iv.sort()
+    tied, active = set(), []
+    for dev, lo, hi, i in iv:
+        active = [a for a in active if a[0] == dev and a[1] > lo]
+        for _, _, j in active:
+            tied.add(layers[max(i, j)][0])
+        active.append((dev, hi, i))
+    return tied
+
+
 def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True):
     if not ((args.w_bit is not None and args.w_bit < 16) and (args.a_bit is None or args.a_bit >= 16)):
         return model
@@ -66,14 +88,15 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
     layers = [(n, m) for n, m in model.named_modules() if _eligible(n, m)]
 
     done = set()
+    tied = _tied(layers) if batched else set()
     g = kw["w_group_size"]
     if (batched and w_format == "int" and not kw["approximate"] and kw["quant_dim"] == 0
             and g in kernels.FAST_GROUPS and 2 <= kw["w_bit"] <= 8 and layers):
         buckets = {}
         for n, m in layers:
             w = m.weight.data
-            if (w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous() and w.shape[1] % g == 0
-                    and w.dtype in (torch.float16, torch.bfloat16, torch.float32)
+            if (n not in tied and w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous()
+                    and w.shape[1] % g == 0 and w.dtype in (torch.float16, torch.bfloat16, torch.float32)
                     and w.data_ptr() % 16 == 0):
                 buckets.setdefault((w.device, w.dtype), []).append((n, m))
         for (dev, dt), items in buckets.items():
@@ -89,7 +112,7 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
                 done.add(n)
     if (batched and w_format in ("fp4", "fp6", "fp8") and kw["quant_dim"] == 0 and g in kernels.FAST_GROUPS
             and not (kw["approximate"] and kw["double_approximate"]) and layers):
-        _batched_fp(model, layers, kw, w_format, done)
+        _batched_fp(model, layers, kw, w_format, done, tied)
     for n, m in layers:
         if n in done:
             continue
@@ -98,7 +121,7 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
     return model
 
 
-def _batched_fp(model, layers, kw, fmt, done):
+def _batched_fp(model, layers, kw, fmt, done, tied):
     """FP formats (and the single-aligned approximate decode) of every eligible fp16 layer on one
     GPU in one launch (kernels.FpBatchPlan); buffers as QuantLinear's FP branches set them."""
     from . import _lib as L
@@ -115,8 +138,8 @@ def _batched_fp(model, layers, kw, fmt, done):
     buckets = {}
     for n, mod in layers:
         w = mod.weight.data
-        if (w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous() and w.shape[1] % g == 0
-                and w.dtype == torch.float16 and w.data_ptr() % 16 == 0):
+        if (n not in tied and w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous()
+                and w.shape[1] % g == 0 and w.dtype == torch.float16 and w.data_ptr() % 16 == 0):
             buckets.setdefault(w.device, []).append((n, mod))
     for dev, items in buckets.items():
         ws = [mod.weight.data for _, mod in items]

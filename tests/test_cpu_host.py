@@ -149,3 +149,47 @@ def test_synth_generator_properties():
     # counter-based: any sub-range can be regenerated from its offset
     from oracle.synth import synth_f32
     assert np.array_equal(synth_f32(5, 1500, 100), a.reshape(-1)[1500:1600])
+
+
+def test_packed_validation_on_host():
+    """kernels._check_packed rejects codes/scales/zeros of the wrong size, dtype or device before
+    any pointer reaches the C-ABI (no GPU needed: the check is pure host logic)."""
+    from iron_weight_only_quant_amd.kernels import _check_packed
+    dev = torch.device("cpu")
+    N, K, g = 256, 512, 128
+    codes = torch.zeros(N * K // 2, dtype=torch.uint8)
+    s = torch.zeros(N * K // g, dtype=torch.float16)
+    _check_packed("t", dev, codes, s, s, 4, g, N, K)
+    _check_packed("t", dev, codes, torch.zeros(N, dtype=torch.float16), None, 4, -2, N, K)
+    with pytest.raises(ValueError):
+        _check_packed("t", dev, codes[:-1], s, s, 4, g, N, K)
+    with pytest.raises(ValueError):
+        _check_packed("t", dev, codes, s, s, 4, 64, N, K)
+    with pytest.raises(TypeError):
+        _check_packed("t", dev, codes, s.float(), None, 4, g, N, K)
+    with pytest.raises(TypeError):
+        _check_packed("t", dev, codes, s, s.bfloat16(), 4, g, N, K)
+    with pytest.raises(ValueError):
+        _check_packed("t", dev, codes, s, s, 8, g, N, K)
+    with pytest.raises(ValueError):
+        _check_packed("t", torch.device("cuda", 0), codes, s, s, 4, g, N, K)
+    with pytest.raises(ValueError):
+        _check_packed("t", dev, codes, s, s, 4, g, N, K, bias=torch.zeros(N + 1, dtype=torch.float16))
+
+
+def test_tied_weight_detection():
+    """quant_wrapper._tied: a layer whose weight bytes overlap an EARLIER layer's goes to the
+    per-layer path; disjoint views of one buffer stay batchable."""
+    from iron_weight_only_quant_amd.quant_wrapper import _tied
+    a, b, c = torch.nn.Linear(8, 8), torch.nn.Linear(8, 8), torch.nn.Linear(8, 8)
+    b.weight = a.weight
+    assert _tied([("a", a), ("b", b), ("c", c)]) == {"b"}
+    assert _tied([("b", b), ("a", a)]) == {"a"}
+    big = torch.zeros(16, 8)
+    d, e, f = torch.nn.Linear(8, 8), torch.nn.Linear(8, 8), torch.nn.Linear(8, 8)
+    d.weight = torch.nn.Parameter(big[:8])
+    e.weight = torch.nn.Parameter(big[8:])
+    f.weight = torch.nn.Parameter(big[4:12])
+    assert _tied([("d", d), ("e", e)]) == set()
+    assert _tied([("f", f), ("d", d), ("e", e)]) == {"d", "e"}
+    assert _tied([("d", d), ("e", e), ("f", f)]) == {"f"}
