@@ -6,8 +6,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
-SOURCES = ["iwq_minmax.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_synth.hip"]
-DEPS = SOURCES + ["iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h"]
+SOURCES = ["iwq_minmax.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip"]
+DEPS = SOURCES + ["iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Numerics: no FMA contraction, IEEE fp32 division, denormals preserved.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
@@ -44,8 +44,17 @@ def build_library(force=False, verbose=True):
             print("[iwq build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True, cwd=CSRC)
 
-    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1)) as ex:
-        list(ex.map(cc, zip(SOURCES, objs)))
+    # recompile only objects older than their source or any shared header
+    headers = [os.path.join(CSRC, d) for d in DEPS if d not in SOURCES] + [os.path.join(HERE, "..", "include", "iwq.h")]
+    newest_header = max(os.path.getmtime(h) for h in headers if os.path.exists(h))
+
+    def obj_stale(src_obj):
+        src, obj = src_obj
+        return (force or not os.path.exists(obj) or os.path.getmtime(obj) < newest_header
+                or os.path.getmtime(obj) < os.path.getmtime(os.path.join(CSRC, src)))
+    todo = [so for so in zip(SOURCES, objs) if obj_stale(so)]
+    with ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 1))) as ex:
+        list(ex.map(cc, todo))
     tmp = LIB + ".tmp"
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

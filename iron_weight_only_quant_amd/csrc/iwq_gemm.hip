@@ -19,6 +19,7 @@
 //     MFMA's 32-wide k slice of lane group q is the logical k range [32q+8s, 32q+8s+8) of the tile.
 //   XCD-aware tile order: consecutive tiles of one X row panel are dealt to one XCD (L2 reuse).
 #include "iwq_common.cuh"
+#include "iwq_prefill.h"
 #include "../../include/iwq.h"
 
 using namespace iwq;
@@ -1197,6 +1198,27 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }
+  } else if (((variant == 0 && M < 512) || (variant >= 50 && variant < 60)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+             mid_supported(M, N, K, a.gpr, a.group)) {
+    // 16 < M < 512 default since round 2: the weight-streaming mid-M kernel (iwq_prefill.hip)
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    const hipError_t e = mid_launch(p, (int)variant, false, st);
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
+  } else if (((variant == 0 && M >= 512) || (variant >= 40 && variant < 50)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+             prefill_b32_supported(M, N, K, a.gpr, a.group)) {
+    // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel
+    // scale factored into the epilogue); the round-1 k_w4a16_big below stays reachable as variant 2
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    const hipError_t e = prefill_b32_launch(p, (int)variant, st);
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
   } else if (N % BG_N == 0 && K % 64 == 0 && M >= 512 && variant != 1 && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              (a.gpr == 1 || a.group % 64 == 0)) {
     const int64_t blocks = ((M + BG_M - 1) / BG_M) * (N / BG_N);

@@ -1,0 +1,855 @@
+// iwq_prefill.hip — prefill (large M) fused dequant -> GEMM for packed INT4 weights, on the
+// 32x32x16 f16 MFMA.
+//
+// Replaces QuantLinear.forward = F.linear(x, W_deq, b) (quant_linear.py:960-972) for weights held
+// packed (include/iwq.h layout): y = x @ W_deq^T + b with W_deq = RN16((q - z) * s) rebuilt in
+// registers from 4-bit codes inside the K loop.
+//
+// Why 32x32x16 and not 16x16x32 (k_w4a16_big, iwq_gemm.hip): the dequant is VALU work that has to
+// hide in the gaps of the MFMA stream.  A 16x16x32 f16 MFMA occupies its SIMD for 16 cycles and
+// holds vector issue for 8 of them, leaving room for 2 four-cycle VALU instructions; a 32x32x16
+// occupies 32 cycles for the same 8 of hold, leaving room for 6 (MI355X_MICROARCH.md, cycle
+// constants: 'vector-instruction ISSUE cost').  Both do the same FLOP per cycle and each B element
+// is dequantized by exactly one lane of its wave either way, so the dequant costs 4 (exact) or 3
+// (scale factored out) VALU per 32x32x16 MFMA: inside the 6 free slots, where with 16x16x32 the
+// same work needs every free slot and anything else (LDS reads, DMA issue, waits) lands on the
+// MFMA critical path.
+//
+// Structure (k_w4a16_b32): 256 x 256 output tile per 512-thread workgroup, 8 waves as 2 (M) x 4
+// (N), 128 x 64 per wave = 4 x 2 MFMA tiles of 32 x 32; K in steps of 64; X and codes staged by
+// LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring, ONE raw s_barrier per K-step with a
+// counted vmcnt (one stage stays in flight across it).
+//   k order: MFMA slice s of a K-step gives lane half h the logical k = 32 h + 8 s + [0, 8): the
+//   lane's B codes for all four slices are then ONE contiguous 16-B piece of its column (one
+//   ds_read_b128 per 32-column tile per K-step), and its A fragment of slice s one 16-B piece of
+//   its X row (ds_read_b128).
+//   LDS images: X rows of 128 B, 16-B chunk c of row r at c ^ ((r >> 1) & 7); codes columns of
+//   32 B, chunk c of column n at c ^ ((n >> 3) & 1): both read conflict-free (16 lanes hit 16
+//   distinct 16-B slots of the 256-B bank row).  The DMA writes lane-linearly, so the swizzle is
+//   applied to the per-lane SOURCE address.
+//   dequant (natural k order): v_perm_b32 replicates a code byte into both halves, one
+//   v_and_or_b32 makes (1024 + q_even, 64 + q_odd), one v_pk_add_f16 subtracts (1024 + z, 64 + z)
+//   exactly; grouped / exact mode: one v_pk_mul_f16 by s = RN16((q - z) s), the reference's fp16
+//   weight.  FACTOR (per-channel): B = (q - z) exactly and the fp32 accumulator is scaled by s in
+//   the epilogue (y = RN16(s * sum x (q - z) + b): no per-element fp16 rounding of the weight, so
+//   y differs from F.linear(x, W_deq) by that rounding only -- within the fp16 output tolerance;
+//   with x = I the result is still W_deq bit for bit, since s (q - z) is exact in fp32).
+#include "iwq_common.cuh"
+#include "iwq_prefill.h"
+
+namespace iwq {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int TM = 256, TN = 256, TK = 64, THR = 512, NSTAGE = 3;
+constexpr int XS = TM * TK * 2;  // X bytes per stage (32 KiB)
+constexpr int CS = TN * TK / 2;  // code bytes per stage (8 KiB)
+constexpr int PS = 2 * TN * 4;   // grouped: 256 scales + 256 zero points, one dword each
+
+__device__ __forceinline__ int xswz(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int cswz(int n) { return (n >> 3) & 1; }
+
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
+  return r;
+}
+
+__device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
+  // consecutive tiles of one X row panel on one XCD (bijective for any block count)
+  const int64_t xcd = bid % 8, i = bid / 8;
+  const int64_t q = nblocks / 8, r = nblocks % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+}
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds2(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 2, 0, 0);
+}
+
+// one code dword (k offsets 0..7, nibble p = offset p) -> 8 fp16 weights in natural k order:
+// (q - z) exactly, times s unless the scale is factored out (SCALE = false)
+template <bool SCALE>
+__device__ __forceinline__ h8 dq8(uint32_t w, h2 zz, h2 s, uint32_t mask_s, uint32_t magic_v) {
+  h2 d0 = as_h2(and_or(__builtin_amdgcn_perm(w, w, 0x0C000C00u), mask_s, magic_v)) - zz;
+  h2 d1 = as_h2(and_or(__builtin_amdgcn_perm(w, w, 0x0C010C01u), mask_s, magic_v)) - zz;
+  h2 d2 = as_h2(and_or(__builtin_amdgcn_perm(w, w, 0x0C020C02u), mask_s, magic_v)) - zz;
+  h2 d3 = as_h2(and_or(__builtin_amdgcn_perm(w, w, 0x0C030C03u), mask_s, magic_v)) - zz;
+  if constexpr (SCALE) {
+    d0 = d0 * s;
+    d1 = d1 * s;
+    d2 = d2 * s;
+    d3 = d3 * s;
+  }
+  return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
+}
+
+// SCHED 0: compiler schedule; 1: slice s+1's dequant interleaved with slice s's MFMAs
+// (sched_group_barrier, 1 MFMA : 3 VALU); PRIO: s_setprio(1) over each slice's MFMAs.
+template <bool GROUPED, bool FACTOR, int SCHED, bool PRIO>
+__global__ __launch_bounds__(THR) void k_w4a16_b32(PrefillArgs a) {
+  static_assert(!(GROUPED && FACTOR), "grouped scales change along k: no factoring");
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PER_STAGE = 4 + 1 + (GROUPED ? 1 : 0);  // DMA instructions per thread per stage
+  constexpr bool SCALE = !FACTOR;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  // DMA sources (per lane); destinations are wave-uniform 1-KiB slots filled lane-linearly:
+  // X: slot 4 wid + i = rows 8 (4 wid + i) + [0, 8), lane = 8 (row % 8) + physical chunk
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;  // rows past M: any valid row (discarded)
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  // codes: slot wid = columns 32 wid + [0, 32), lane = 2 (col % 32) + physical chunk
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {  // wave w < 4: scale of column 64 w + lane; w >= 4: its zero point
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+  };
+
+  h2 sv[2], zz[2];
+  float sf[2] = {1.0f, 1.0f};
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = n0 + wn * 64 + nt * 32 + r32;
+      const _Float16 sc = gp<_Float16>(a.scales)[col];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+      sv[nt] = h2{sc, sc};
+      sf[nt] = (float)sc;
+      zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};  // exact: z is a small integer
+    }
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  f16x acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // own DMA of stage kt retired (stage kt+1's stays in flight); the barrier makes every wave's
+    // part visible and proves every wave is done reading the stage about to be refilled
+    if (kt + 1 < nk) {
+      if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(kt + 2, (kt + 2) % NSTAGE);
+    const uint8_t* xs = smem + (kt % NSTAGE) * STAGE;
+    const uint8_t* cs = xs + XS;
+    if constexpr (GROUPED) {
+      const uint32_t* ps = reinterpret_cast<const uint32_t*>(cs + CS);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = wn * 64 + nt * 32 + r32;
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
+        const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[TN + col]) : a.zsym;
+        sv[nt] = h2{sc, sc};
+        zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      }
+    }
+    u32x4 wc[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = wn * 64 + nt * 32 + r32;
+      wc[nt] = *reinterpret_cast<const u32x4*>(cs + col * 32 + ((h ^ cswz(col)) << 4));
+    }
+    h8 bf[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bf[nt][0] = dq8<SCALE>(wc[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      h8 af[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int row = wm * 128 + mt * 32 + r32;
+        af[mt] = *reinterpret_cast<const h8*>(xs + row * 128 + (((4 * h + s) ^ xswz(row)) << 4));
+      }
+      if (s + 1 < 4) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) bf[nt][s + 1] = dq8<SCALE>(wc[nt][s + 1], zz[nt], sv[nt], mask_s, magic_v);
+      }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[mt], bf[nt][s], acc[mt][nt], 0, 0, 0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      if constexpr (SCHED == 1) {
+        // per slice: the A reads, then each MFMA followed by ~3 of the next slice's dequant VALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // 4 DS reads
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // 3 VALU
+        }
+      }
+    }
+  }
+
+  // epilogue, 32x32 C layout: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+// Early-barrier form (k_w4a16_b32e): the barrier that publishes stage kt+1 sits BEFORE the last
+// MFMA slice of stage kt, whose operands are already in registers.  After the barrier a wave
+// issues the next DMA, the LDS reads of stage kt+1's codes and first A slice and that slice's
+// dequant, and only then slice 3's 8 MFMAs (256 cycles of MFMA work) -- which cover the LDS read
+// latency and the dequant chain of the next K-step instead of leaving the MFMA pipe idle at every
+// K-step start.  Same k order, same accumulation order: bit-identical to k_w4a16_b32.
+// WAR: a wave's last reads of stage kt (slice 3's A fragments) are retired (lgkmcnt(0)) before the
+// barrier after which stage kt is refilled.
+template <bool GROUPED, bool FACTOR>
+__global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
+  static_assert(!(GROUPED && FACTOR), "grouped scales change along k: no factoring");
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PER_STAGE = 4 + 1 + (GROUPED ? 1 : 0);
+  constexpr bool SCALE = !FACTOR;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+  };
+
+  h2 sv[2], zz[2];
+  float sf[2] = {1.0f, 1.0f};
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = n0 + wn * 64 + nt * 32 + r32;
+      const _Float16 sc = gp<_Float16>(a.scales)[col];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+      sv[nt] = h2{sc, sc};
+      sf[nt] = (float)sc;
+      zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    }
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  // stage-local reads: grouped parameters, the codes of both 32-column tiles, one A slice
+  auto read_params = [&](const uint8_t* xs) {
+    if constexpr (GROUPED) {
+      const uint32_t* ps = reinterpret_cast<const uint32_t*>(xs + XS + CS);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = wn * 64 + nt * 32 + r32;
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
+        const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[TN + col]) : a.zsym;
+        sv[nt] = h2{sc, sc};
+        zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      }
+    }
+  };
+  auto read_codes = [&](const uint8_t* xs, u32x4 (&wc)[2]) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = wn * 64 + nt * 32 + r32;
+      wc[nt] = *reinterpret_cast<const u32x4*>(xs + XS + col * 32 + ((h ^ cswz(col)) << 4));
+    }
+  };
+  auto read_a = [&](const uint8_t* xs, int s, h8 (&af)[4]) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int row = wm * 128 + mt * 32 + r32;
+      af[mt] = *reinterpret_cast<const h8*>(xs + row * 128 + (((4 * h + s) ^ xswz(row)) << 4));
+    }
+  };
+
+  f16x acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+#define IWQ_MFMA_SLICE(AF, B0)                                                                   \
+  _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                \
+  _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                \
+    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AF[mt], B0[nt], acc[mt][nt], 0, 0, 0);
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (nk > 2) issue(2, 2);
+  u32x4 wc[2];
+  h8 af[4], bcur[2];
+  read_params(smem);
+  read_codes(smem, wc);
+  read_a(smem, 0, af);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) bcur[nt] = dq8<SCALE>(wc[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+
+  // slices 0..2 of the stage at xs: each slice's MFMAs behind the next slice's reads + dequant
+#define IWQ_SLICES_012(XS)                                                                        \
+  _Pragma("unroll") for (int s = 0; s < 3; ++s) {                                                 \
+    h8 an[4], bn[2];                                                                              \
+    read_a(XS, s + 1, an);                                                                        \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                              \
+      bn[nt] = dq8<SCALE>(wc[nt][s + 1], zz[nt], sv[nt], mask_s, magic_v);                        \
+    IWQ_MFMA_SLICE(af, bcur)                                                                      \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) af[mt] = an[mt];                            \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt) bcur[nt] = bn[nt];                          \
+  }
+  // the last K-step is peeled: no branch between the barrier and slice 3 inside the loop
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint8_t* xs = smem + (kt % NSTAGE) * STAGE;
+    IWQ_SLICES_012(xs)
+    // slice 3's operands are in registers; publish stage kt+1, retire this wave's reads of stage kt
+    if (kt + 2 < nk) {
+      if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + 3 < nk) issue(kt + 3, kt % NSTAGE);
+    const uint8_t* xn = smem + ((kt + 1) % NSTAGE) * STAGE;
+    h8 an[4], bn[2];
+    u32x4 wn2[2];
+    read_params(xn);
+    read_codes(xn, wn2);
+    read_a(xn, 0, an);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bn[nt] = dq8<SCALE>(wn2[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+    IWQ_MFMA_SLICE(af, bcur)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = an[mt];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      bcur[nt] = bn[nt];
+      wc[nt] = wn2[nt];
+    }
+  }
+  {
+    const uint8_t* xs = smem + ((nk - 1) % NSTAGE) * STAGE;
+    IWQ_SLICES_012(xs)
+    IWQ_MFMA_SLICE(af, bcur)
+  }
+#undef IWQ_SLICES_012
+
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+#undef IWQ_MFMA_SLICE
+
+template <bool GROUPED, bool FACTOR>
+hipError_t launch_e(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_b32e<GROUPED, FACTOR>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  return hipGetLastError();
+}
+
+// 16x16x32 form of the early-barrier kernel (k_w4a16_b16e).  MI355X_MICROARCH.md (DVFS item 7):
+// on random data a 16x16x32 MFMA loop holds a ~13 % higher clock than a 32x32x16 loop at equal
+// cycles per FLOP, so with the dequant trimmed to 12 VALU per 8 weights (factored scale) the
+// smaller shape can come out ahead despite its 2-slot gaps.  Same tile, staging and barrier
+// placement as k_w4a16_b32e; per wave 128 x 64 = 8 x 4 tiles of 16 x 16; k order: lane group q
+// of slice s holds k = 16 q + 8 s + [0, 8), so a lane's codes for a K-step are ONE 8-byte piece of
+// its column.  A K-step is 4 sub-steps (slice s, rows half) of 16 MFMAs; each sub-step's MFMAs
+// run behind the next sub-step's A reads (and the next slice's dequant).
+template <bool GROUPED, bool FACTOR>
+__global__ __launch_bounds__(THR) void k_w4a16_b16e(PrefillArgs a) {
+  static_assert(!(GROUPED && FACTOR), "grouped scales change along k: no factoring");
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PER_STAGE = 4 + 1 + (GROUPED ? 1 : 0);
+  constexpr bool SCALE = !FACTOR;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+  };
+
+  h2 sv[4], zz[4];
+  float sf[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = n0 + wn * 64 + nt * 16 + r16;
+      const _Float16 sc = gp<_Float16>(a.scales)[col];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+      sv[nt] = h2{sc, sc};
+      sf[nt] = (float)sc;
+      zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    }
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  auto read_params = [&](const uint8_t* xs) {
+    if constexpr (GROUPED) {
+      const uint32_t* ps = reinterpret_cast<const uint32_t*>(xs + XS + CS);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int col = wn * 64 + nt * 16 + r16;
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
+        const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[TN + col]) : a.zsym;
+        sv[nt] = h2{sc, sc};
+        zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      }
+    }
+  };
+  // lane's 8 code bytes of column col = k 16 q + [0, 16): logical chunk q >> 1, half q & 1
+  auto read_codes = [&](const uint8_t* xs, u32x2 (&wc)[4]) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = wn * 64 + nt * 16 + r16;
+      wc[nt] = *reinterpret_cast<const u32x2*>(xs + XS + col * 32 + ((((q >> 1) ^ cswz(col)) << 4) | ((q & 1) << 3)));
+    }
+  };
+  // A fragments of slice s, row half hf (4 of the 8 16-row tiles)
+  auto read_a = [&](const uint8_t* xs, int s, int hf, h8 (&af)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 128 + (hf * 4 + i) * 16 + r16;
+      af[i] = *reinterpret_cast<const h8*>(xs + row * 128 + (((2 * q + s) ^ xswz(row)) << 4));
+    }
+  };
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f4){0.f, 0.f, 0.f, 0.f};
+#define IWQ_MFMA_HALF(AF, B0, HF)                                                                  \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                   \
+  _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                                \
+    acc[(HF) * 4 + i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(AF[i], B0[nt], acc[(HF) * 4 + i][nt], 0, 0, 0);
+#define IWQ_DQ_SLICE(DST, WC, S)                                                                   \
+  _Pragma("unroll") for (int nt = 0; nt < 4; ++nt)                                                \
+    DST[nt] = dq8<SCALE>(WC[nt][S], zz[nt], sv[nt], mask_s, magic_v);
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (nk > 2) issue(2, 2);
+  u32x2 wc[4];
+  h8 af[4], bcur[4];
+  read_params(smem);
+  read_codes(smem, wc);
+  read_a(smem, 0, 0, af);
+  IWQ_DQ_SLICE(bcur, wc, 0)
+
+  // sub-steps 0..2 of the stage at XS: (s 0, half 0), (0, 1), (1, 0); sub-step 3 = (1, 1)
+#define IWQ_SUBSTEPS_012(XS)                                                                       \
+  {                                                                                               \
+    h8 an[4], bn[4];                                                                              \
+    read_a(XS, 0, 1, an);                                                                         \
+    IWQ_MFMA_HALF(af, bcur, 0)                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) af[i] = an[i];                                 \
+    read_a(XS, 1, 0, an);                                                                         \
+    IWQ_DQ_SLICE(bn, wc, 1)                                                                       \
+    IWQ_MFMA_HALF(af, bcur, 1)                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) af[i] = an[i];                                 \
+    _Pragma("unroll") for (int nt = 0; nt < 4; ++nt) bcur[nt] = bn[nt];                          \
+    read_a(XS, 1, 1, an);                                                                         \
+    IWQ_MFMA_HALF(af, bcur, 0)                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) af[i] = an[i];                                 \
+  }
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint8_t* xs = smem + (kt % NSTAGE) * STAGE;
+    IWQ_SUBSTEPS_012(xs)
+    if (kt + 2 < nk) {
+      if constexpr (PER_STAGE == 6) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (kt + 3 < nk) issue(kt + 3, kt % NSTAGE);
+    const uint8_t* xn = smem + ((kt + 1) % NSTAGE) * STAGE;
+    h8 an[4], bn[4];
+    u32x2 wn2[4];
+    read_params(xn);
+    read_codes(xn, wn2);
+    read_a(xn, 0, 0, an);
+    IWQ_DQ_SLICE(bn, wn2, 0)
+    IWQ_MFMA_HALF(af, bcur, 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = an[i];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      bcur[nt] = bn[nt];
+      wc[nt] = wn2[nt];
+    }
+  }
+  {
+    const uint8_t* xs = smem + ((nk - 1) % NSTAGE) * STAGE;
+    IWQ_SUBSTEPS_012(xs)
+    IWQ_MFMA_HALF(af, bcur, 1)
+  }
+#undef IWQ_SUBSTEPS_012
+#undef IWQ_DQ_SLICE
+#undef IWQ_MFMA_HALF
+
+  // epilogue, 16x16 C layout: col = lane & 15, row = 4 (lane >> 4) + reg
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wn * 64 + nt * 16 + r16;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 128 + mt * 16 + 4 * q + r;
+        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+template <bool GROUPED, bool FACTOR>
+hipError_t launch_16e(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_b16e<GROUPED, FACTOR>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_mid: 16 < M < 512 (batched decode, short prompts).  A 256 x 256 tile leaves most of the
+// chip idle here (q_proj at M = 64: 16 workgroups) and the weight stream, not the MFMA, is the
+// floor, so this is the decode GEMV's structure (k_w4a16_gemv_ct, iwq_gemm.hip) widened to MT
+// tiles of 16 rows: a workgroup of S waves owns CT column tiles x MT row tiles; wave ks takes the
+// 128-k steps ks, ks + S, ...; each wave keeps a ring of PF steps of code loads (CT x 16 B per lane)
+// AND of X fragments (MT x 4 x 16 B per lane, read from L2 in natural k order -- no LDS image, no
+// permutation) in flight; per step every dequantized B fragment feeds MT MFMAs (the dequant VALU
+// per FLOP drops MT-fold vs the GEMV); the S partial tiles are summed through LDS in k-split order.
+// k order: lane group q of slice s holds k = 32 q + 8 s + [0, 8) -- exactly the GEMV's code bytes
+// (row-major or the decode tile layout), decoded in natural order (dq8).  grid = (N / (16 CT),
+// ceil(M / (16 MT))): row tiles past M read row M-1 (discarded).
+// ---------------------------------------------------------------------------------------------
+template <int PF, int S, int CT, int MT, bool FACTOR, bool TILED>
+__global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
+  constexpr bool SCALE = !FACTOR;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int lane = threadIdx.x & 63;
+  const int ks = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int tile0 = blockIdx.x * CT;
+  const int mrow0 = blockIdx.y * 16 * MT;
+  const int nks = a.K / 128;
+  const int nj = nks > ks ? (nks - ks + S - 1) / S : 0;
+  const int64_t crow = a.K / 2;
+  const int64_t tstride = TILED ? (int64_t)nks * 1024 : 16 * crow;  // code bytes between column tiles
+  const uint8_t* cbase = TILED ? a.codes + (int64_t)tile0 * tstride + lane * 16
+                               : a.codes + (int64_t)(tile0 * 16 + r16) * crow + q * 16;
+  const _Float16* xrow[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int r = mrow0 + mt * 16 + r16;
+    xrow[mt] = a.x + (int64_t)(r < a.M ? r : a.M - 1) * a.lda + 32 * q;
+  }
+  const bool perch = a.gpr == 1;
+  h2 zz0[CT], sv0[CT];
+  float sf[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int n = (tile0 + c) * 16 + r16;
+    const _Float16 sc = perch ? gp<_Float16>(a.scales)[n] : (_Float16)1.0f;
+    const float zf = perch ? (a.zeros ? (float)gp<_Float16>(a.zeros)[n] : a.zsym) : 0.0f;
+    sv0[c] = h2{sc, sc};
+    sf[c] = (FACTOR && perch) ? (float)sc : 1.0f;
+    zz0[c] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  u32x4 bc[PF][CT];
+  u32x4 xa[PF][MT][4];
+  _Float16 sv[PF][CT], zv[PF][CT];
+  auto load = [&](int j, int u) {
+    const int kt = ks + j * S;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+      bc[u][c] = __builtin_nontemporal_load(gp<u32x4>(cbase + c * tstride + kt * (TILED ? 1024 : 64)));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xa[u][mt][s] = *gp<u32x4>(xrow[mt] + kt * 128 + 8 * s);
+    if (!perch) {
+      const int gk = (kt * 128 + 32 * q) / a.group;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int64_t gi = (int64_t)((tile0 + c) * 16 + r16) * a.gpr + gk;
+        sv[u][c] = gp<_Float16>(a.scales)[gi];
+        zv[u][c] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
+      }
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nj) load(u, u);
+
+  f4 acc[MT][CT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[mt][c] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nj; j0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int j = j0 + u;
+      if (j >= nj) break;
+      h2 s2[CT], z2[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        if (perch) {
+          s2[c] = sv0[c];
+          z2[c] = zz0[c];
+        } else {
+          const float zf = (float)zv[u][c];
+          s2[c] = h2{sv[u][c], sv[u][c]};
+          z2[c] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const h8 bf = (perch && FACTOR) ? dq8<false>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v)
+                                          : dq8<true>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, xa[u][mt][s]), bf,
+                                                                acc[mt][c], 0, 0, 0);
+        }
+      }
+      if (j + PF < nj) load(j + PF, u);
+    }
+  }
+  (void)SCALE;
+  float* red = reinterpret_cast<float*>(dsm);  // [S][MT * CT][256]
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+      *reinterpret_cast<f4*>(red + ((ks * MT + mt) * CT + c) * 256 + lane * 4) = acc[mt][c];
+  __syncthreads();
+  for (int o = threadIdx.x; o < MT * CT * 256; o += S * 64) {
+    const int tc = o >> 8, e = o & 255;
+    const int mt = tc / CT, c = tc % CT;
+    const int ln = e >> 2, reg = e & 3;
+    const int row = mrow0 + mt * 16 + 4 * (ln >> 4) + reg, col = (tile0 + c) * 16 + (ln & 15);
+    if (row < a.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) v += red[(k * MT * CT + tc) * 256 + e];
+      if (FACTOR && perch) v *= (float)gp<_Float16>(a.scales)[col];
+      if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
+      gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+    }
+  }
+}
+
+template <int PF, int S, int CT, int MT>
+hipError_t launch_mid(const PrefillArgs& a, bool tiled, hipStream_t st) {
+  const dim3 grid((unsigned)(a.N / (16 * CT)), (unsigned)((a.M + 16 * MT - 1) / (16 * MT)));
+  const size_t red = (size_t)S * MT * CT * 256 * 4;
+  if (tiled) hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true>), grid, dim3(S * 64), red, st, a);
+  else hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false>), grid, dim3(S * 64), red, st, a);
+  return hipGetLastError();
+}
+
+template <bool GROUPED, bool FACTOR, int SCHED, bool PRIO>
+hipError_t launch(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_b32<GROUPED, FACTOR, SCHED, PRIO>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool mid_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
+  return M >= 1 && N % 64 == 0 && K % 128 == 0 && (gpr == 1 || group % 32 == 0);
+}
+
+// variants: 50 MT 1 CT 2, 51 MT 2 CT 1, 52 MT 2 CT 2, 53 MT 2 CT 4, 54 MT 4 CT 1, 55 MT 4 CT 2;
+// 0 = by M (interleaved A/B vs hipBLASLt on the Llama-2-7B shapes, profiles/r02_ab_mid*.jsonl:
+// M <= 32 -> 50, M <= 64 -> 52, above -> 53)
+hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t st) {
+  if (variant == 0) variant = a.M <= 32 ? 50 : (a.M <= 64 ? 52 : 53);
+  switch (variant) {
+    case 50: return launch_mid<2, 8, 2, 1>(a, tiled, st);
+    case 51: return launch_mid<2, 8, 1, 2>(a, tiled, st);
+    case 53: return launch_mid<2, 8, 4, 2>(a, tiled, st);
+    case 54: return launch_mid<2, 8, 1, 4>(a, tiled, st);
+    case 55: return launch_mid<2, 8, 2, 4>(a, tiled, st);
+    default: return launch_mid<2, 8, 2, 2>(a, tiled, st);
+  }
+}
+
+bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
+  return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || group % TK == 0);
+}
+
+// variants (flags bits 16..23 of iwq_w4a16_gemm, for A/B): 0 default = 45 (interleaved A/B on the
+// Llama-2-7B shapes at M = 8192, profiles/r02_ab_gemm_*.jsonl); per channel: 40 exact
+// (scale per element), 41 factored, 42 factored + interleave, 43 factored + setprio,
+// 44 exact + interleave, 45 early barrier factored, 46 early barrier exact, 47 / 48 the same on
+// 16x16x32, 49 = 41; grouped: 40, 41 and 49 plain, 42/43 interleave / setprio, 45 early barrier,
+// 47 16x16x32.
+hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st) {
+  if (a.gpr != 1) {
+    switch (variant) {
+      case 42: return launch<true, false, 1, false>(a, st);
+      case 43: return launch<true, false, 0, true>(a, st);
+      case 45: return launch_e<true, false>(a, st);
+      case 47: return launch_16e<true, false>(a, st);
+      case 49: return launch<true, false, 0, false>(a, st);
+      default: return launch_e<true, false>(a, st);
+    }
+  }
+  switch (variant) {
+    case 40: return launch<false, false, 0, false>(a, st);
+    case 42: return launch<false, true, 1, false>(a, st);
+    case 43: return launch<false, true, 0, true>(a, st);
+    case 44: return launch<false, false, 1, false>(a, st);
+    case 45: return launch_e<false, true>(a, st);
+    case 46: return launch_e<false, false>(a, st);
+    case 47: return launch_16e<false, true>(a, st);
+    case 48: return launch_16e<false, false>(a, st);
+    case 49: return launch<false, true, 0, false>(a, st);
+    default: return launch_e<false, true>(a, st);
+  }
+}
+
+}  // namespace iwq

@@ -317,6 +317,9 @@ def gemm_variant_flags(v: int) -> int:
 
 
 GEMV_MAX_M = 16  # iwq_w4a16_gemm takes the weight-streaming decode kernel up to this many rows
+# w4a16_linear keeps the fused kernel (decode GEMV, then the mid-M weight-streaming kernel) up to
+# this many rows; above, dequantize-once + hipBLASLt is faster (profiles/r02_gemm_sweep.jsonl)
+FUSED_MAX_M = 128
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
@@ -421,12 +424,13 @@ def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zer
                  n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None,
                  tiled_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
-    decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), dequant-once
-    + hipBLASLt (F.linear) above, where the library GEMM on a freshly dequantized weight beats the
-    fused MFMA kernel."""
+    decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), the mid-M
+    weight-streaming kernel up to FUSED_MAX_M rows, dequant-once + hipBLASLt (F.linear) above,
+    where the library GEMM on a freshly dequantized weight beats the fused kernels."""
     K = x.shape[-1]
-    if x.numel() // K <= GEMV_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
-        if tiled_codes is not None:
+    M = x.numel() // K
+    if M <= FUSED_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
+        if tiled_codes is not None and M <= GEMV_MAX_M:
             return w4a16_gemm(x, tiled_codes, scales, zeros, n_bits, group, N, bias, tiled=True)
         return w4a16_gemm(x, codes, scales, zeros, n_bits, group, N, bias)
     w = dequant_packed(codes, scales, zeros, n_bits, group, N, K)

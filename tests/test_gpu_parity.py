@@ -795,10 +795,13 @@ def test_w4a16_prefill_big_tile(K, M, sym, group):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
     err = (y.float() - ref).abs()
     assert bool((err <= tol).all()), float(err.max())
+    # variant 2: the round-1 k_w4a16_big (the default is iwq_prefill.hip since round 2)
+    y_big = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(2))
+    assert bool(((y_big.float() - ref).abs() <= tol).all())
     if group == -2:
-        for v in (24,):  # k-slice-outer: same BK, same accumulation order
+        for v in (24,):  # k-slice-outer: same BK, same accumulation order as k_w4a16_big
             yv = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
-            assert torch.equal(yv, y), v
+            assert torch.equal(yv, y_big), v
         y23 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(23))  # BK=128
         assert bool(((y23.float() - ref).abs() <= tol).all())
     y1 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(1))
@@ -813,3 +816,87 @@ def test_w4a16_prefill_big_identity(K):
     x = torch.eye(Kd, device=DEV, dtype=torch.float16)
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
+
+
+# prefill variants (iwq_prefill.hip) with identical bits within a set: per channel, scale per
+# element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape
+B32_SETS_PC = ((40, 44, 46), (41, 42, 43, 45), (47,), (48,))
+B32_SETS_G = ((40, 41, 42, 43, 45), (47,))
+B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
+
+
+@pytest.mark.parametrize("M", [300, 512, 1024])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("group", [-2, 128, 64])
+def test_w4a16_prefill_b32(K, M, sym, group):
+    """The 32x32x16 prefill kernel (iwq_prefill.hip, variants 40-44) vs an fp32 GEMM on the bit-exact
+    dequantized weight; variants that differ only in scheduling give identical bits."""
+    N, Kd = 512, 4352
+    torch.manual_seed(2)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 93)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    ys = {}
+    for v in B32_ALL:
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (v, float(err.max()))
+        ys[v] = y
+    for vs in (B32_SETS_PC if group == -2 else B32_SETS_G):
+        for v in vs[1:]:
+            assert torch.equal(ys[v], ys[vs[0]]), (vs[0], v)
+
+
+@pytest.mark.parametrize("group", [-2, 128])
+def test_w4a16_prefill_b32_identity(K, group):
+    """A = I through the 32x32x16 prefill kernel picks W_deq^T exactly for every variant (operand k
+    order, LDS swizzles, C layout; factored scale: s * (q - z) is exact in fp32)."""
+    N, Kd = 768, 512
+    w = (torch.arange(N * Kd, device=DEV, dtype=torch.float32).reshape(N, Kd) % 13 - 6).half()
+    w[:, 128:256] *= 0.25  # a different scale per group along k
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    x = torch.eye(Kd, device=DEV, dtype=torch.float16)
+    for v in B32_ALL:
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, r.out.t().contiguous()), v
+
+
+MID_VARIANTS = (50, 51, 52, 53, 54, 55)  # k_w4a16_mid: (MT row tiles, CT column tiles) shapes
+
+
+@pytest.mark.parametrize("M", [17, 40, 64, 100, 257])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("group", [-2, 128, 32])
+def test_w4a16_mid(K, M, sym, group):
+    """The mid-M weight-streaming kernel (iwq_prefill.hip k_w4a16_mid, variants 50-55; row tiles past
+    M) vs an fp32 GEMM on the bit-exact dequantized weight."""
+    N, Kd = 256, 2304
+    torch.manual_seed(3)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 95)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in MID_VARIANTS + (0,):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (v, float(err.max()))
+
+
+def test_w4a16_mid_identity(K):
+    """A = I (rows 0..M-1 of the identity) through every mid-M variant picks W_deq^T rows exactly."""
+    N, Kd = 256, 512
+    w = (torch.arange(N * Kd, device=DEV, dtype=torch.float32).reshape(N, Kd) % 13 - 6).half()
+    for group in (-2, 128):
+        r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+        for M in (48, 130):
+            x = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
+            for v in MID_VARIANTS:
+                y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
+                assert torch.equal(y, r.out.t()[:M].contiguous()), (group, M, v)

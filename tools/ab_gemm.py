@@ -1,0 +1,77 @@
+"""Interleaved A/B timing of prefill GEMM variants (iwq_w4a16_gemm flags variant) against the
+reference forward F.linear(x, W_deq) (hipBLASLt fp16): every round times each arm once (R calls
+back to back, HIP events), arms in rotating order, median over rounds (cdna_hip_programming.md
+§5.4 rule 24: same process, interleaved, after a clock ramp).  One JSON line per (shape, arm)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096, 11008),
+          "70b_q": (8192, 8192), "70b_gate": (28672, 8192), "70b_down": (8192, 28672)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--group", type=int, default=-2)
+    ap.add_argument("--variants", default="0,45,47")
+    ap.add_argument("--shapes", default="q_proj,gate_proj,down_proj")
+    ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--warm-seconds", type=float, default=2.0)
+    a = ap.parse_args()
+    from iron_weight_only_quant_amd import kernels
+    xw = torch.randn(8192, 4096, device="cuda").half()
+    ww = torch.randn(4096, 4096, device="cuda").half()
+    t_end = time.time() + a.warm_seconds
+    while time.time() < t_end:
+        for _ in range(20):
+            torch.nn.functional.linear(xw, ww)
+        torch.cuda.synchronize()
+    del xw, ww
+    for name in a.shapes.split(","):
+        N, K = SHAPES[name]
+        w = torch.empty(N, K, dtype=torch.float16, device="cuda")
+        kernels.fill_synthetic(w, 7)
+        r = kernels.quantize_minmax(w, 4, a.group, False, 0, want_codes=True)
+        x = (torch.randn(a.m, K, device="cuda") * 0.5).half()
+        y = torch.empty(a.m, N, dtype=torch.float16, device="cuda")
+        arms = {"hipblaslt": lambda: torch.nn.functional.linear(x, r.out)}
+        for v in [int(t) for t in a.variants.split(",")]:
+            fl = kernels.gemm_variant_flags(v)
+            arms[f"v{v}"] = (lambda fl=fl: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N,
+                                                              flags=fl, out=y))
+        for f in arms.values():
+            f()
+        torch.cuda.synchronize()
+        times = {k: [] for k in arms}
+        st = torch.cuda.current_stream()
+        keys = list(arms)
+        for rd in range(a.rounds):
+            order = keys[rd % len(keys):] + keys[:rd % len(keys)]
+            for k in order:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(a.reps):
+                    arms[k]()
+                e1.record(st)
+                torch.cuda.synchronize()
+                times[k].append(e0.elapsed_time(e1) / a.reps)
+        flops = 2.0 * a.m * N * K
+        for k in keys:
+            ts = sorted(times[k])
+            med = ts[len(ts) // 2]
+            print(json.dumps({"shape": name, "M": a.m, "N": N, "K": K, "group": a.group, "arm": k,
+                              "ms": round(med, 4), "ms_min": round(ts[0], 4), "tflops": round(flops / med / 1e9, 1)}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

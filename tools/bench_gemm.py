@@ -68,8 +68,19 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="0", help="decode-kernel variants to time for M <= 16 (IWQ_FLAG_VARIANT)")
     ap.add_argument("--shapes", default="q_proj,gate_proj,down_proj")
+    ap.add_argument("--warm-seconds", type=float, default=1.5,
+                    help="untimed MFMA load before the first measurement (clock ramp)")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels
+    import time
+    xw = torch.randn(8192, 4096, device="cuda").half()
+    ww = torch.randn(4096, 4096, device="cuda").half()
+    t_end = time.time() + a.warm_seconds
+    while time.time() < t_end:
+        for _ in range(20):
+            torch.nn.functional.linear(xw, ww)
+        torch.cuda.synchronize()
+    del xw, ww
     shapes = SHAPES + [("70b_gate", 28672, 8192), ("70b_down", 8192, 28672)]
     for name, N, K in [t for t in shapes if t[0] in a.shapes.split(",")]:
         w = torch.empty(N, K, dtype=torch.float16, device="cuda")

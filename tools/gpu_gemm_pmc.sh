@@ -1,0 +1,25 @@
+#!/bin/bash
+# Prefill GEMM diagnostics on one box: interleaved A/B timing, then PMC passes (one rocprofv3 run per
+# counter set, kernel trace for durations) for each arm on q_proj and down_proj.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
+VARS=${VARS:-0,45,47}
+timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" > "$OUT/ab_gemm_pc.jsonl" 2>&1 || exit $?
+timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" --group 128 > "$OUT/ab_gemm_g128.jsonl" 2>&1 || exit $?
+cd /tmp
+P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+P2="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
+for shape in "4096 4096" "4096 11008"; do
+  set -- $shape; N=$1; K=$2
+  for arm in ref $(echo $VARS | tr ',' ' '); do
+    if [ $arm = ref ]; then A="--ref"; else A="--variant $arm"; fi
+    for p in 1 2; do
+      eval C=\$P$p
+      D=$OUT/pmc_${N}x${K}_${arm}_p$p
+      timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $C --output-format csv -d $D -o run -- python3 $ROOT/tools/gemm_pmc.py --n $N --k $K $A > $D.log 2>&1 || { echo "pmc fail $D"; exit 3; }
+    done
+  done
+done
+cd $ROOT
+for D in $OUT/pmc_*_p1 $OUT/pmc_*_p2; do echo "== $D"; python3 tools/pmc_kernels.py $D; done > $OUT/pmc_gemm_summary.txt 2>&1
+echo ok
