@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--variants", default="", help="A/B: comma list of variants timed in interleaved rounds")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--inplace", action="store_true",
-                    help="write the dequantized weights over the inputs (QuantLinear / quantize_model semantics)")
+                    help="time the in-place form instead: dequantized weights over the inputs "
+                         "(QuantLinear.quantize_weight / quantize_model semantics, quant_linear.py:949)")
     ap.add_argument("--ramp-seconds", type=float, default=1.0,
                     help="untimed clock ramp before the copy-ceiling probe and the W warmup steps")
     ap.add_argument("--no-shapes", action="store_true",
@@ -242,8 +243,9 @@ def clock_ramp(plan, seconds):
 
 
 def copy_ceiling(plan, steps=5):
-    """In-run ceiling: a plain 16-B non-temporal copy of the same bytes (read w, write out), same grid
-    shape policy (probe variant 100).  Overwrites plan.outs; call before the timed warmup."""
+    """In-run ceiling: a plain 16-B non-temporal copy of the same bytes (read w, write out; in place:
+    w onto itself, which leaves the values unchanged), same grid shape policy (probe variant 100).
+    Overwrites plan.outs; call before the timed warmup."""
     stream = torch.cuda.current_stream()
     plan.run(stream, variant=100)
     torch.cuda.synchronize()
@@ -308,6 +310,37 @@ def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
     return out
 
 
+def other_placement_kernel(weights, plan, args, steps=10):
+    """The same launch in the other placement, HIP-event time on its stream, reported beside the
+    headline: in place (QuantLinear.quantize_weight writes the dequantized weight back into the weight
+    storage, quant_linear.py:949) when the headline is out of place, and vice versa.  Its inputs are
+    copies, so the headline plan's inputs are untouched.  Which placement is faster depends on the box
+    (DESIGN.md §5): the headline stays pseudo_quantize_tensor's default, out of place."""
+    from iron_weight_only_quant_amd import kernels
+    if args.inplace:
+        other = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
+    else:
+        copies = [w.clone() for w in weights]
+        other = kernels.BatchPlan(copies, args.bits, args.group, args.symmetric, outs=copies)
+    stream = torch.cuda.current_stream()
+    for _ in range(3):
+        other.run(stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        other.run(stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    numel = other.numel
+    alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
+    del other
+    torch.cuda.empty_cache()
+    return {"placement": "out-of-place" if args.inplace else "in-place", "kernel_ms": round(ms, 4),
+            "achieved_GBps": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / HBM_PEAK_GBS, 4)}
+
+
 def ab_variants(plan, variants, args):
     """Interleaved in-process A/B of kernel variants (cdna_hip_programming.md §5.4 rule 24)."""
     stream = torch.cuda.current_stream()
@@ -315,10 +348,10 @@ def ab_variants(plan, variants, args):
     torch.cuda.synchronize()
     ref = [o.clone() for o in plan.outs[:3]]
     times = {v: [] for v in variants}
-    for v in variants:  # warm + correctness vs variant 0 (probes >= 100 are not quantizers)
-        plan.run(stream, variant=v)
+    for v in variants:  # warm + correctness vs variant 0 (probes >= 100 are not quantizers; in place
+        plan.run(stream, variant=v)  # the inputs change every run, so only out of place compares)
         torch.cuda.synchronize()
-        if v < 100:
+        if v < 100 and not args.inplace:
             for o, r in zip(plan.outs[:3], ref):
                 assert torch.equal(o.view(torch.int16), r.view(torch.int16)), f"variant {v} differs"
     for _ in range(args.rounds):
@@ -334,7 +367,7 @@ def ab_variants(plan, variants, args):
     for v in variants:
         t = sorted(times[v])
         med = t[len(t) // 2]
-        nbytes = numel * (2 if v in (103, 104) else 4)
+        nbytes = numel * (2 if v in (103, 104) or 106 <= v <= 111 else 4)
         print(f"[ab] variant {v}: median {med:.4f} ms  min {t[0]:.4f} ms  -> {nbytes / med / 1e6:.1f} GB/s moved",
               file=sys.stderr, flush=True)
 
@@ -359,7 +392,7 @@ def main():
     if args.variants:
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
     clock_ramp(plan, args.ramp_seconds)
-    ceiling = copy_ceiling(plan) if not args.inplace else None  # the copy probe would clobber in-place inputs
+    ceiling = copy_ceiling(plan)
     for _ in range(args.warmup):
         plan.run(variant=args.variant)
     torch.cuda.synchronize()
@@ -380,6 +413,10 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
     wall_max = max_over_ranks(wall, ws_n)
     ms_per_step = wall_max / args.steps * 1e3
+
+    other = None
+    if not strong:
+        other = other_placement_kernel(weights, plan, args)
 
     shapes_rec = None
     if not args.no_shapes and not strong:
@@ -437,7 +474,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "k_group<f16,128,asym,batched>", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes, "in_run_copy_ceiling_GBps": ceiling},
+                         "alg_bytes_per_launch": alg_bytes, "in_run_copy_ceiling_GBps": ceiling,
+                         "other_placement": other},
             "shapes": shapes_rec,
             "cpu_baseline": cpu,
             "ppl_delta": None,

@@ -1208,7 +1208,7 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
-  } else if (((variant == 0 && M >= 512) || (variant >= 40 && variant < 50)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+  } else if (((variant == 0 && M >= 512) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 70)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel
     // scale factored into the epilogue); the round-1 k_w4a16_big below stays reachable as variant 2

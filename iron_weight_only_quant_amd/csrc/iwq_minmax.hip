@@ -927,6 +927,33 @@ hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st, int max_blocks_p
 // achievable HBM rate of a given access style on the box at hand.  Timing reference only.
 //   MODE 0: copy, nt load + nt store     MODE 1: copy, plain       MODE 2: copy, 4 x 16 B in flight/lane (nt)
 //   MODE 3: read only (xor-reduce)       MODE 4: write only (nt)
+//   k_probe_pol<POL, COPY>: write-only (COPY false) or nt-load copy (COPY true) with the store's
+//   cache policy POL: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 nt sc1, 5 sc0 sc1 nt (vector stores only).
+template <int POL>
+__device__ __forceinline__ void store_pol(IWQ_GLOBAL u32x4* p, u32x4 v) {
+  if constexpr (POL == 0) *p = v;
+  else if constexpr (POL == 1) __builtin_nontemporal_store(v, p);
+  else if constexpr (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+  else asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <int POL, bool COPY>
+__global__ __launch_bounds__(BLOCK) void k_probe_pol(const iwq_batch_entry* entries, int32_t n) {
+  for (int32_t i = 0; i < n; ++i) {
+    const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(entries);
+    const int64_t nvec = tab[i].rows * tab[i].cols / 8;
+    const IWQ_GLOBAL u32x4* src = gp<u32x4>(tab[i].w);
+    IWQ_GLOBAL u32x4* dst = gp<u32x4>(tab[i].out_deq);
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t j = (int64_t)blockIdx.x * BLOCK + threadIdx.x; j < nvec; j += stride) {
+      if constexpr (COPY) store_pol<POL>(dst + j, __builtin_nontemporal_load(src + j));
+      else store_pol<POL>(dst + j, (u32x4){(uint32_t)j, 0u, 0u, 0u});
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int MODE>
 __global__ __launch_bounds__(BLOCK) void k_probe(const iwq_batch_entry* entries, int32_t n, uint32_t* sink) {
   uint32_t acc = 0;
@@ -974,12 +1001,22 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 10: return launch_variant_t<4, false, true, true>(a, st, 6);           // default kernel, 6 waves/SIMD
     case 11: return launch_variant_t<4, false, true, true>(a, st, 4);           // default kernel, 4 waves/SIMD
     case 12: return launch_variant_t<4, false, true, true>(a, st, 8);           // default kernel (same as 0)
+    case 13: return launch_variant_t<4, false, true, false>(a, st);             // default walk, plain stores
+    case 14: return launch_variant_t<4, false, false, false>(a, st);            // plain loads + plain stores
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 103: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 104: hipLaunchKernelGGL(k_probe<4>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 105: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 32)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+#define IWQ_PROBE_POL(V, POL, COPY)                                                                  \
+  case V: hipLaunchKernelGGL((k_probe_pol<POL, COPY>), dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, \
+                             a.entries, a.n_entries); return hipGetLastError();
+    IWQ_PROBE_POL(106, 0, false) IWQ_PROBE_POL(107, 1, false) IWQ_PROBE_POL(108, 2, false)
+    IWQ_PROBE_POL(109, 3, false) IWQ_PROBE_POL(110, 4, false) IWQ_PROBE_POL(111, 5, false)
+    IWQ_PROBE_POL(112, 0, true) IWQ_PROBE_POL(113, 1, true) IWQ_PROBE_POL(114, 2, true)
+    IWQ_PROBE_POL(115, 3, true) IWQ_PROBE_POL(116, 4, true) IWQ_PROBE_POL(117, 5, true)
+#undef IWQ_PROBE_POL
   }
   return hipErrorInvalidValue;
 }

@@ -91,6 +91,27 @@ __device__ __forceinline__ h8 dq8(uint32_t w, h2 zz, h2 s, uint32_t mask_s, uint
   return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
 }
 
+// NIB layout (iwq_prefill.hip variant 66; codes repacked so that nibble p of a code dword holds
+// k = (0, 2, 4, 6, 1, 3, 5, 7)[p]): two and-or per dword half give (1024 + k0, 1024 + k1) and
+// (64 + k2, 64 + k3) (nibble at mantissa bits 4-7 under exponent 64: unit 1/16 x 16), one shift
+// for the upper half -- 9 VALU per 8 weights in natural k order instead of 12.
+template <bool SCALE>
+__device__ __forceinline__ h8 dq8n(uint32_t w, h2 zl, h2 zh, h2 s, uint32_t m0_s, uint32_t m1_s, uint32_t mg64,
+                                   uint32_t mg54) {
+  const uint32_t t = w >> 8;
+  h2 d0 = as_h2(and_or(w, m0_s, mg64)) - zl;
+  h2 d1 = as_h2(and_or(w, m1_s, mg54)) - zh;
+  h2 d2 = as_h2(and_or(t, m0_s, mg64)) - zl;
+  h2 d3 = as_h2(and_or(t, m1_s, mg54)) - zh;
+  if constexpr (SCALE) {
+    d0 = d0 * s;
+    d1 = d1 * s;
+    d2 = d2 * s;
+    d3 = d3 * s;
+  }
+  return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
+}
+
 // SCHED 0: compiler schedule; 1: slice s+1's dequant interleaved with slice s's MFMAs
 // (sched_group_barrier, 1 MFMA : 3 VALU); PRIO: s_setprio(1) over each slice's MFMAs.
 template <bool GROUPED, bool FACTOR, int SCHED, bool PRIO>
@@ -252,8 +273,11 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32(PrefillArgs a) {
 // K-step start.  Same k order, same accumulation order: bit-identical to k_w4a16_b32.
 // WAR: a wave's last reads of stage kt (slice 3's A fragments) are retired (lgkmcnt(0)) before the
 // barrier after which stage kt is refilled.
-template <bool GROUPED, bool FACTOR>
+template <bool GROUPED, bool FACTOR, int WM, bool PHI = false, bool NIB = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
+  // WM waves along M x WN along N; a wave owns (TM / WM) x (TN / WN) = MTL x NTL tiles of 32 x 32
+  constexpr int WN = 8 / WM, MTL = TM / WM / 32, NTL = TN / WN / 32;
+  static_assert(WM * WN == 8 && MTL * NTL == 8, "8 waves, 8 MFMA tiles per wave");
   static_assert(!(GROUPED && FACTOR), "grouped scales change along k: no factoring");
   constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
   constexpr int PER_STAGE = 4 + 1 + (GROUPED ? 1 : 0);
@@ -262,7 +286,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WN, wn = wid % WN;
   const int r32 = lane & 31, h = lane >> 5;
   const int tiles_n = a.N / TN;
   const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
@@ -292,64 +316,82 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
     if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
   };
 
-  h2 sv[2], zz[2];
-  float sf[2] = {1.0f, 1.0f};
+  h2 sv[NTL], zz[NTL], zl[NTL], zh[NTL];
+  float sf[NTL];
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) sf[nt] = 1.0f;
   if constexpr (!GROUPED) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int col = n0 + wn * 64 + nt * 32 + r32;
+    for (int nt = 0; nt < NTL; ++nt) {
+      const int col = n0 + wn * (32 * NTL) + nt * 32 + r32;
       const _Float16 sc = gp<_Float16>(a.scales)[col];
       const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
       sv[nt] = h2{sc, sc};
       sf[nt] = (float)sc;
       zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+      zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
     }
   }
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
-  uint32_t magic_v;
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
   asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+#define IWQ_DQ(W, NT)                                                                             \
+  (NIB ? dq8n<SCALE>((W), zl[NT], zh[NT], sv[NT], m0_s, m1_s, mg64, mg54)                         \
+       : dq8<SCALE>((W), zz[NT], sv[NT], mask_s, magic_v))
 
   // stage-local reads: grouped parameters, the codes of both 32-column tiles, one A slice
   auto read_params = [&](const uint8_t* xs) {
     if constexpr (GROUPED) {
       const uint32_t* ps = reinterpret_cast<const uint32_t*>(xs + XS + CS);
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = wn * 64 + nt * 32 + r32;
+      for (int nt = 0; nt < NTL; ++nt) {
+        const int col = wn * (32 * NTL) + nt * 32 + r32;
         const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
         const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[TN + col]) : a.zsym;
         sv[nt] = h2{sc, sc};
         zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+        zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+        zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
       }
     }
   };
-  auto read_codes = [&](const uint8_t* xs, u32x4 (&wc)[2]) {
+  auto read_codes = [&](const uint8_t* xs, u32x4 (&wc)[NTL]) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int col = wn * 64 + nt * 32 + r32;
+    for (int nt = 0; nt < NTL; ++nt) {
+      const int col = wn * (32 * NTL) + nt * 32 + r32;
       wc[nt] = *reinterpret_cast<const u32x4*>(xs + XS + col * 32 + ((h ^ cswz(col)) << 4));
     }
   };
-  auto read_a = [&](const uint8_t* xs, int s, h8 (&af)[4]) {
+  auto read_a = [&](const uint8_t* xs, int s, h8 (&af)[MTL]) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int row = wm * 128 + mt * 32 + r32;
+    for (int mt = 0; mt < MTL; ++mt) {
+      const int row = wm * (32 * MTL) + mt * 32 + r32;
       af[mt] = *reinterpret_cast<const h8*>(xs + row * 128 + (((4 * h + s) ^ xswz(row)) << 4));
     }
   };
 
-  f16x acc[4][2];
+  f16x acc[MTL][NTL];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MTL; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NTL; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 #define IWQ_MFMA_SLICE(AF, B0)                                                                   \
-  _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                \
-  _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                \
+  _Pragma("unroll") for (int mt = 0; mt < MTL; ++mt)                                              \
+  _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt)                                              \
     acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AF[mt], B0[nt], acc[mt][nt], 0, 0, 0);
 
+  // PHI: static priority 1 for the second-dispatched half (waves 4-7, the VALU-arbitration loser;
+  // cdna_hip_programming.md T5 static form)
+  if constexpr (PHI) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   issue(0, 0);
   if (nk > 1) {
     issue(1, 1);
@@ -360,24 +402,24 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   }
   __builtin_amdgcn_s_barrier();
   if (nk > 2) issue(2, 2);
-  u32x4 wc[2];
-  h8 af[4], bcur[2];
+  u32x4 wc[NTL];
+  h8 af[MTL], bcur[NTL];
   read_params(smem);
   read_codes(smem, wc);
   read_a(smem, 0, af);
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) bcur[nt] = dq8<SCALE>(wc[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+  for (int nt = 0; nt < NTL; ++nt) bcur[nt] = IWQ_DQ(wc[nt][0], nt);
 
   // slices 0..2 of the stage at xs: each slice's MFMAs behind the next slice's reads + dequant
 #define IWQ_SLICES_012(XS)                                                                        \
   _Pragma("unroll") for (int s = 0; s < 3; ++s) {                                                 \
-    h8 an[4], bn[2];                                                                              \
+    h8 an[MTL], bn[NTL];                                                                          \
     read_a(XS, s + 1, an);                                                                        \
-    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                              \
-      bn[nt] = dq8<SCALE>(wc[nt][s + 1], zz[nt], sv[nt], mask_s, magic_v);                        \
+    _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt)                                            \
+      bn[nt] = IWQ_DQ(wc[nt][s + 1], nt);                        \
     IWQ_MFMA_SLICE(af, bcur)                                                                      \
-    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) af[mt] = an[mt];                            \
-    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt) bcur[nt] = bn[nt];                          \
+    _Pragma("unroll") for (int mt = 0; mt < MTL; ++mt) af[mt] = an[mt];                          \
+    _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt) bcur[nt] = bn[nt];                        \
   }
   // the last K-step is peeled: no branch between the barrier and slice 3 inside the loop
   for (int kt = 0; kt + 1 < nk; ++kt) {
@@ -393,18 +435,18 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
     __builtin_amdgcn_s_barrier();
     if (kt + 3 < nk) issue(kt + 3, kt % NSTAGE);
     const uint8_t* xn = smem + ((kt + 1) % NSTAGE) * STAGE;
-    h8 an[4], bn[2];
-    u32x4 wn2[2];
+    h8 an[MTL], bn[NTL];
+    u32x4 wn2[NTL];
     read_params(xn);
     read_codes(xn, wn2);
     read_a(xn, 0, an);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) bn[nt] = dq8<SCALE>(wn2[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+    for (int nt = 0; nt < NTL; ++nt) bn[nt] = IWQ_DQ(wn2[nt][0], nt);
     IWQ_MFMA_SLICE(af, bcur)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) af[mt] = an[mt];
+    for (int mt = 0; mt < MTL; ++mt) af[mt] = an[mt];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTL; ++nt) {
       bcur[nt] = bn[nt];
       wc[nt] = wn2[nt];
     }
@@ -417,11 +459,236 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
 #undef IWQ_SLICES_012
 
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int col = n0 + wn * 64 + nt * 32 + r32;
+  for (int nt = 0; nt < NTL; ++nt) {
+    const int col = n0 + wn * (32 * NTL) + nt * 32 + r32;
     const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < MTL; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (32 * MTL) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+#undef IWQ_DQ
+#undef IWQ_MFMA_SLICE
+
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_w4e: the same 256 x 256 tile on FOUR waves (one per SIMD), 128 x 128 per wave = 4 x 4
+// MFMA tiles of 32 x 32, the 256 fp32 accumulators in AGPRs (amdgpu_waves_per_eu(1, 1): 512
+// registers per lane).  Against the 8-wave form: every dequantized B fragment and every A
+// fragment feeds 4 MFMAs (2 and 4 there), so the LDS A reads per MFMA halve and no two waves of a
+// SIMD compete for its issue port; the operand prefetch (next slice's A reads + dequant behind the
+// current slice's 16 MFMAs = 512 cycles) must hide the LDS latency on its own.  Same LDS images,
+// k order, early barrier and stage ring as k_w4a16_b32e; per stage a wave issues 8 X pieces, 2 code
+// pieces (+ 2 parameter pieces grouped).
+// ---------------------------------------------------------------------------------------------
+// SG: pin the interleave with sched_group_barrier (hipcc otherwise issues each A read right before
+// its MFMAs and waits on it: ds_read -> lgkmcnt(0) -> MFMA, the LDS latency on the critical path):
+// per slice, the next slice's 4 A reads first, then 16 x {1 MFMA, 3 VALU of the next slice's
+// dequant}; after the barrier, the next stage's code/A reads, 4 bare MFMAs (cover the code read),
+// then 12 x {1 MFMA, 4 VALU}.
+template <bool GROUPED, bool FACTOR, bool SG = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_w4a16_w4e(PrefillArgs a) {
+  static_assert(!(GROUPED && FACTOR), "grouped scales change along k: no factoring");
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PER_STAGE = 8 + 2 + (GROUPED ? 2 : 0);
+  constexpr bool SCALE = !FACTOR;
+  constexpr int MTL = 4, NTL = 4;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  // X: slot 8 wid + i = rows 8 (8 wid + i) + [0, 8); lane = 8 (row % 8) + physical chunk.  Rows
+  // 8 (8 wid + i) + lane / 8 = 64 wid + 8 i + lane / 8: one base pointer + i * 8 rows.
+  const int xrow0 = wid * 64 + (lane >> 3);
+  const int xgm0 = m0 + xrow0;
+  const _Float16* xsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = xrow0 + 8 * i;
+    const int gm = xgm0 + 8 * i < a.M ? xgm0 + 8 * i : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  // codes: slots 2 wid, 2 wid + 1 = columns 64 wid + [0, 64)
+  const uint8_t* csrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ccol = (2 * wid + i) * 32 + (lane >> 1);
+    csrc[i] = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  }
+  const _Float16* psrc_s = nullptr;
+  const _Float16* psrc_z = nullptr;
+  if constexpr (GROUPED) {
+    psrc_s = a.scales + (int64_t)(n0 + wid * 64 + lane) * a.gpr;
+    psrc_z = (a.zeros ? a.zeros : a.scales) + (int64_t)(n0 + wid * 64 + lane) * a.gpr;
+  }
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 8 + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(csrc[i] + kt * (TK / 2), base + XS + (wid * 2 + i) * 1024);
+    if constexpr (GROUPED) {
+      glds2(psrc_s + (kt * TK) / a.group, base + XS + CS + wid * 256);
+      glds2(psrc_z + (kt * TK) / a.group, base + XS + CS + (4 + wid) * 256);
+    }
+  };
+
+  h2 sv[NTL], zz[NTL];
+  float sf[NTL];
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) sf[nt] = 1.0f;
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+      const int col = n0 + wn * 128 + nt * 32 + r32;
+      const _Float16 sc = gp<_Float16>(a.scales)[col];
+      const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+      sv[nt] = h2{sc, sc};
+      sf[nt] = (float)sc;
+      zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    }
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  auto read_params = [&](const uint8_t* xs) {
+    if constexpr (GROUPED) {
+      const uint32_t* ps = reinterpret_cast<const uint32_t*>(xs + XS + CS);
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt) {
+        const int col = wn * 128 + nt * 32 + r32;
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)ps[col]);
+        const float zf = a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)ps[TN + col]) : a.zsym;
+        sv[nt] = h2{sc, sc};
+        zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+      }
+    }
+  };
+  auto read_codes = [&](const uint8_t* xs, u32x4 (&wc)[NTL]) {
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+      const int col = wn * 128 + nt * 32 + r32;
+      wc[nt] = *reinterpret_cast<const u32x4*>(xs + XS + col * 32 + ((h ^ cswz(col)) << 4));
+    }
+  };
+  auto read_a = [&](const uint8_t* xs, int s, h8 (&af)[MTL]) {
+#pragma unroll
+    for (int mt = 0; mt < MTL; ++mt) {
+      const int row = wm * 128 + mt * 32 + r32;
+      af[mt] = *reinterpret_cast<const h8*>(xs + row * 128 + (((4 * h + s) ^ xswz(row)) << 4));
+    }
+  };
+
+  f16x acc[MTL][NTL];
+#pragma unroll
+  for (int i = 0; i < MTL; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+#define IWQ_MFMA_SLICE4(AF, B0)                                                                  \
+  _Pragma("unroll") for (int mt = 0; mt < MTL; ++mt)                                              \
+  _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt)                                              \
+    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AF[mt], B0[nt], acc[mt][nt], 0, 0, 0);
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (nk > 2) issue(2, 2);
+  u32x4 wc[NTL];
+  h8 af[MTL], bcur[NTL];
+  read_params(smem);
+  read_codes(smem, wc);
+  read_a(smem, 0, af);
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) bcur[nt] = dq8<SCALE>(wc[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+
+#define IWQ_SLICES4_012(XS)                                                                       \
+  _Pragma("unroll") for (int s = 0; s < 3; ++s) {                                                 \
+    h8 an[MTL], bn[NTL];                                                                          \
+    read_a(XS, s + 1, an);                                                                        \
+    _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt)                                            \
+      bn[nt] = dq8<SCALE>(wc[nt][s + 1], zz[nt], sv[nt], mask_s, magic_v);                        \
+    IWQ_MFMA_SLICE4(af, bcur)                                                                     \
+    if constexpr (SG) {                                                                           \
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                          \
+      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                            \
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                                        \
+      }                                                                                           \
+      __builtin_amdgcn_sched_barrier(0);                                                          \
+    }                                                                                             \
+    _Pragma("unroll") for (int mt = 0; mt < MTL; ++mt) af[mt] = an[mt];                          \
+    _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt) bcur[nt] = bn[nt];                        \
+  }
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint8_t* xs = smem + (kt % NSTAGE) * STAGE;
+    IWQ_SLICES4_012(xs)
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_STAGE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 3 < nk) issue(kt + 3, kt % NSTAGE);
+    const uint8_t* xn = smem + ((kt + 1) % NSTAGE) * STAGE;
+    h8 an[MTL], bn[NTL];
+    u32x4 wn2[NTL];
+    read_params(xn);
+    read_codes(xn, wn2);
+    read_a(xn, 0, an);
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) bn[nt] = dq8<SCALE>(wn2[nt][0], zz[nt], sv[nt], mask_s, magic_v);
+    IWQ_MFMA_SLICE4(af, bcur)
+    if constexpr (SG) {
+      __builtin_amdgcn_sched_group_barrier(0x100, GROUPED ? 16 : 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MTL; ++mt) af[mt] = an[mt];
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+      bcur[nt] = bn[nt];
+      wc[nt] = wn2[nt];
+    }
+  }
+  {
+    const uint8_t* xs = smem + ((nk - 1) % NSTAGE) * STAGE;
+    IWQ_SLICES4_012(xs)
+    IWQ_MFMA_SLICE4(af, bcur)
+  }
+#undef IWQ_SLICES4_012
+#undef IWQ_MFMA_SLICE4
+
+#pragma unroll
+  for (int nt = 0; nt < NTL; ++nt) {
+    const int col = n0 + wn * 128 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < MTL; ++mt) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -432,12 +699,17 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   }
 }
 
-#undef IWQ_MFMA_SLICE
+template <bool GROUPED, bool FACTOR, bool SG = false>
+hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_w4e<GROUPED, FACTOR, SG>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
 
-template <bool GROUPED, bool FACTOR>
+template <bool GROUPED, bool FACTOR, int WM = 2, bool PHI = false, bool NIB = false>
 hipError_t launch_e(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
-  hipLaunchKernelGGL((k_w4a16_b32e<GROUPED, FACTOR>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  hipLaunchKernelGGL((k_w4a16_b32e<GROUPED, FACTOR, WM, PHI, NIB>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
   return hipGetLastError();
 }
 
@@ -835,6 +1107,11 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
       case 45: return launch_e<true, false>(a, st);
       case 47: return launch_16e<true, false>(a, st);
       case 49: return launch<true, false, 0, false>(a, st);
+      case 60: return launch_e<true, false, 4>(a, st);
+      case 62: return launch_e<true, false, 2, true>(a, st);
+      case 63: return launch_w4<true, false>(a, st);
+      case 65: return launch_w4<true, false, true>(a, st);
+      case 66: return launch_e<true, false, 2, false, true>(a, st);
       default: return launch_e<true, false>(a, st);
     }
   }
@@ -848,6 +1125,14 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 47: return launch_16e<false, true>(a, st);
     case 48: return launch_16e<false, false>(a, st);
     case 49: return launch<false, true, 0, false>(a, st);
+    case 60: return launch_e<false, true, 4>(a, st);
+    case 61: return launch_e<false, false, 4>(a, st);
+    case 62: return launch_e<false, true, 2, true>(a, st);
+    case 63: return launch_w4<false, true>(a, st);
+    case 64: return launch_w4<false, false>(a, st);
+    case 65: return launch_w4<false, true, true>(a, st);
+    case 66: return launch_e<false, true, 2, false, true>(a, st);   // codes in the NIB layout
+    case 67: return launch_e<false, false, 2, false, true>(a, st);  // NIB, exact
     default: return launch_e<false, true>(a, st);
   }
 }

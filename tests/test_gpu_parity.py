@@ -819,10 +819,25 @@ def test_w4a16_prefill_big_identity(K):
 
 
 # prefill variants (iwq_prefill.hip) with identical bits within a set: per channel, scale per
-# element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape
-B32_SETS_PC = ((40, 44, 46), (41, 42, 43, 45), (47,), (48,))
-B32_SETS_G = ((40, 41, 42, 43, 45), (47,))
+# element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
+# The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
+# neither the k order nor the accumulation order, so those join the 32x32x16 sets.
+B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65), (47,), (48,))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
+
+
+def nib_layout(codes, N, K):
+    """Row-major codes -> the NIB layout of prefill variants 66/67 (tools/ab_gemm.py)."""
+    c = codes.view(N, K // 8, 4)
+    lo, hi = c & 0xF, c >> 4
+    out = torch.stack([lo[..., 0] | (lo[..., 1] << 4), lo[..., 2] | (lo[..., 3] << 4),
+                       hi[..., 0] | (hi[..., 1] << 4), hi[..., 2] | (hi[..., 3] << 4)], dim=-1)
+    return out.reshape(N, K // 2).contiguous()
+
+
+# NIB-layout variants: same k order and accumulation order as their row-major twins
+B32_NIB = {66: 45, 67: 46}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -849,6 +864,12 @@ def test_w4a16_prefill_b32(K, M, sym, group):
     for vs in (B32_SETS_PC if group == -2 else B32_SETS_G):
         for v in vs[1:]:
             assert torch.equal(ys[v], ys[vs[0]]), (vs[0], v)
+    nib = nib_layout(r.codes, N, Kd)
+    for v, twin in B32_NIB.items():
+        if group != -2 and v == 67:
+            continue  # grouped: one exact kernel, variant 66
+        y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
 
 
 @pytest.mark.parametrize("group", [-2, 128])

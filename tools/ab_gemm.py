@@ -17,6 +17,19 @@ SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096
           "70b_q": (8192, 8192), "70b_gate": (28672, 8192), "70b_down": (8192, 28672)}
 
 
+def nib_layout(codes, N, K):
+    """Row-major packed codes -> the NIB layout of prefill variants 66/67 (nibble p of each code dword
+    holds k = (0, 2, 4, 6, 1, 3, 5, 7)[p]); A/B and tests only."""
+    c = codes.view(N, K // 8, 4)
+    lo, hi = c & 0xF, c >> 4
+    out = torch.stack([lo[..., 0] | (lo[..., 1] << 4), lo[..., 2] | (lo[..., 3] << 4),
+                       hi[..., 0] | (hi[..., 1] << 4), hi[..., 2] | (hi[..., 3] << 4)], dim=-1)
+    return out.reshape(N, K // 2).contiguous()
+
+
+NIB_VARIANTS = (66, 67)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=8192)
@@ -44,10 +57,12 @@ def main():
         x = (torch.randn(a.m, K, device="cuda") * 0.5).half()
         y = torch.empty(a.m, N, dtype=torch.float16, device="cuda")
         arms = {"hipblaslt": lambda: torch.nn.functional.linear(x, r.out)}
+        nib = nib_layout(r.codes, N, K)
         for v in [int(t) for t in a.variants.split(",")]:
             fl = kernels.gemm_variant_flags(v)
-            arms[f"v{v}"] = (lambda fl=fl: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N,
-                                                              flags=fl, out=y))
+            cd = nib if v in NIB_VARIANTS else r.codes
+            arms[f"v{v}"] = (lambda fl=fl, cd=cd: kernels.w4a16_gemm(x, cd, r.scales, r.zeros, 4, a.group, N,
+                                                                     flags=fl, out=y))
         for f in arms.values():
             f()
         torch.cuda.synchronize()
