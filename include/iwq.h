@@ -224,6 +224,20 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
                    unsigned flags, void* stream);
 
 /*
+ * iwq_w4a16_gemm with a caller-provided fp32 workspace (16-B aligned).  For M >= 256 where the
+ * prefill kernel's 256 x 256 output tiles leave CUs idle (a time model picks S, see
+ * iwq_prefill.hip prefill_splitk_count), K is split into S ranges: each
+ * workgroup writes its fp32 partial tile to the workspace and a second kernel sums the S partials in
+ * range order (deterministic) and applies scale / bias -- within the fp16 output tolerance of the
+ * unsplit kernel, not bit-identical to it.  A NULL or too small workspace runs iwq_w4a16_gemm.
+ * iwq_w4a16_gemm_workspace_bytes: the size that enables the split for this problem (0: none needed).
+ */
+int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group);
+int iwq_w4a16_gemm_ws(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                      const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
+                      void* workspace, int64_t workspace_bytes, unsigned flags, void* stream);
+
+/*
  * Row-major packed 4-bit codes [N, K/2] -> the decode tile layout read by iwq_w4a16_gemm with
  * IWQ_FLAG_TILED_CODES: for each 16-row tile t and 128-k step kt a contiguous 1 KiB block at
  * byte (t * K/128 + kt) * 1024, byte 16 l + i of it = row 16 t + (l % 16), code byte

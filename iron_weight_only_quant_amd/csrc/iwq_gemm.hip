@@ -1103,9 +1103,35 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
   return IWQ_OK;
 }
 
+int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
+  if (g <= 0 || K % g != 0 || M < 256 || !prefill_b32_supported(M, N, K, (int)(K / g), (int)g)) return 0;
+  return prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
+}
+
+static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                           const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y,
+                           int64_t ldy, void* workspace, int64_t workspace_bytes, unsigned flags, void* stream);
+
 int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
                    const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
                    unsigned flags, void* stream) {
+  return w4a16_gemm_impl(x, M, K, lda, codes, scales, zeros, n_bits, group, N, bias, y, ldy, nullptr, 0, flags,
+                         stream);
+}
+
+int iwq_w4a16_gemm_ws(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                      const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y, int64_t ldy,
+                      void* workspace, int64_t workspace_bytes, unsigned flags, void* stream) {
+  if (workspace_bytes < 0 || (workspace_bytes > 0 && !workspace)) return IWQ_ERR_ARG;
+  return w4a16_gemm_impl(x, M, K, lda, codes, scales, zeros, n_bits, group, N, bias, y, ldy, workspace,
+                         workspace_bytes, flags, stream);
+}
+
+static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, const void* codes, const void* scales,
+                           const void* zeros, int n_bits, int64_t group, int64_t N, const void* bias, void* y,
+                           int64_t ldy, void* workspace, int64_t workspace_bytes, unsigned flags, void* stream) {
   if (!x || !codes || !scales || !y) return IWQ_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldy < N) return IWQ_ERR_SHAPE;
   if (N % BN != 0 || K % BK != 0 || (lda % 8) != 0) return IWQ_ERR_SHAPE;
@@ -1198,9 +1224,13 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }
-  } else if (((variant == 0 && M < 512) || (variant >= 50 && variant < 60)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+  } else if (((variant == 0 && M < 512 && !(M >= 256 && workspace &&
+                                            prefill_b32_supported(M, N, K, a.gpr, a.group) &&
+                                            prefill_splitk_count(M, N, K, 0) > 1 &&
+                                            workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0)))) ||
+              (variant >= 50 && variant < 60)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              mid_supported(M, N, K, a.gpr, a.group)) {
-    // 16 < M < 512 default since round 2: the weight-streaming mid-M kernel (iwq_prefill.hip)
+    // 16 < M < 512 (M < 256, or no split-K workspace): the weight-streaming mid-M kernel
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     const hipError_t e = mid_launch(p, (int)variant, false, st);
     if (e != hipSuccess) {
@@ -1208,12 +1238,23 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
-  } else if (((variant == 0 && M >= 512) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 70)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+  } else if (((variant == 0 && M >= 256) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 70) ||
+              (variant > 81 && variant < 96)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel
-    // scale factored into the epilogue); the round-1 k_w4a16_big below stays reachable as variant 2
+    // scale factored into the epilogue); the round-1 k_w4a16_big below stays reachable as variant 2.
+    // With a workspace and fewer 256 x 256 tiles than CUs it splits K (variant 80 + S forces S ranges).
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
-    const hipError_t e = prefill_b32_launch(p, (int)variant, st);
+    hipError_t e;
+    const int nsplit = (variant == 0 || variant > 81) ? prefill_splitk_count(M, N, K, variant > 81 ? (int)variant - 80 : 0) : 1;
+    if (nsplit > 1 && workspace && workspace_bytes >= prefill_splitk_bytes(M, N, nsplit)) {
+      p.ws = static_cast<float*>(workspace);
+      p.nsplit = nsplit;
+      e = prefill_splitk_launch(p, st);
+    } else {
+      if (variant > 81) return IWQ_ERR_WORKSPACE;
+      e = prefill_b32_launch(p, (int)variant, st);
+    }
     if (e != hipSuccess) {
       iwq::last_hip_error() = (int)e;
       return IWQ_ERR_HIP;

@@ -20,6 +20,9 @@ struct PrefillArgs {
   int gpr;                 // scale groups per row (K / group)
   int group;               // group length along K
   float zsym;              // symmetric code offset 2^(b-1)
+  float* ws = nullptr;     // split-K: fp32 partial tiles (prefill_splitk_bytes), else unused
+  int nsplit = 1;          // split-K: number of K ranges
+  int kps = 0;             // split-K: 64-k steps per range
 };
 
 // mid-size M (k_w4a16_mid): N % 64 == 0, K % 128 == 0, per-channel or group % 32 == 0; codes
@@ -31,5 +34,12 @@ hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t
 bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);
 // variant: 0 = default; A/B variants documented at the dispatch in iwq_prefill.hip
 hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st);
+
+// split-K form of the prefill kernel for M where the 256 x 256 tiles leave CUs idle: number of K
+// ranges for the problem (1 = no split; force > 1 overrides the rule), the fp32 workspace it needs,
+// and the launch (partial tiles to a.ws, then one reduce kernel: fixed split order, deterministic)
+int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force);
+int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit);
+hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st);
 
 }  // namespace iwq

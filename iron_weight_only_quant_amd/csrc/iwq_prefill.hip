@@ -258,7 +258,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32(PrefillArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        const float v = FACTOR ? opaque(acc[mt][nt][r] * sf[nt]) : acc[mt][nt][r];  // no fma_mix fold
         if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
       }
     }
@@ -273,7 +273,16 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32(PrefillArgs a) {
 // K-step start.  Same k order, same accumulation order: bit-identical to k_w4a16_b32.
 // WAR: a wave's last reads of stage kt (slice 3's A fragments) are retired (lgkmcnt(0)) before the
 // barrier after which stage kt is refilled.
-template <bool GROUPED, bool FACTOR, int WM, bool PHI = false, bool NIB = false>
+// SWAP: the weight fragment is the MFMA's A operand and X's the B operand, so the accumulator holds
+// C^T: a lane owns one output row m and, per register quad, 4 consecutive columns n -- the epilogue
+// stores 8 B per instruction (4 per 32 x 32 tile) instead of 2 B (16 per tile).  The two operand
+// layouts of the 32x32x16 MFMA are the same, so the swap costs nothing in the loop.
+// SPLIT: the workgroup's tile and K range come from blockIdx = split * tiles + tile (adjacent tiles of
+// one K range share an XCD: the same X rows and K range); the raw fp32 accumulators go to
+// a.ws[(tile * nsplit + split)][wave][mt, nt][reg][lane] (256-B coalesced stores) for
+// k_splitk_reduce, which applies the epilogue.
+template <bool GROUPED, bool FACTOR, int WM, bool PHI = false, bool NIB = false, bool SWAP = false,
+          bool SPLIT = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   // WM waves along M x WN along N; a wave owns (TM / WM) x (TN / WN) = MTL x NTL tiles of 32 x 32
   constexpr int WN = 8 / WM, MTL = TM / WM / 32, NTL = TN / WN / 32;
@@ -289,9 +298,19 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   const int wm = wid / WN, wn = wid % WN;
   const int r32 = lane & 31, h = lane >> 5;
   const int tiles_n = a.N / TN;
-  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  int64_t t;
+  int kbase = 0, nk = a.K / TK, split = 0;
+  if constexpr (SPLIT) {
+    const int64_t tiles = (int64_t)gridDim.x / a.nsplit;
+    const int64_t b = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+    split = (int)(b / tiles);
+    t = b - (int64_t)split * tiles;
+    kbase = split * a.kps;
+    nk = min(a.kps, nk - kbase);  // >= 1 by construction (prefill_splitk_count)
+  } else {
+    t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  }
   const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
-  const int nk = a.K / TK;
   const int64_t crow = a.K / 2;
 
   const _Float16* xsrc[4];
@@ -299,10 +318,10 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int row = (wid * 4 + i) * 8 + (lane >> 3);
     const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
-    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+    xsrc[i] = a.x + (int64_t)gm * a.lda + kbase * TK + (((lane & 7) ^ xswz(row)) << 3);
   }
   const int ccol = wid * 32 + (lane >> 1);
-  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + kbase * (TK / 2) + (((lane & 1) ^ cswz(ccol)) << 4);
   const _Float16* psrc = nullptr;
   if constexpr (GROUPED) {
     const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
@@ -313,7 +332,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+    if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
   };
 
   h2 sv[NTL], zz[NTL], zl[NTL], zh[NTL];
@@ -385,7 +404,8 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
 #define IWQ_MFMA_SLICE(AF, B0)                                                                   \
   _Pragma("unroll") for (int mt = 0; mt < MTL; ++mt)                                              \
   _Pragma("unroll") for (int nt = 0; nt < NTL; ++nt)                                              \
-    acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AF[mt], B0[nt], acc[mt][nt], 0, 0, 0);
+    acc[mt][nt] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x16_f16(B0[nt], AF[mt], acc[mt][nt], 0, 0, 0) \
+                       : __builtin_amdgcn_mfma_f32_32x32x16_f16(AF[mt], B0[nt], acc[mt][nt], 0, 0, 0);
 
   // PHI: static priority 1 for the second-dispatched half (waves 4-7, the VALU-arbitration loser;
   // cdna_hip_programming.md T5 static form)
@@ -458,6 +478,40 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
   }
 #undef IWQ_SLICES_012
 
+  if constexpr (SPLIT) {
+    float* dst = a.ws + ((t * a.nsplit + split) * 8 + wid) * 8192 + lane;
+#pragma unroll
+    for (int mt = 0; mt < MTL; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NTL; ++nt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gp<float>(dst)[((mt * NTL + nt) * 16 + r) * 64] = acc[mt][nt][r];
+  } else if constexpr (SWAP) {
+    // C^T layout: row m = lane & 31 of the tile, columns n = (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+    for (int nt = 0; nt < NTL; ++nt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = n0 + wn * (32 * NTL) + nt * 32 + 8 * g + 4 * h;
+        float sc[4], bb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sc[j] = FACTOR ? (float)gp<_Float16>(a.scales)[col + j] : 1.0f;
+          bb[j] = a.bias ? (float)gp<_Float16>(a.bias)[col + j] : 0.0f;
+        }
+#pragma unroll
+        for (int mt = 0; mt < MTL; ++mt) {
+          const int row = m0 + wm * (32 * MTL) + mt * 32 + r32;
+          h2 lo = h2{(_Float16)(opaque(acc[mt][nt][4 * g + 0] * sc[0]) + bb[0]), (_Float16)(opaque(acc[mt][nt][4 * g + 1] * sc[1]) + bb[1])};
+          h2 hi = h2{(_Float16)(opaque(acc[mt][nt][4 * g + 2] * sc[2]) + bb[2]), (_Float16)(opaque(acc[mt][nt][4 * g + 3] * sc[3]) + bb[3])};
+          typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+          if (row < a.M)
+            *reinterpret_cast<IWQ_GLOBAL u32x2v*>(gp<_Float16>(a.y) + (int64_t)row * a.ldy + col) =
+                u32x2v{as_u32(lo), as_u32(hi)};
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int nt = 0; nt < NTL; ++nt) {
     const int col = n0 + wn * (32 * NTL) + nt * 32 + r32;
@@ -467,15 +521,17 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32e(PrefillArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * (32 * MTL) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        const float v = FACTOR ? opaque(acc[mt][nt][r] * sf[nt]) : acc[mt][nt][r];  // no fma_mix fold
         if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
       }
     }
+  }
   }
 }
 
 #undef IWQ_DQ
 #undef IWQ_MFMA_SLICE
+
 
 // ---------------------------------------------------------------------------------------------
 // k_w4a16_w4e: the same 256 x 256 tile on FOUR waves (one per SIMD), 128 x 128 per wave = 4 x 4
@@ -692,7 +748,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        const float v = FACTOR ? opaque(acc[mt][nt][r] * sf[nt]) : acc[mt][nt][r];  // no fma_mix fold
         if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
       }
     }
@@ -706,10 +762,43 @@ hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool GROUPED, bool FACTOR, int WM = 2, bool PHI = false, bool NIB = false>
+// Split-K epilogue: y = RN16(s * sum_split partial + b) (per channel, FACTOR) or RN16(sum + b), the
+// partials summed in split order 0..S-1 in fp32.  One thread per 4 consecutive lanes of one
+// accumulator register = 4 consecutive columns of one output row (16-B loads, 8-B stores); the
+// register -> (row, col) map is k_w4a16_b32e's (WM = 2: wave (wm, wn) owns rows 128 wm + [0, 128),
+// columns 64 wn + [0, 64); 32x32 C layout).
+template <bool FACTOR>
+__global__ __launch_bounds__(256) void k_splitk_reduce(PrefillArgs a) {
+  const int tiles_n = a.N / TN;
+  const int64_t t = blockIdx.x;
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int e = (blockIdx.y * 256 + threadIdx.x) * 4;  // element of the tile's 65536, lane-aligned
+  const int wave = e >> 13, rem = e & 8191;
+  const int tl = rem >> 10, reg = (rem >> 6) & 15, lane0 = rem & 63;
+  const int mt = tl >> 1, nt = tl & 1;  // MTL 4 x NTL 2
+  const int wm = wave >> 2, wn = wave & 3;
+  const int row = m0 + wm * 128 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane0 >> 5);
+  const int col = n0 + wn * 64 + nt * 32 + (lane0 & 31);
+  if (row >= a.M) return;
+  const IWQ_GLOBAL f4* src = gp<f4>(a.ws + (t * a.nsplit) * 65536 + e);
+  f4 sum = src[0];
+  for (int sp = 1; sp < a.nsplit; ++sp) sum += src[(int64_t)sp * (65536 / 4)];
+  _Float16 o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col + j] : 0.0f;
+    const float v = FACTOR ? opaque(sum[j] * (float)gp<_Float16>(a.scales)[col + j]) : sum[j];
+    o[j] = (_Float16)(v + b);
+  }
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<IWQ_GLOBAL u32x2v*>(gp<_Float16>(a.y) + (int64_t)row * a.ldy + col) =
+      u32x2v{as_u32(h2{o[0], o[1]}), as_u32(h2{o[2], o[3]})};
+}
+
+template <bool GROUPED, bool FACTOR, int WM = 2, bool PHI = false, bool NIB = false, bool SWAP = false>
 hipError_t launch_e(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
-  hipLaunchKernelGGL((k_w4a16_b32e<GROUPED, FACTOR, WM, PHI, NIB>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  hipLaunchKernelGGL((k_w4a16_b32e<GROUPED, FACTOR, WM, PHI, NIB, SWAP>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
   return hipGetLastError();
 }
 
@@ -901,7 +990,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16e(PrefillArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 128 + mt * 16 + 4 * q + r;
-        const float v = FACTOR ? acc[mt][nt][r] * sf[nt] : acc[mt][nt][r];
+        const float v = FACTOR ? opaque(acc[mt][nt][r] * sf[nt]) : acc[mt][nt][r];  // no fma_mix fold
         if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
       }
     }
@@ -1089,6 +1178,71 @@ hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t
   }
 }
 
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// Split-count model (times in us, fitted to profiles/r02_ab_gemm_splitk_forced.jsonl on the Llama-2-7B
+// shapes, M = 256..4096): one 512-thread workgroup per CU (120 KiB of LDS), so T x S workgroups run
+// in ceil(T S / CUs) rounds of ceil(nk / S) K-steps at ~1.4 us each; a split adds the fp32 partial
+// tiles (256 KiB per workgroup, written and read back: ~0.105 us per workgroup at ~5 TB/s) and the
+// reduce launch (~4 us).  The smallest modelled time wins (S = 1 on ties).
+int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force) {
+  const int64_t tiles = ((M + TM - 1) / TM) * (N / TN);
+  const int64_t nk = K / TK;
+  const int64_t cus = cu_count();
+  int64_t s = 1;
+  if (force > 1) {
+    s = force;
+  } else {
+    auto model = [&](int64_t c) {
+      const double t = (double)((tiles * c + cus - 1) / cus) * (double)((nk + c - 1) / c) * 1.4;
+      return c == 1 ? t : t + 4.0 + 0.105 * (double)(tiles * c);
+    };
+    double best = model(1);
+    for (int64_t c = 2; c <= 32 && c <= nk / 2; ++c) {
+      const double tc = model(c);
+      if (tc < best) {
+        best = tc;
+        s = c;
+      }
+    }
+  }
+  if (s > nk / 2) s = nk / 2;  // at least 2 K-steps per range
+  if (s < 2) return 1;
+  const int64_t kps = (nk + s - 1) / s;
+  return (int)((nk + kps - 1) / kps);  // no empty range
+}
+
+int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit) {
+  if (nsplit <= 1) return 0;
+  return ((M + TM - 1) / TM) * (N / TN) * (int64_t)nsplit * 65536 * 4;
+}
+
+hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st) {
+  PrefillArgs a = a0;
+  const int64_t tiles = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  const int nk = a.K / TK;
+  a.kps = (nk + a.nsplit - 1) / a.nsplit;
+  const dim3 grid((unsigned)(tiles * a.nsplit));
+  if (a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32e<true, false, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  else hipLaunchKernelGGL((k_w4a16_b32e<false, true, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 rgrid((unsigned)tiles, 65536 / 4 / 256);
+  if (a.gpr != 1) hipLaunchKernelGGL((k_splitk_reduce<false>), rgrid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((k_splitk_reduce<true>), rgrid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
   return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || group % TK == 0);
 }
@@ -1112,6 +1266,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
       case 63: return launch_w4<true, false>(a, st);
       case 65: return launch_w4<true, false, true>(a, st);
       case 66: return launch_e<true, false, 2, false, true>(a, st);
+      case 68: return launch_e<true, false, 2, false, false, true>(a, st);
+      case 69: return launch_e<true, false, 2, false, true, true>(a, st);
       default: return launch_e<true, false>(a, st);
     }
   }
@@ -1133,6 +1289,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 65: return launch_w4<false, true, true>(a, st);
     case 66: return launch_e<false, true, 2, false, true>(a, st);   // codes in the NIB layout
     case 67: return launch_e<false, false, 2, false, true>(a, st);  // NIB, exact
+    case 68: return launch_e<false, true, 2, false, false, true>(a, st);  // C^T epilogue
+    case 69: return launch_e<false, true, 2, false, true, true>(a, st);   // NIB + C^T epilogue
     default: return launch_e<false, true>(a, st);
   }
 }

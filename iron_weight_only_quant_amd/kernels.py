@@ -317,9 +317,11 @@ def gemm_variant_flags(v: int) -> int:
 
 
 GEMV_MAX_M = 16  # iwq_w4a16_gemm takes the weight-streaming decode kernel up to this many rows
-# w4a16_linear keeps the fused kernel (decode GEMV, then the mid-M weight-streaming kernel) up to
-# this many rows; above, dequantize-once + hipBLASLt is faster (profiles/r02_gemm_sweep.jsonl)
-FUSED_MAX_M = 128
+# w4a16_linear keeps the fused kernels (decode GEMV, the mid-M weight-streaming kernel below 256
+# rows, the split-K prefill kernel from 256) up to this many rows; above, dequantize-once + hipBLASLt
+# is faster (profiles/r02_ab_gemm_splitk_auto.jsonl vs the dequant pass of r02_gemm_sweep.jsonl:
+# at M = 1024 fused / dequant+hipBLASLt = 1.10 q_proj, 0.96 gate_proj, 0.84 down_proj)
+FUSED_MAX_M = 1024
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
@@ -380,10 +382,17 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
                 or out.numel() != M * N):
             raise ValueError("w4a16_gemm: out must be a contiguous fp16 tensor of M*N elements on x's device")
         y = out.view(M, N)
+    # split-K workspace (prefill kernel with fewer 256 x 256 tiles than CUs; variants 82-95 force 2-15
+    # K ranges for A/B): fp32 partial tiles, from torch's caching allocator
+    ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if not tiled else 0
+    v = (int(flags) >> 16) & 0xFF
+    if 81 < v < 96 and N % 256 == 0:
+        ws_bytes = max(ws_bytes, ((M + 255) // 256) * (N // 256) * (v - 80) * 65536 * 4)
+    ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
     with L.on_device(x.device):
-        st = lib.iwq_w4a16_gemm(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
-                                int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, int(flags),
-                                L.stream_handle(x.device))
+        st = lib.iwq_w4a16_gemm_ws(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
+                                   int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, L.ptr(ws), ws_bytes,
+                                   int(flags), L.stream_handle(x.device))
     _raise_for(st, "iwq_w4a16_gemm")
     return y.reshape(*x.shape[:-1], N)
 
@@ -425,7 +434,8 @@ def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zer
                  tiled_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
     decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), the mid-M
-    weight-streaming kernel up to FUSED_MAX_M rows, dequant-once + hipBLASLt (F.linear) above,
+    weight-streaming kernel and the split-K prefill kernel up to FUSED_MAX_M rows, dequant-once +
+    hipBLASLt (F.linear) above,
     where the library GEMM on a freshly dequantized weight beats the fused kernels."""
     K = x.shape[-1]
     M = x.numel() // K

@@ -822,8 +822,8 @@ def test_w4a16_prefill_big_identity(K):
 # element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
 # The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
-B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65), (47,), (48,))
-B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65), (47,))
+B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68), (47,), (48,))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
 
@@ -837,7 +837,7 @@ def nib_layout(codes, N, K):
 
 
 # NIB-layout variants: same k order and accumulation order as their row-major twins
-B32_NIB = {66: 45, 67: 46}
+B32_NIB = {66: 45, 67: 46, 69: 45}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -870,6 +870,53 @@ def test_w4a16_prefill_b32(K, M, sym, group):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
+
+
+@pytest.mark.parametrize("M", [256, 300, 512, 1024])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("group", [-2, 128])
+def test_w4a16_prefill_splitk(K, M, sym, group):
+    """Split-K prefill (iwq_w4a16_gemm_ws: fp32 partial tiles summed in range order by a second
+    kernel): within the fp16 tolerance of an fp32 GEMM on the bit-exact dequantized weight for the
+    default split and forced 2/4/8/15 ranges (15 > K-steps / 2 clamps), deterministic, and A = I
+    still picks W_deq^T exactly (every partial but one is an exact 0)."""
+    N, Kd = 512, 4352
+    torch.manual_seed(3)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 94)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (0, 82, 84, 88, 95):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (v, float(err.max()))
+        y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y2), v
+    xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
+    for v in (84, 95):
+        y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, r.out[:, :M].t().contiguous()), v
+
+
+def test_w4a16_splitk_workspace_rule(K):
+    """iwq_w4a16_gemm_workspace_bytes: the split the time model picks (iwq_prefill.hip
+    prefill_splitk_count, 256 CUs), sized tiles x ranges x 256 KiB; none below M = 256, where the
+    prefill kernel does not run (N % 256), or where splitting does not pay."""
+    lib = K.L.load()
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("expected split counts are for 256 CUs")
+    tile = 65536 * 4
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 4096, 4096, -2) == 0  # M < 256: mid-M kernel
+    assert lib.iwq_w4a16_gemm_workspace_bytes(256, 4096, 4096, -2) == 16 * 8 * tile
+    assert lib.iwq_w4a16_gemm_workspace_bytes(512, 4096, 4096, -2) == 32 * 5 * tile
+    assert lib.iwq_w4a16_gemm_workspace_bytes(512, 11008, 4096, 128) == 86 * 2 * tile
+    assert lib.iwq_w4a16_gemm_workspace_bytes(1024, 11008, 4096, -2) == 0  # 172 tiles: no gain
+    assert lib.iwq_w4a16_gemm_workspace_bytes(1024, 4096, 11008, -2) == 64 * 4 * tile
+    assert lib.iwq_w4a16_gemm_workspace_bytes(8192, 4096, 4096, -2) == 0  # 512 tiles
+    assert lib.iwq_w4a16_gemm_workspace_bytes(512, 4224, 4096, -2) == 0  # N % 256 != 0: no prefill kernel
 
 
 @pytest.mark.parametrize("group", [-2, 128])
