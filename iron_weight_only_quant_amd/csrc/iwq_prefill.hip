@@ -755,6 +755,236 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_b32w: 256 x 256 tile, 8 waves as 1 (M) x 8 (N): a wave owns ALL 256 rows x 32 columns
+// (8 x 1 tiles of 32x32x16).  Against the 2 x 4 layout each weight is dequantized once per
+// workgroup instead of twice (12 -> 6 dequant VALU per wave per MFMA slice... 96 -> 48 per K-step),
+// for twice the LDS A bytes (256 KiB per K-step: 1 ds_read_b128 per MFMA gap, the array's 256 B/clk
+// keeps up).  The per-SIMD issue budget is the limit of this loop (MFMA 8 of 32 cycles + ~4 per VALU,
+// two waves per SIMD), which is what the halved VALU buys back.
+// Hand-ordered stream: every LDS read is inline asm with hand-counted waits, every group pinned by
+// sched_barrier (hipcc's waitcnt pass waits lgkmcnt(0) on reads it has just issued).  Per MFMA
+// slice: MFMA mt then the rolling read of fragment mt of the next slice (7 MFMAs ahead of its use:
+// before MFMA mt exactly 7 newer reads are outstanding -> lgkmcnt(7)); the next slice's dequant
+// (4 pairs of 3, or 9 VALU with the NIB layout) between the MFMAs.  Early barrier as k_w4a16_b32e.
+// Per channel (scale in the epilogue) only.
+// ---------------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ h8 lds_rd(uint32_t addr) {
+  h8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_rd_u(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+
+template <bool NIB>
+__global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
+  constexpr int STAGE = XS + CS;
+  constexpr int PER_STAGE = 5;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+  // one DMA piece (i < 4: X rows, 4: codes) of K-step kt into stage stg
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * STAGE;
+    if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+
+  // this lane's column and its per-channel parameters
+  const int col = n0 + wid * 32 + r32;
+  const _Float16 sc = gp<_Float16>(a.scales)[col];
+  const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+  const float sfl = (float)sc;
+  const h2 zz = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+  const h2 zl = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+  const h2 zh = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  // LDS byte addresses: A fragment (stage st, slice s, tile mt) = la[s] + st * STAGE + 4096 mt
+  // (row = 32 mt + r32, and (row >> 1) & 7 does not depend on mt); codes of this lane's column
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) la[s] = lbase + (uint32_t)(r32 * 128 + (((4 * h + s) ^ xswz(r32)) << 4));
+  const int ccl = wid * 32 + r32;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));
+
+  // dequant pair j (weights 2j, 2j+1 of the 8 in code dword w), natural k order
+  auto dqp = [&](uint32_t w, uint32_t t8, int j) -> h2 {
+    if constexpr (NIB) {
+      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl;
+      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh;
+      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl;
+      return as_h2(and_or(t8, m1_s, mg54)) - zh;
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz;
+    }
+  };
+
+  f16x acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  h8 af[8];
+  h8 bcur;
+  u32x4 wc;
+
+#define IWQ_RD_A(MT, ADDR) af[MT] = lds_rd<(MT) * 4096>(ADDR)
+#define IWQ_MF(MT) acc[MT] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[MT], bcur, acc[MT], 0, 0, 0)
+  // one MFMA slice: MFMA mt, then the read of fragment mt of the next slice at address NADDR, the
+  // next slice's dequant (dword W) interleaved; WAITA: the lgkmcnt(7) before each MFMA
+#define IWQ_SLICE(NADDR, W, WAITA)                                                                 \
+  {                                                                                               \
+    const uint32_t wq = (W);                                                                      \
+    uint32_t t8 = 0;                                                                              \
+    h2 p0, p1, p2, p3;                                                                            \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(0); IWQ_RD_A(0, NADDR); p0 = dqp(wq, t8, 0); IWQ_PIN();                     \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(1); IWQ_RD_A(1, NADDR); if (NIB) t8 = wq >> 8; IWQ_PIN();                   \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(2); IWQ_RD_A(2, NADDR); p1 = dqp(wq, t8, 1); IWQ_PIN();                     \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(3); IWQ_RD_A(3, NADDR); IWQ_PIN();                                          \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(4); IWQ_RD_A(4, NADDR); p2 = dqp(wq, t8, 2); IWQ_PIN();                     \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, NADDR); IWQ_PIN();                                          \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(6); IWQ_RD_A(6, NADDR); p3 = dqp(wq, t8, 3); IWQ_PIN();                     \
+    if (WAITA) IWQ_LGKM(7);                                                                       \
+    IWQ_PIN(); IWQ_MF(7); IWQ_RD_A(7, NADDR); IWQ_PIN();                                          \
+    bcur = h8{p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};                                    \
+  }
+
+  // prologue: stages 0, 1, 2 (K-steps clamped to nk - 1: re-loads of stages nobody reads again)
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  issue(nk > 2 ? 2 : nk - 1, 2);
+  IWQ_PIN();
+  wc = lds_rd_u<0>(lc);
+  IWQ_RD_A(0, la[0]); IWQ_RD_A(1, la[0]); IWQ_RD_A(2, la[0]); IWQ_RD_A(3, la[0]);
+  IWQ_RD_A(4, la[0]); IWQ_RD_A(5, la[0]); IWQ_RD_A(6, la[0]); IWQ_RD_A(7, la[0]);
+  IWQ_LGKM(0);
+  IWQ_PIN();
+  {
+    const uint32_t t8 = NIB ? wc[0] >> 8 : 0u;
+    const h2 p0 = dqp(wc[0], t8, 0), p1 = dqp(wc[0], t8, 1), p2 = dqp(wc[0], t8, 2), p3 = dqp(wc[0], t8, 3);
+    bcur = h8{p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
+  }
+  // the last K-step is peeled (no branch in the loop body: acc / af need no merge copies)
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, wc[1], true)
+    IWQ_SLICE(la[2] + so, wc[2], true)
+    IWQ_SLICE(la[3] + so, wc[3], true)
+    // stage kt+1 landed (this wave's part: only stage kt+2's 5 pieces may still fly; near the end
+    // those are re-loads of the last K-step into a stage nobody reads again, so the count is
+    // constant), every read of stage kt retired
+    asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;  // DMA source K-step (clamped: see above)
+    const int sd = kt % NSTAGE;
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
+    const u32x4 wn = lds_rd_u<0>(lc + sn);
+    // slice 3 of this stage; rolling reads of the next stage's slice 0; the refill of stage kt
+    // spread one DMA piece per MFMA gap (each costs the issuing wave ~60-185 cycles: back to back
+    // after the barrier they left the MFMA pipe idle); the next slice's dequant once the code read
+    // (older than the 4 A reads before it) has landed
+    const uint32_t na = la[0] + sn;
+    h2 p0, p1, p2, p3;
+    uint32_t t8 = 0;
+    IWQ_PIN(); IWQ_MF(0); IWQ_RD_A(0, na); issue1(kd, sd, 0); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(1); IWQ_RD_A(1, na); issue1(kd, sd, 1); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(2); IWQ_RD_A(2, na); issue1(kd, sd, 2); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(3); IWQ_RD_A(3, na); issue1(kd, sd, 3); IWQ_PIN();
+    IWQ_LGKM(4);
+    IWQ_PIN(); IWQ_MF(4); IWQ_RD_A(4, na); issue1(kd, sd, 4); p0 = dqp(wn[0], t8, 0); if (NIB) t8 = wn[0] >> 8; IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, na); p1 = dqp(wn[0], t8, 1); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(6); IWQ_RD_A(6, na); p2 = dqp(wn[0], t8, 2); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(7); IWQ_RD_A(7, na); p3 = dqp(wn[0], t8, 3); IWQ_PIN();
+    bcur = h8{p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
+    wc = wn;
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, wc[1], true)
+    IWQ_SLICE(la[2] + so, wc[2], true)
+    IWQ_SLICE(la[3] + so, wc[3], true)
+    IWQ_LGKM(0);
+    IWQ_PIN();
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) IWQ_MF(mt);
+  }
+  // no LDS-DMA may still be landing when the workgroup retires (the CU's next workgroup owns the LDS)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_MF
+#undef IWQ_RD_A
+
+  const float bcol = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float v = opaque(acc[mt][r] * sfl);
+      if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + bcol);
+    }
+  }
+}
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+template <bool NIB>
+hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_b32w<NIB>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  return hipGetLastError();
+}
+
 template <bool GROUPED, bool FACTOR, bool SG = false>
 hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
@@ -1247,8 +1477,10 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
   return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || group % TK == 0);
 }
 
-// variants (flags bits 16..23 of iwq_w4a16_gemm, for A/B): 0 default = 45 (interleaved A/B on the
-// Llama-2-7B shapes at M = 8192, profiles/r02_ab_gemm_*.jsonl); per channel: 40 exact
+// variants (flags bits 16..23 of iwq_w4a16_gemm, for A/B): 0 default = 74 per channel (1 x 8 waves,
+// hand-ordered stream; +1-5 % over 45 and bit-identical to it, profiles/r02_ab_gemm_w18*.jsonl),
+// 45 grouped (interleaved A/B on the Llama-2-7B shapes at M = 8192, profiles/r02_ab_gemm_*.jsonl);
+// 60-69, 74, 75: see DESIGN.md section 5 (round 2); per channel: 40 exact
 // (scale per element), 41 factored, 42 factored + interleave, 43 factored + setprio,
 // 44 exact + interleave, 45 early barrier factored, 46 early barrier exact, 47 / 48 the same on
 // 16x16x32, 49 = 41; grouped: 40, 41 and 49 plain, 42/43 interleave / setprio, 45 early barrier,
@@ -1291,7 +1523,9 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 67: return launch_e<false, false, 2, false, true>(a, st);  // NIB, exact
     case 68: return launch_e<false, true, 2, false, false, true>(a, st);  // C^T epilogue
     case 69: return launch_e<false, true, 2, false, true, true>(a, st);   // NIB + C^T epilogue
-    default: return launch_e<false, true>(a, st);
+    case 74: return launch_w<false>(a, st);   // 1 x 8 waves, hand-ordered stream
+    case 75: return launch_w<true>(a, st);    // 1 x 8 waves, hand-ordered stream, NIB codes
+    default: return launch_w<false>(a, st);
   }
 }
 
