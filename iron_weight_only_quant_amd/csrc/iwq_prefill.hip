@@ -985,6 +985,8 @@ hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+
+
 template <bool GROUPED, bool FACTOR, bool SG = false>
 hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
