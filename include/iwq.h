@@ -208,6 +208,26 @@ int iwq_quantize_bfp(const void* w, int64_t rows, int64_t cols, int64_t ld_w, in
 int iwq_fp4_grid(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
                  void* out_scales, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag, unsigned flags,
                  void* stream);
+/* the same with the E2M1 codes of the grid values q (out = RN16(q * S)): nibble-packed, low nibble =
+ * even element, [rows * cols / 2] bytes (cols even), for storage / iwq_dequant_fp_packed (2, 1).
+ * lut: NULL (bit-level codec) or the IWQ_CODEC_GRID decode table (same bits, table speed) */
+int iwq_fp4_grid_packed(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                        void* out_codes, void* out_scales, void* workspace, int64_t workspace_bytes,
+                        uint32_t* nan_flag, unsigned flags, void* stream, const void* lut);
+
+/*
+ * FP codes -> fp16 weights (the dequant of quant_linear.py:773-777 / :825-829 / :876-880 and of
+ * fp4_quantize_cpu.py:66-72, from codes kept packed): out[N, K] = RN16(decode(code) * s) (+ z),
+ * bit-identical to iwq_quantize_fp's / iwq_fp4_grid_packed's out_deq for the codes they emit.
+ * codes: iwq_quantize_fp's layout (nibbles, low = even element, when 1 + exp_bits + mant_bits <= 4;
+ * else one byte per element), quant_dim 0 order; scales / zeros (NULL: symmetric) [G] fp16 in the
+ * reference's group order: group > 0 (K % group == 0, group % 8 == 0), IWQ_GROUP_PER_CHANNEL or
+ * IWQ_GROUP_PER_TENSOR.  K % 8 == 0, ld_out == K, out 16-B aligned.  E2M1 and E4M3 decode on the
+ * CDNA4 scaled conversions (v_cvt_scalef32_pk_f16_fp4 / _fp8; E4M3 codes 0x7F / 0xFF are the
+ * reference's +-480, not OCP NaN), other formats through an LDS table.
+ */
+int iwq_dequant_fp_packed(const void* codes, const void* scales, const void* zeros, int exp_bits, int mant_bits,
+                          int64_t group, int64_t N, int64_t K, void* out, int64_t ld_out, void* stream);
 
 /*
  * Fused dequant -> GEMM forward (QuantLinear.forward, quant_linear.py:960-972, on packed weights):

@@ -32,7 +32,7 @@ EXPORTS = (
     "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
     "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
     "iwq_dequant_packed", "iwq_quantize_fp_batched", "iwq_tile_codes",
-    "iwq_w4a16_gemm_workspace_bytes", "iwq_w4a16_gemm_ws",
+    "iwq_w4a16_gemm_workspace_bytes", "iwq_w4a16_gemm_ws", "iwq_fp4_grid_packed", "iwq_dequant_fp_packed",
 )
 
 IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX, IWQ_CODEC_APX_DOUBLE = 0, 1, 2, 3
@@ -90,6 +90,10 @@ def load():
                                         i64, vp, u32, vp]
         lib.iwq_quantize_fp.restype = i32
         lib.iwq_fp4_grid.argtypes = [vp, i64, i64, i64, i32, vp, vp, vp, i64, vp, u32, vp]
+        lib.iwq_fp4_grid_packed.argtypes = [vp, i64, i64, i64, i32, vp, vp, vp, vp, i64, vp, u32, vp, vp]
+        lib.iwq_fp4_grid_packed.restype = i32
+        lib.iwq_dequant_fp_packed.argtypes = [vp, vp, vp, i32, i32, i64, i64, i64, vp, i64, vp]
+        lib.iwq_dequant_fp_packed.restype = i32
         lib.iwq_fp4_grid.restype = i32
         lib.iwq_w4a16_gemm.argtypes = [vp, i64, i64, i64, vp, vp, vp, i32, i64, i64, vp, vp, i64, u32, vp]
         lib.iwq_w4a16_gemm.restype = i32

@@ -374,16 +374,27 @@ __device__ __forceinline__ void fp_decode_double4(const uint32_t (&code)[4], con
 }
 
 // fp4_quantize_cpu._fp_scale element (:37-44) with S = RN16(max(absmax, fp16(1e-8)) / 6)
-__device__ __forceinline__ float grid_elem(float x, float S, float rS, bool fast, const Log2Tabs& tabs) {
+// code (optional): the E2M1 code of q (sign | exponent field | mantissa; |q| in {0, .5, 1, 1.5, 2,
+// 3, 4, 6} -> 0..7), so that decode(code) * S (iwq_dequant_fp_packed) reproduces the output
+__device__ __forceinline__ float grid_elem(float x, float S, float rS, bool fast, const Log2Tabs& tabs,
+                                           uint32_t* code = nullptr) {
   float u = (fast && S > 0.0f) ? (float)(_Float16)div_f16vals(x, S, rS) : f16r(x / S);
   u = clamp_nan(u, -6.0f, 6.0f);
-  if (u != u) return u;
+  if (u != u) {
+    if (code) *code = 0;
+    return u;
+  }
   const uint32_t mag = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)u) & 0x7FFFu;
   // ls = clamp(floor(log2|u| + 1), 1): |u| == 0 -> -inf -> 1
   int ls = mag == 0 ? 1 : fp16_floor_log2_torch(mag, tabs.p1) + 1;
   ls = ls < 1 ? 1 : ls;
   const float sc = __builtin_ldexpf(1.0f, ls - 2);                        // 2^(ls - M - bias)
   const float q = __builtin_rintf(u / sc) * sc;                           // exact (power-of-two scale)
+  if (code) {
+    const int i2 = (int)(__builtin_fabsf(q) * 2.0f);                      // 0 1 2 3 4 6 8 12
+    const uint32_t e = i2 <= 4 ? (uint32_t)i2 : (i2 == 6 ? 5u : (i2 == 8 ? 6u : 7u));
+    *code = (__builtin_signbit(q) ? 8u : 0u) | e;
+  }
   return f16r(f16r(q) * S);
 }
 

@@ -203,7 +203,8 @@ typedef __attribute__((address_space(3))) const _Float16 lds_h;
 
 // Two fp16 weights of a finite group -> two fake-quantized fp16 values through the LDS table.
 template <int CODEC, bool SYM>
-__device__ __forceinline__ uint32_t fp_pair_lut(uint32_t wpair, const FpParams& p, h2 bound2, lds_char* lut) {
+__device__ __forceinline__ uint32_t fp_pair_lut(uint32_t wpair, const FpParams& p, h2 bound2, lds_char* lut,
+                                                uint32_t* qbits = nullptr) {
   const h2 s16 = h2{(_Float16)p.s, (_Float16)p.s};
   const h2 z16 = h2{(_Float16)p.z, (_Float16)p.z};
   h2 d = as_h2(wpair);
@@ -221,9 +222,23 @@ __device__ __forceinline__ uint32_t fp_pair_lut(uint32_t wpair, const FpParams& 
     const uint32_t sum = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, tb) + (u16x2)0x7FFF);
     rb |= tb & ~sum & 0x80008000u;
   }
+  if (qbits) *qbits = rb;
   h2 y = as_h2(rb) * s16;                              // RN16(exact product)
   if constexpr (!SYM) y = y + z16;                     // RN16(exact sum)
   return as_u32(y);
+}
+
+// The codes of two decoded values (the table path's pre-scale result, signs included), one per
+// 16-bit half.  Every format fp_spec accepts has E <= 4, so each magnitude code decodes to a distinct
+// fp16 value v = 2^(ef - bias) * 1.m (or m * 2^(1 - bias - M) when ef = 0), and v * 2^(bias - 15) is
+// exact in fp16 with exponent field ef (fp16 subnormal m * 2^(-14 - M) when ef = 0): its bits
+// >> (10 - M) ARE the magnitude code.  One packed multiply + shifts per pair.  The sign bit moves
+// from bit 15 to bit E + M (a sign-only code decodes to -0, so it round-trips too).
+__device__ __forceinline__ uint32_t codes_of_values(uint32_t q, const FpSpec& f, h2 rebias) {
+  const uint32_t t = as_u32(as_h2(q & 0x7FFF7FFFu) * rebias);
+  const u16x2 mag = __builtin_bit_cast(u16x2, t) >> (u16x2)(uint16_t)(10 - f.M);
+  const u16x2 sgn = __builtin_bit_cast(u16x2, q & 0x80008000u) >> (u16x2)(uint16_t)(15 - f.E - f.M);
+  return __builtin_bit_cast(uint32_t, mag | sgn);
 }
 
 __device__ __forceinline__ void fp_flag_nan(uint32_t* nan_flag, bool any_nan) {
@@ -257,7 +272,7 @@ __device__ __forceinline__ float fp_elem(float w, const FpParams& p, const FpSpe
                                          const Log2Tabs& tabs) {
   if constexpr (CODEC == CODEC_GRID) {
     code = 0;
-    return grid_elem(w, p.s, p.rs, p.fast, tabs);
+    return grid_elem(w, p.s, p.rs, p.fast, tabs, WANT_CODE ? &code : nullptr);
   } else if constexpr (CODEC == CODEC_APX) {
     return fp_apx_elem(w, p, f, code, tabs);
   } else {
@@ -367,7 +382,7 @@ __device__ __forceinline__ FpParams bcast_fp_params(const FpParams& p, int k) {
 // table (<= 48 KB for E4M3) once; finite groups take fp_pair_lut, the rest the exact ALU chain.
 // Group parameters are computed once per iteration of 4 units (g >= 32: lane l computes unit l % 4
 // of its group) and DPP-broadcast, as in k_group; GS = grid-stride walk (large single tensors).
-template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false>
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0>
 __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
@@ -395,6 +410,8 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   }
   const _Float16 bnd = __builtin_bit_cast(_Float16, (uint16_t)lut_bound_bits(CODEC, a.f));
   const h2 bound2 = {bnd, bnd};
+  const _Float16 rb16 = (_Float16)__builtin_ldexpf(1.0f, a.f.bias - 15);
+  const h2 rebias = {rb16, rb16};
   bool any_nan = false;
   // current tensor (batched: wave-uniform cursor over the table, entries ordered by unit_begin)
   const char* tw = a.w;
@@ -423,14 +440,22 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
   auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
     Vec8<DT_F16> o;
     bool nan8 = false;
+    uint32_t c[8];
     if (table) {  // finite group (grid: S > 0): table path, no NaN possible
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o.u[j] = fp_pair_lut<CODEC, SYM>(vk.u[j], p, bound2, lut);
+      for (int j = 0; j < 4; ++j) {
+        uint32_t q;
+        o.u[j] = fp_pair_lut<CODEC, SYM>(vk.u[j], p, bound2, lut, CODES ? &q : nullptr);
+        if constexpr (CODES != 0) {
+          const uint32_t cc = codes_of_values(q, a.f, rebias);
+          c[2 * j] = cc & 0xFFFFu;
+          c[2 * j + 1] = cc >> 16;
+        }
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        uint32_t c;
-        const float y = fp_elem<CODEC, SYM, false>(F::to_f(vk.get(i)), p, a.f, c, tabs);
+        const float y = fp_elem<CODEC, SYM, CODES != 0>(F::to_f(vk.get(i)), p, a.f, c[i], tabs);
         nan8 |= (y != y);
         o.set(i, F::from_f(y));
       }
@@ -438,6 +463,7 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
     if (e0 < tnumel) {
       any_nan |= nan8;
       if (tout) o.store(tout + e0 * F::BYTES);
+      if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
       if ((lane % LPG) == 0) {
         if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
         if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);
@@ -724,11 +750,11 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, int G, bool SYM>
+template <int CODEC, int G, bool SYM, int CODES = 0>
 hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
   // walk policy as k_group's single tensors: grid-stride at >= 2 grid rounds, else contiguous
-  auto kern = k_fp_group_lut<CODEC, G, SYM, false>;
-  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true>;
+  auto kern = k_fp_group_lut<CODEC, G, SYM, false, false, CODES>;
+  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true, false, CODES>;
   const size_t lds = (size_t)a.lut_n8 * 2;
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
@@ -772,16 +798,16 @@ hipError_t launch_fp_lut_batched(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, bool SYM>
+template <int CODEC, bool SYM, int CODES = 0>
 hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
   switch (g) {
-    case 8: return launch_fp_lut_t<CODEC, 8, SYM>(a, st);
-    case 16: return launch_fp_lut_t<CODEC, 16, SYM>(a, st);
-    case 32: return launch_fp_lut_t<CODEC, 32, SYM>(a, st);
-    case 64: return launch_fp_lut_t<CODEC, 64, SYM>(a, st);
-    case 128: return launch_fp_lut_t<CODEC, 128, SYM>(a, st);
-    case 256: return launch_fp_lut_t<CODEC, 256, SYM>(a, st);
-    case 512: return launch_fp_lut_t<CODEC, 512, SYM>(a, st);
+    case 8: return launch_fp_lut_t<CODEC, 8, SYM, CODES>(a, st);
+    case 16: return launch_fp_lut_t<CODEC, 16, SYM, CODES>(a, st);
+    case 32: return launch_fp_lut_t<CODEC, 32, SYM, CODES>(a, st);
+    case 64: return launch_fp_lut_t<CODEC, 64, SYM, CODES>(a, st);
+    case 128: return launch_fp_lut_t<CODEC, 128, SYM, CODES>(a, st);
+    case 256: return launch_fp_lut_t<CODEC, 256, SYM, CODES>(a, st);
+    case 512: return launch_fp_lut_t<CODEC, 512, SYM, CODES>(a, st);
   }
   return hipErrorInvalidValue;
 }
@@ -816,7 +842,14 @@ hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpAr
     if (codec == CODEC_APX) return launch_fp_lut_g<CODEC_APX, true>(g, a, st);
     return sym ? launch_fp_lut_g<CODEC_FP, true>(g, a, st) : launch_fp_lut_g<CODEC_FP, false>(g, a, st);
   }
-  if (codec == CODEC_GRID) return launch_fp_group_g<CODEC_GRID, true, 0>(g, a, st);
+  if (a.lut) {  // codes re-encoded from the table's decoded values (code_of_value)
+    if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true, 4>(g, a, st);
+    if (codes == 4)
+      return sym ? launch_fp_lut_g<CODEC_FP, true, 4>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 4>(g, a, st);
+    return sym ? launch_fp_lut_g<CODEC_FP, true, 8>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 8>(g, a, st);
+  }
+  if (codec == CODEC_GRID)
+    return codes == 4 ? launch_fp_group_g<CODEC_GRID, true, 4>(g, a, st) : launch_fp_group_g<CODEC_GRID, true, 0>(g, a, st);
   if (codec == CODEC_APX) return launch_fp_group_g<CODEC_APX, true, 0>(g, a, st);
   if (sym) {
     if (codes == 0) return launch_fp_group_g<CODEC_FP, true, 0>(g, a, st);
@@ -906,7 +939,7 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
   }
   int codes = 0;
   if (codes_out) {
-    if (codec != CODEC_FP) return IWQ_ERR_CODES;
+    if (codec != CODEC_FP && codec != CODEC_GRID) return IWQ_ERR_CODES;
     codes = (exp_bits + mant_bits + 1) <= 4 ? 4 : 8;
     if (codes == 4 && (cols & 1)) return IWQ_ERR_CODES;
   }
@@ -1197,6 +1230,14 @@ int iwq_fp4_grid_lut(const void* w, int64_t rows, int64_t cols, int64_t group, i
   // else rows of the 2-D input
   const int64_t g = per_tensor ? IWQ_GROUP_PER_TENSOR : (group > 0 ? group : IWQ_GROUP_PER_CHANNEL);
   return run_fp(CODEC_GRID, w, rows, cols, cols, IWQ_F16, 2, 1, g, 1, 0, out, cols, nullptr, out_scales, nullptr,
+                workspace, workspace_bytes, nan_flag, flags, stream, 0, 0, 0, lut);
+}
+
+int iwq_fp4_grid_packed(const void* w, int64_t rows, int64_t cols, int64_t group, int per_tensor, void* out,
+                        void* out_codes, void* out_scales, void* workspace, int64_t workspace_bytes,
+                        uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
+  const int64_t g = per_tensor ? IWQ_GROUP_PER_TENSOR : (group > 0 ? group : IWQ_GROUP_PER_CHANNEL);
+  return run_fp(CODEC_GRID, w, rows, cols, cols, IWQ_F16, 2, 1, g, 1, 0, out, cols, out_codes, out_scales, nullptr,
                 workspace, workspace_bytes, nan_flag, flags, stream, 0, 0, 0, lut);
 }
 

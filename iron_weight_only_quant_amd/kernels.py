@@ -282,8 +282,10 @@ def quantize_bfp(w: torch.Tensor, w_bit: int, group: int, quant_dim: int = 0, ou
 
 
 def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int = 0,
-             use_lut: bool = True) -> QuantResult:
-    """fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 arithmetic on the GPU; output in w's element order."""
+             use_lut: bool = True, want_codes: bool = False) -> QuantResult:
+    """fp4_quantize_cpu.quantize_fp16_to_fp4_e1m2 arithmetic on the GPU; output in w's element order.
+    want_codes: also the E2M1 codes of the grid values (nibble-packed, low nibble = even element;
+    iwq_fp4_grid_packed), so that dequant_fp_packed(codes, scales, None, 2, 1, ...) == out."""
     L.require_device(w)
     lib = L.load()
     w = w.contiguous()
@@ -303,12 +305,51 @@ def fp4_grid(w: torch.Tensor, group: int, per_tensor: bool = False, flags: int =
     wsb = ((8 * G + 255) // 256) * 256
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
     lut = _luts.get(dev, L.IWQ_CODEC_GRID) if use_lut else None
+    if want_codes:
+        if cols % 2:
+            raise ValueError("fp4_grid: packed codes need an even number of columns")
+        codes = torch.empty(rows * cols // 2, dtype=torch.uint8, device=dev)
+        with L.on_device(dev):
+            st = lib.iwq_fp4_grid_packed(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out),
+                                         L.ptr(codes), L.ptr(scales), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags),
+                                         L.stream_handle(dev), L.ptr(lut))
+        _raise_for(st, "iwq_fp4_grid_packed")
+        return QuantResult(out, scales, None, codes, nan_flag)
     with L.on_device(dev):
         st = lib.iwq_fp4_grid_lut(L.ptr(w), rows, cols, int(group), int(bool(per_tensor)), L.ptr(out),
                                   L.ptr(scales), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev),
                                   L.ptr(lut))
     _raise_for(st, "iwq_fp4_grid")
     return QuantResult(out, scales, None, None, nan_flag)
+
+
+def dequant_fp_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor], exp_bits: int,
+                      mant_bits: int, group: int, N: int, K: int,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FP codes (iwq_quantize_fp / fp4_grid(want_codes=True) layout: nibbles for 1+E+M <= 4, else one
+    byte per element) -> fp16 [N, K] = RN16(decode(code) * s) (+ z): bit-identical to the fake-quant
+    output of the same quantization (quant_linear.py:773-777; fp4_quantize_cpu.py:66-72).  E2M1 and
+    E4M3 decode on the CDNA4 scaled-conversion instructions, other formats through a table."""
+    L.require_device(codes)
+    nib = 1 + exp_bits + mant_bits <= 4
+    G = 1 if group == -1 else (N if group == -2 else (N * K // group if group > 0 else 0))
+    if codes.dtype != torch.uint8 or not codes.is_contiguous() or codes.numel() != (N * K // 2 if nib else N * K):
+        raise ValueError("dequant_fp_packed: codes must be contiguous uint8 of N*K/2 (nibbles) or N*K bytes")
+    for name, t in (("scales", scales), ("zeros", zeros)):
+        if t is not None and (t.dtype != torch.float16 or t.device != codes.device or t.numel() != G
+                              or not t.is_contiguous()):
+            raise ValueError(f"dequant_fp_packed: {name} must be contiguous fp16 [{G}] on the codes' device")
+    lib = L.load()
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float16, device=codes.device)
+    elif (out.dtype != torch.float16 or out.device != codes.device or out.shape != (N, K)
+          or not out.is_contiguous()):
+        raise ValueError("dequant_fp_packed: out must be a contiguous fp16 [N, K] tensor")
+    with L.on_device(codes.device):
+        st = lib.iwq_dequant_fp_packed(L.ptr(codes), L.ptr(scales), L.ptr(zeros), int(exp_bits), int(mant_bits),
+                                       int(group), int(N), int(K), L.ptr(out), K, L.stream_handle(codes.device))
+    _raise_for(st, "iwq_dequant_fp_packed")
+    return out
 
 
 def gemm_variant_flags(v: int) -> int:

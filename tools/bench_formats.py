@@ -1,6 +1,7 @@
 """Throughput of every weight-format path on one Llama-2-7B gate_proj weight ([11008, 4096] fp16,
 resident in HBM): INT (pseudo_quantize_tensor / QuantLinear modes), FP8/FP6/FP4 (config 5), the E2M1
-grid, BFP and the approximate / double-approximate decodes.
+grid, BFP and the approximate / double-approximate decodes; and the "unpack" paths (packed FP / grid
+codes -> fp16, iwq_dequant_fp_packed) and the grid's "pack" (fp4_grid with codes).
 
 Prints one JSON line per path: weights GB/s (fp16 input bytes / time), algorithmic HBM bytes per call
 (read weight + write dequant + scales/zeros [+ codes]), achieved GB/s and the fraction of 8 TB/s.
@@ -78,6 +79,10 @@ def main():
         ("fp8_e4m3_g128_asym", lambda w, out: K.quantize_fp(w, 4, 3, g, False, 0, out=out), 4 * n + 4 * G),
         ("fp6_e3m2_g128_asym", lambda w, out: K.quantize_fp(w, 3, 2, g, False, 0, out=out), 4 * n + 4 * G),
         ("fp4_e2m1_g128_asym", lambda w, out: K.quantize_fp(w, 2, 1, g, False, 0, out=out), 4 * n + 4 * G),
+        ("fp8_e4m3_g128_asym_codes", lambda w, out: K.quantize_fp(w, 4, 3, g, False, 0, out=out, want_codes=True),
+         5 * n + 4 * G),
+        ("fp4_e2m1_g128_asym_codes", lambda w, out: K.quantize_fp(w, 2, 1, g, False, 0, out=out, want_codes=True),
+         4.5 * n + 4 * G),
         ("fp4_grid_g128", lambda w, out: K.fp4_grid(w, g), 4 * n + 2 * G),
         ("bfp_w4_g128", lambda w, out: K.quantize_bfp(w, 4, g, out=out), 4 * n),
         ("bfp_w8_g32", lambda w, out: K.quantize_bfp(w, 8, 32, out=out), 4 * n),
@@ -86,14 +91,46 @@ def main():
         ("approx_fp8_g128_double", lambda w, out: K.quantize_fp_approx(w, 4, 3, g, 0, 12, 15, 1, True, out=out),
          4 * n + 2 * G),
     ]
+    # packed inputs of the unpack paths: codes + scales (+ zeros) of every copy
+    packs = {}
+
+    def packed(fmt):
+        if fmt not in packs:
+            if fmt == "grid":
+                packs[fmt] = [K.fp4_grid(w, g, want_codes=True) for w in ws]
+            else:
+                e, m, sym = fmt
+                packs[fmt] = [K.quantize_fp(w, e, m, g, sym, 0, want_codes=True) for w in ws]
+        return packs[fmt]
+    unpack = [
+        ("fp4_grid_g128_codes (pack)", lambda i, w, out: K.fp4_grid(w, g, want_codes=True), 4 * n + 2 * G + n // 2),
+        ("unpack_fp8_e4m3_g128_sym", ("e4m3s", (4, 3, True)), 3 * n + 2 * G),
+        ("unpack_fp8_e4m3_g128_asym", ("e4m3a", (4, 3, False)), 3 * n + 4 * G),
+        ("unpack_fp6_e3m2_g128_asym", ("e3m2a", (3, 2, False)), 3 * n + 4 * G),
+        ("unpack_fp4_e2m1_g128_asym", ("e2m1a", (2, 1, False)), 2.5 * n + 4 * G),
+        ("unpack_fp4_grid_g128", ("grid", "grid"), 2.5 * n + 2 * G),
+    ]
+    for name, spec, algo in unpack:
+        if callable(spec):
+            cases.append((name, spec, algo))
+            continue
+        fmt = spec[1]
+        e, m = (2, 1) if fmt == "grid" else fmt[:2]
+
+        def f1(i, w, out, fmt=fmt, e=e, m=m):
+            r = packed(fmt)[i]
+            K.dequant_fp_packed(r.codes, r.scales, r.zeros, e, m, g, R, C, out=out)
+        cases.append((name, f1, algo))
     only = set(a.only.split(",")) if a.only else None
     for name, f1, algo in cases:
         if only is not None and name not in only:
             continue
+        if f1.__code__.co_argcount == 2:
+            f1 = (lambda f: (lambda i, w, out: f(w, out)))(f1)
 
         def fn(f1=f1):
-            for w, out in zip(ws, outs):
-                f1(w, out)
+            for i, (w, out) in enumerate(zip(ws, outs)):
+                f1(i, w, out)
         fn()
         torch.cuda.synchronize()
         t = timed(fn, a.reps) / len(ws)
