@@ -987,6 +987,310 @@ hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
 
 
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_w4h: the 256 x 256 tile on FOUR waves (one per SIMD, 128 x 128 each: 4 x 4 tiles of
+// 32x32x16, 256 fp32 accumulators per lane in AGPRs), with k_w4a16_b32w's hand-ordered stream.
+// Against the 8-wave forms the LDS read traffic per K-step drops 3x (each A fragment feeds 4 MFMAs,
+// each dequantized B fragment 4: 80 KiB per K-step per CU instead of 264) and no second wave shares
+// a SIMD's issue port; the price is that nothing else covers this wave's stalls, so:
+//  * X and codes are staged through REGISTERS (global_load_dwordx4 -> ds_write_b128: an LDS-DMA
+//    instruction holds its issuing wave ~60-185 cycles, 10 per K-step would idle the MFMA pipe),
+//    issued one K-step ahead of their LDS write, into a 2-stage ring (80 KiB);
+//  * every LDS access is inline asm with hand-counted waits and every group is pinned by
+//    sched_barrier; each MFMA gap holds at most one LDS read, one staged write + load and a
+//    dequant pair;
+//  * one barrier per K-step, before its last slice (its 16 MFMAs cover the next stage's first
+//    reads).  The stage written in K-step kt is the one read in kt - 1, whose reads all retired
+//    before that K-step's barrier.
+// Same LDS images, k order and accumulation order as k_w4a16_b32w: bit-identical to 45 / 74
+// (NIB: to 66 / 75 on NIB codes).  Per channel (scale in the epilogue) only.
+// Measured (profiles/r02_ab_gemm_w4h.jsonl): 1-4 % behind 74 (76; NIB 77 at
+// par); the loop with the staging removed runs 10-14 % faster than 76 (78 of the A/B log), with the
+// staging reading one cache-resident K-step over and over 3-4 % -- so the staging's cost is mostly
+// its issue and LDS-write traffic, not memory latency; DMA staging (79) is no better.  Kept for A/B.
+// ---------------------------------------------------------------------------------------------
+template <int OFF>
+__device__ __forceinline__ void lds_wr(uint32_t addr, u32x4 v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "n"(OFF) : "memory");
+}
+
+// WMW: waves along M -- 2: 2 x 2 waves of 128 x 128 (4 x 4 tiles); 1: 1 x 4 waves of 256 x 64
+// (8 x 2 tiles: every weight dequantized once per workgroup, twice the A reads)
+template <bool NIB, int WMW, bool DMA = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_w4a16_w4h(PrefillArgs a) {
+  constexpr int STAGE = XS + CS;  // 40 KiB
+  constexpr int NST = DMA ? 3 : 2;
+  constexpr int MT = 8 / WMW, NT = 2 * WMW;  // 32 x 32 tiles per wave
+  constexpr int P = 4 * NT;                  // dequant pairs per slice
+  constexpr int PSTEP = 16 / P;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NST * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = WMW == 2 ? wid >> 1 : 0, wn = WMW == 2 ? wid & 1 : wid;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+
+  // staging sources as 32-bit byte offsets from uniform bases (the launcher checks the ranges):
+  // X slot i of wave w = rows 64 w + 8 i + lane / 8; codes slots 2 w + i = columns 64 w + 32 i + lane / 2
+  uint32_t xoff[8], coff[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wid * 64 + i * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xoff[i] = (uint32_t)(((int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3)) * 2);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ccol = (2 * wid + i) * 32 + (lane >> 1);
+    coff[i] = (uint32_t)((int64_t)(n0 + ccol) * (a.K / 2) + (((lane & 1) ^ cswz(ccol)) << 4));
+  }
+  const char* xg = reinterpret_cast<const char*>(a.x);
+  const char* cg = reinterpret_cast<const char*>(a.codes);
+  u32x4 g[10];
+  auto gload = [&](int kt, int j) {
+    if (j < 8) g[j] = *gp<u32x4>(xg + (int64_t)kt * (TK * 2) + xoff[j]);
+    else g[j] = *gp<u32x4>(cg + (int64_t)kt * (TK / 2) + coff[j - 8]);
+  };
+  // DMA staging: piece j of K-step kt straight into stage stg (lane-linear destination)
+  auto dma1 = [&](int kt, int stg, int j) {
+    uint8_t* base = smem + stg * STAGE;
+    if (j < 8) glds16(xg + (int64_t)kt * (TK * 2) + xoff[j], base + wid * 8192 + j * 1024);
+    else glds16(cg + (int64_t)kt * (TK / 2) + coff[j - 8], base + XS + wid * 2048 + (j - 8) * 1024);
+  };
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  const uint32_t wx = lbase + (uint32_t)(wid * 8192 + lane * 16);            // + 1024 i
+  const uint32_t wcd = lbase + XS + (uint32_t)(wid * 2048 + lane * 16);      // + 1024 i
+#define IWQ_GWRITE(J, SO)                                              \
+  do {                                                                 \
+    if ((J) < 8) lds_wr<((J) < 8 ? (J) : 0) * 1024>(wx + (SO), g[J]);  \
+    else lds_wr<((J) >= 8 ? (J) - 8 : 0) * 1024>(wcd + (SO), g[J]);    \
+  } while (0)
+
+  // per-channel parameters of this lane's NT columns
+  h2 zz[NT], zl[NT], zh[NT];
+  float sfl[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = n0 + wn * (NT * 32) + nt * 32 + r32;
+    const _Float16 sc = gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    sfl[nt] = (float)sc;
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  // LDS read addresses: A fragment (slice s, tile mt) = la[s] + stage + 4096 mt; codes of tile nt
+  // = lc + stage + 1024 nt
+  uint32_t la[4];
+  const int arow = wm * (MT * 32) + r32;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) la[s2] = lbase + (uint32_t)(arow * 128 + (((4 * h + s2) ^ xswz(arow)) << 4));
+  const int ccl = wn * (NT * 32) + r32;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));
+
+  auto dqp = [&](uint32_t w, uint32_t t8, int j, int nt) -> h2 {
+    if constexpr (NIB) {
+      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl[nt];
+      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh[nt];
+      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl[nt];
+      return as_h2(and_or(t8, m1_s, mg54)) - zh[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+  };
+
+  f16x acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  h8 A0[MT], A1[MT];
+  h2 B0[NT][4], B1[NT][4];  // [nt][pair]
+  u32x4 wc[NT], wq[NT];
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+#define IWQ_BV(B, NT) (h8{B[NT][0].x, B[NT][0].y, B[NT][1].x, B[NT][1].y, B[NT][2].x, B[NT][2].y, B[NT][3].x, B[NT][3].y})
+#define IWQ_MF(AC, BC, I) \
+  acc[(I) / NT][(I) % NT] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AC[(I) / NT], IWQ_BV(BC, (I) % NT), acc[(I) / NT][(I) % NT], 0, 0, 0)
+  // dequant pair (nt, j) of slice S2 from code dwords W[nt][S2] into BN; NIB keeps w >> 8 per nt
+#define IWQ_DQ(BN, W, S2, NT, J)                                                   \
+  {                                                                               \
+    const uint32_t wv = W[NT][S2];                                                \
+    BN[NT][J] = dqp(wv, NIB ? (wv >> 8) : 0u, J, NT);                             \
+  }
+  // one slice: 16 MFMAs on (AC, BC); step i also: i < MT the read of A fragment i of the next
+  // slice (address NA) into AN; every PSTEP-th step one of the P dequant pairs of the next slice
+  // (code dwords W, slice S2) into BN; STG: staged write + refill j = STG0 + (i - 5) / 2 for odd i
+  // in [5, 15)
+#define IWQ_SLICE(AC, BC, AN, BN, NA, W, S2, STG, STG0, SO, KD)                     \
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                \
+    IWQ_PIN();                                                                    \
+    IWQ_MF(AC, BC, i);                                                            \
+    if (i < MT) AN[i % MT] = lds_rd<0>((NA) + 4096u * (uint32_t)(i % MT));         \
+    if (i % PSTEP == 0) IWQ_DQ(BN, W, S2, ((i / PSTEP) >> 2), ((i / PSTEP) & 3));  \
+    if (STG && i >= 5 && i < 15 && ((i - 5) & 1) == 0) {                          \
+      const int jj = (STG0) + ((i - 5) >> 1);                                     \
+      if constexpr (DMA) {                                                        \
+        dma1(KD, (int)(SO), jj);                                                  \
+      } else {                                                                    \
+        IWQ_GWRITE_RT(jj, SO);                                                    \
+        gload(KD, jj);                                                            \
+      }                                                                           \
+    }                                                                             \
+    IWQ_PIN();                                                                    \
+  }                                                                               \
+  if (!DMA && STG) IWQ_LGKM(5); else IWQ_LGKM(0);
+
+  // runtime-j staged write (j is a compile-time constant after unrolling)
+#define IWQ_GWRITE_RT(J, SO)                  \
+  switch (J) {                                \
+    case 0: IWQ_GWRITE(0, SO); break;         \
+    case 1: IWQ_GWRITE(1, SO); break;         \
+    case 2: IWQ_GWRITE(2, SO); break;         \
+    case 3: IWQ_GWRITE(3, SO); break;         \
+    case 4: IWQ_GWRITE(4, SO); break;         \
+    case 5: IWQ_GWRITE(5, SO); break;         \
+    case 6: IWQ_GWRITE(6, SO); break;         \
+    case 7: IWQ_GWRITE(7, SO); break;         \
+    case 8: IWQ_GWRITE(8, SO); break;         \
+    default: IWQ_GWRITE(9, SO); break;        \
+  }
+
+  // prologue: K-step 0 -> stage 0 (written), K-step 1 in flight in g (DMA: K-steps 0 and 1 into
+  // stages 0 and 1, the first landed)
+  if constexpr (DMA) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) dma1(0, 0, j);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) dma1(nk > 1 ? 1 : 0, 1, j);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) gload(0, j);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) IWQ_GWRITE_RT(j, 0u);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) gload(nk > 1 ? 1 : 0, j);
+  }
+  IWQ_LGKM(0);
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) wc[nt] = lds_rd_u<0>(lc + 1024u * (uint32_t)nt);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) A0[mt] = lds_rd<0>(la[0] + 4096u * (uint32_t)mt);
+  IWQ_LGKM(0);
+  IWQ_PIN();
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) IWQ_DQ(B0, wc, 0, nt, j);
+
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NST) * STAGE);        // stage of K-step kt
+    const uint32_t sn = (uint32_t)(((kt + 1) % NST) * STAGE);  // stage of K-step kt + 1
+    const int kd = kt + 2 < nk ? kt + 2 : nk - 1;              // refill source (clamped: re-load)
+    // refill target: registers -> stage kt+1 (written this K-step, K-step kt+2 loaded); DMA ->
+    // stage kt+2 (the one read in K-step kt-1), landing before the barrier of K-step kt+1
+    const uint32_t sw = DMA ? (uint32_t)((kt + 2) % NST) : sn;
+    IWQ_SLICE(A0, B0, A1, B1, la[1] + so, wc, 1, true, 0, sw, kd)
+    IWQ_SLICE(A1, B1, A0, B0, la[2] + so, wc, 2, true, 5, sw, kd)
+    IWQ_SLICE(A0, B0, A1, B1, la[3] + so, wc, 3, false, 0, sw, kd)
+    // stage kt+1 written / landed for every wave, every read of stage kt retired (lgkmcnt(0) above)
+    if constexpr (DMA) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    // slice 3: codes of K-step kt+1 first, then its slice-0 A fragments; the dequant once the codes
+    // have landed (MT younger A reads may still fly: lgkmcnt(MT)), PP pairs per step
+    constexpr int S0 = NT + MT;
+    constexpr int PP = (P + (16 - S0) - 1) / (16 - S0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      IWQ_PIN();
+      IWQ_MF(A1, B1, i);
+      if (i < NT) wq[i % NT] = lds_rd_u<0>(lc + sn + 1024u * (uint32_t)(i % NT));
+      else if (i < S0) A0[(i - NT) % MT] = lds_rd<0>(la[0] + sn + 4096u * (uint32_t)((i - NT) % MT));
+      if (i == S0) {
+        if constexpr (MT == 8) IWQ_LGKM(8);
+        else IWQ_LGKM(4);
+      }
+      if (i >= S0) {
+#pragma unroll
+        for (int u = 0; u < PP; ++u) {
+          const int q = (i - S0) * PP + u;
+          if (q < P) IWQ_DQ(B0, wq, 0, (q >> 2), (q & 3));
+        }
+      }
+      IWQ_PIN();
+    }
+    IWQ_LGKM(0);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) wc[nt] = wq[nt];
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) % NST) * STAGE);
+    IWQ_SLICE(A0, B0, A1, B1, la[1] + so, wc, 1, false, 0, so, 0)
+    IWQ_SLICE(A1, B1, A0, B0, la[2] + so, wc, 2, false, 0, so, 0)
+    IWQ_SLICE(A0, B0, A1, B1, la[3] + so, wc, 3, false, 0, so, 0)
+    IWQ_PIN();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) IWQ_MF(A1, B1, i);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_DQ
+#undef IWQ_MF
+#undef IWQ_BV
+#undef IWQ_GWRITE_RT
+#undef IWQ_GWRITE
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = n0 + wn * (NT * 32) + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (MT * 32) + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = opaque(acc[mt][nt][r] * sfl[nt]);
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+// the 32-bit staging offsets of k_w4a16_w4h must cover X and the codes
+bool w4h_fits(const PrefillArgs& a) {
+  return (int64_t)a.M * a.lda * 2 < ((int64_t)1 << 31) && (int64_t)a.N * (a.K / 2) < ((int64_t)1 << 31);
+}
+
+template <bool NIB, int WMW, bool DMA = false>
+hipError_t launch_w4h(const PrefillArgs& a, hipStream_t st) {
+  if (!w4h_fits(a)) return launch_w<NIB>(a, st);
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_w4h<NIB, WMW, DMA>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 template <bool GROUPED, bool FACTOR, bool SG = false>
 hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
@@ -1527,6 +1831,10 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 69: return launch_e<false, true, 2, false, true, true>(a, st);   // NIB + C^T epilogue
     case 74: return launch_w<false>(a, st);   // 1 x 8 waves, hand-ordered stream
     case 75: return launch_w<true>(a, st);    // 1 x 8 waves, hand-ordered stream, NIB codes
+    case 76: return launch_w4h<false, 2>(a, st);  // 2 x 2 waves of 128^2, register-staged, hand-ordered
+    case 77: return launch_w4h<true, 2>(a, st);   // the same on NIB codes
+    case 78: return launch_w4h<false, 1>(a, st);        // 1 x 4 waves of 256 x 64
+    case 79: return launch_w4h<false, 2, true>(a, st);  // 2 x 2, LDS-DMA staging (3 stages)
     default: return launch_w<false>(a, st);
   }
 }

@@ -822,8 +822,8 @@ def test_w4a16_prefill_big_identity(K):
 # element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
 # The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
-B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 74), (47,), (48,))
-B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68), (47,))
+B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 74, 76, 78, 79), (47,), (48,))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 74, 76, 78, 79), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
 
@@ -837,7 +837,7 @@ def nib_layout(codes, N, K):
 
 
 # NIB-layout variants: same k order and accumulation order as their row-major twins
-B32_NIB = {66: 45, 67: 46, 69: 45, 75: 45}
+B32_NIB = {66: 45, 67: 46, 69: 45, 75: 45, 77: 45}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -866,7 +866,7 @@ def test_w4a16_prefill_b32(K, M, sym, group):
             assert torch.equal(ys[v], ys[vs[0]]), (vs[0], v)
     nib = nib_layout(r.codes, N, Kd)
     for v, twin in B32_NIB.items():
-        if group != -2 and v in (67, 75):
+        if group != -2 and v in (67, 75, 77):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
@@ -931,6 +931,31 @@ def test_w4a16_prefill_b32_identity(K, group):
     for v in B32_ALL:
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, r.out.t().contiguous()), v
+
+
+@pytest.mark.parametrize("Kd", [128, 256, 384])
+def test_w4a16_prefill_short_k(K, Kd):
+    """2, 4, 6 K-steps (the C-ABI takes K % 128 == 0) through the hand-ordered kernels (prologue,
+    peeled last step, the 2- / 3-stage rings' wrap): identical bits to variant 45 (NIB twins on NIB
+    codes)."""
+    N, M = 512, 300
+    torch.manual_seed(5)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 96)
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    y45 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(45))
+    assert bool(((y45.float() - ref).abs() <= tol).all())
+    for v in (74, 76, 78, 79):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y45), v
+    nib = nib_layout(r.codes, N, Kd)
+    for v in (75, 77):
+        y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y45), v
 
 
 MID_VARIANTS = (50, 51, 52, 53, 54, 55)  # k_w4a16_mid: (MT row tiles, CT column tiles) shapes

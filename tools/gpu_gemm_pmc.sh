@@ -4,13 +4,16 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 VARS=${VARS:-0,45,47}
-timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" > "$OUT/ab_gemm_pc.jsonl" 2>&1 || exit $?
-timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" --group 128 > "$OUT/ab_gemm_g128.jsonl" 2>&1 || exit $?
+SHAPES=${SHAPES:-"4096x4096 4096x11008"}
+if [ -z "$NO_AB" ]; then
+  timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" > "$OUT/ab_gemm_pc.jsonl" 2>&1 || exit $?
+  timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" --group 128 > "$OUT/ab_gemm_g128.jsonl" 2>&1 || exit $?
+fi
 cd /tmp
 P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 P2="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
-for shape in "4096 4096" "4096 11008"; do
-  set -- $shape; N=$1; K=$2
+for shape in $SHAPES; do
+  N=${shape%x*}; K=${shape#*x}
   for arm in ref $(echo $VARS | tr ',' ' '); do
     if [ $arm = ref ]; then A="--ref"; else A="--variant $arm"; fi
     for p in 1 2; do
