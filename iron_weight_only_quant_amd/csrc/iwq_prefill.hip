@@ -1291,6 +1291,208 @@ hipError_t launch_w4h(const PrefillArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_w4b: k_w4a16_w4h with the weight tile dequantized ONCE per workgroup into LDS: each lane
+// stages its own column's codes (32 B per K-step) in registers, dequantizes them and writes the
+// column's 64 fp16 weights (q - z, natural k order) as one 128-B row of a B image laid out like the
+// X image; the MFMA loop then reads A and B fragments alike from LDS (hipBLASLt's structure plus a
+// dequant pass).  Per wave and K-step: 96 dequant VALU (72 NIB) instead of 192, 32 fragment reads
+// and 16 staged writes instead of 20 + 10.  Same k order / accumulation order as 74: bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <bool NIB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_w4a16_w4b(PrefillArgs a) {
+  constexpr int BS = TN * TK * 2;      // B image bytes per stage (32 KiB)
+  constexpr int STAGE = XS + BS;       // 64 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+
+  uint32_t xoff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wid * 64 + i * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xoff[i] = (uint32_t)(((int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3)) * 2);
+  }
+  const int dcol = wid * 64 + lane;  // the column this lane dequantizes
+  const uint32_t coff = (uint32_t)((int64_t)(n0 + dcol) * (a.K / 2));
+  const char* xg = reinterpret_cast<const char*>(a.x);
+  const char* cg = reinterpret_cast<const char*>(a.codes);
+  u32x4 gx[8], gc[2];
+  auto ldx = [&](int kt, int j) { gx[j] = *gp<u32x4>(xg + (int64_t)kt * (TK * 2) + xoff[j]); };
+  auto ldc = [&](int kt, int j) { gc[j] = *gp<u32x4>(cg + (int64_t)kt * (TK / 2) + coff + 16 * j); };
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  const uint32_t wx = lbase + (uint32_t)(wid * 8192 + lane * 16);  // + 1024 i
+  uint32_t bw[8];                                                  // B image chunk j of dcol
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bw[j] = lbase + XS + (uint32_t)(dcol * 128 + ((j ^ xswz(dcol)) << 4));
+
+  // zero point of the dequantized column; scales of this lane's 4 MFMA columns (epilogue)
+  const float zfd = a.zeros ? (float)gp<_Float16>(a.zeros)[n0 + dcol] : a.zsym;
+  const h2 zz = h2{(_Float16)(1024.0f + zfd), (_Float16)(64.0f + zfd)};
+  const h2 zl = h2{(_Float16)(1024.0f + zfd), (_Float16)(1024.0f + zfd)};
+  const h2 zh = h2{(_Float16)(64.0f + zfd), (_Float16)(64.0f + zfd)};
+  float sfl[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) sfl[nt] = (float)gp<_Float16>(a.scales)[n0 + wn * 128 + nt * 32 + r32];
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+  auto dqp = [&](uint32_t w, int j) -> h2 {
+    if constexpr (NIB) {
+      const uint32_t t8 = w >> 8;
+      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl;
+      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh;
+      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl;
+      return as_h2(and_or(t8, m1_s, mg54)) - zh;
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz;
+    }
+  };
+
+  // fragment read addresses: A (slice s, tile mt) = la[s] + stage + 4096 mt, B (slice s, tile nt) =
+  // lb[s] + stage + 4096 nt
+  uint32_t la[4], lb[4];
+  const int arow = wm * 128 + r32, brow = wn * 128 + r32;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) {
+    la[s2] = lbase + (uint32_t)(arow * 128 + (((4 * h + s2) ^ xswz(arow)) << 4));
+    lb[s2] = lbase + XS + (uint32_t)(brow * 128 + (((4 * h + s2) ^ xswz(brow)) << 4));
+  }
+
+  f16x acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  h8 A0[4], A1[4], B0[4], B1[4];
+  h2 dq[4];
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+#define IWQ_MF(AC, BC, I) \
+  acc[(I) >> 2][(I) & 3] = __builtin_amdgcn_mfma_f32_32x32x16_f16(AC[(I) >> 2], BC[(I) & 3], acc[(I) >> 2][(I) & 3], 0, 0, 0)
+#define IWQ_WRB(J, SO)                                                                              \
+  {                                                                                                 \
+    const h8 v = h8{dq[0].x, dq[0].y, dq[1].x, dq[1].y, dq[2].x, dq[2].y, dq[3].x, dq[3].y};        \
+    lds_wr<0>(bw[J] + (SO), __builtin_bit_cast(u32x4, v));                                         \
+  }
+  // one slice: 16 MFMAs on (AC, BC); steps 0-7 read the next slice's fragments (A i, B i - 4) at
+  // NS (slice offset: la/lb index, stage); STG: steps 0-15 dequantize 4 code dwords (one pair per
+  // step; dword d = 4 H + step / 4, its B row chunk written after its last pair), even steps >= 8
+  // write X piece 4 H + (step - 8) / 2 and refill it; the code piece H is refilled after its dwords
+#define IWQ_SLICE(AC, BC, AN, BN, S2N, SOR, STG, H, SOW, KD)                                       \
+  _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                                \
+    IWQ_PIN();                                                                                    \
+    IWQ_MF(AC, BC, i);                                                                            \
+    if (i < 4) AN[i] = lds_rd<0>(la[S2N] + (SOR) + 4096u * (uint32_t)i);                           \
+    else if (i < 8) BN[i - 4] = lds_rd<0>(lb[S2N] + (SOR) + 4096u * (uint32_t)(i - 4));            \
+    if (STG) {                                                                                    \
+      dq[i & 3] = dqp(gc[H][i >> 2], i & 3);                                                      \
+      if ((i & 3) == 3) IWQ_WRB(4 * (H) + (i >> 2), SOW);                                         \
+      if (i >= 8 && (i & 1) == 0) {                                                               \
+        const int jx = 4 * (H) + ((i - 8) >> 1);                                                  \
+        lds_wr<0>(wx + 1024u * (uint32_t)jx + (SOW), gx[jx]);                                     \
+        ldx(KD, jx);                                                                              \
+      }                                                                                           \
+      if (i == 15) ldc(KD, H);                                                                    \
+    }                                                                                             \
+    IWQ_PIN();                                                                                    \
+  }                                                                                               \
+  if (STG) IWQ_LGKM(7); else IWQ_LGKM(0);  /* STG: 7 writes were issued after the last read */
+
+  // prologue: K-step 0 staged into stage 0 (X copied, codes dequantized), K-step 1 in flight
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ldx(0, j);
+  ldc(0, 0);
+  ldc(0, 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) lds_wr<0>(wx + 1024u * (uint32_t)j, gx[j]);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+#pragma unroll
+    for (int p2 = 0; p2 < 4; ++p2) dq[p2] = dqp(gc[d >> 2][d & 3], p2);
+    IWQ_WRB(d, 0u);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ldx(nk > 1 ? 1 : 0, j);
+  ldc(nk > 1 ? 1 : 0, 0);
+  ldc(nk > 1 ? 1 : 0, 1);
+  IWQ_LGKM(0);
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) A0[i] = lds_rd<0>(la[0] + 4096u * (uint32_t)i);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) B0[i] = lds_rd<0>(lb[0] + 4096u * (uint32_t)i);
+  IWQ_LGKM(0);
+  IWQ_PIN();
+
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt & 1) * STAGE);
+    const uint32_t sn = (uint32_t)(((kt + 1) & 1) * STAGE);
+    const int kd = kt + 2 < nk ? kt + 2 : nk - 1;
+    IWQ_SLICE(A0, B0, A1, B1, 1, so, true, 0, sn, kd)
+    IWQ_SLICE(A1, B1, A0, B0, 2, so, true, 1, sn, kd)
+    IWQ_SLICE(A0, B0, A1, B1, 3, so, false, 0, sn, kd)
+    // stage kt+1 complete (X and B written by every wave), every read of stage kt retired
+    __builtin_amdgcn_s_barrier();
+    IWQ_SLICE(A1, B1, A0, B0, 0, sn, false, 0, sn, kd)
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) & 1) * STAGE);
+    IWQ_SLICE(A0, B0, A1, B1, 1, so, false, 0, so, 0)
+    IWQ_SLICE(A1, B1, A0, B0, 2, so, false, 0, so, 0)
+    IWQ_SLICE(A0, B0, A1, B1, 3, so, false, 0, so, 0)
+    IWQ_PIN();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) IWQ_MF(A1, B1, i);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_WRB
+#undef IWQ_MF
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = n0 + wn * 128 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = opaque(acc[mt][nt][r] * sfl[nt]);
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+template <bool NIB>
+hipError_t launch_w4b(const PrefillArgs& a, hipStream_t st) {
+  if (!w4h_fits(a)) return launch_w<NIB>(a, st);
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_w4b<NIB>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 template <bool GROUPED, bool FACTOR, bool SG = false>
 hipError_t launch_w4(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
@@ -1835,6 +2037,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 77: return launch_w4h<true, 2>(a, st);   // the same on NIB codes
     case 78: return launch_w4h<false, 1>(a, st);        // 1 x 4 waves of 256 x 64
     case 79: return launch_w4h<false, 2, true>(a, st);  // 2 x 2, LDS-DMA staging (3 stages)
+    case 80: return launch_w4b<false>(a, st);           // 2 x 2, weights dequantized once into LDS
+    case 81: return launch_w4b<true>(a, st);            // the same on NIB codes
     default: return launch_w<false>(a, st);
   }
 }
