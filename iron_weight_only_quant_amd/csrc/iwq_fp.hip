@@ -115,12 +115,23 @@ __device__ __forceinline__ int apxd_tgt(uint32_t b0, uint32_t b1, uint32_t b2, u
   return tgt;
 }
 
-// value of lane (lane ^ M): ds_swizzle in bit-mask mode (no address VGPR) inside 32-lane halves,
-// ds_bpermute (__shfl_xor) across them
+// value of lane (lane ^ M) without the LDS pipe where CDNA4 allows: M = 8 is a DPP row rotation by
+// 8 (inside 16-lane rows), M = 16 / 32 the gfx950 v_permlane16_swap / v_permlane32_swap (odd rows
+// <-> even rows, upper <-> lower half: with both operands = v, each lane takes the half of the pair
+// that came from its partner); M = 4 stays a ds_swizzle in bit-mask mode
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
-  if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);
-  else return (uint32_t)__shfl_xor((int)v, M);
+  if constexpr (M == 8) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (M == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? r[0] : r[1];
+  } else if constexpr (M == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? r[0] : r[1];
+  } else {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);
+  }
 }
 
 // apxd_tgt on 4 elements at once: bytes of x / a / b / c are the info bytes of the quad members
@@ -527,8 +538,8 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
 // a quad is 4 consecutive groups at one in-group position, i.e. lanes l, l^LPG, l^2LPG, l^3LPG of
 // the same 512-element unit at the same element slot (4 LPG <= 64).  Per element: symmetric FP
 // t = clamp(RN16(w / s)) (packed on finite groups), its info word from the LDS table (exact ALU
-// codec on non-finite groups), one info byte per element exchanged with the 3 partners (6
-// ds_bpermute per unit), then the quad decode and RN16(v * s) -- the reference's two passes
+// codec on non-finite groups), one info byte per element exchanged with the 3 partners (6 lane
+// exchanges per unit: DPP / permlane swaps, lane_xor), then the quad decode and RN16(v * s) -- the reference's two passes
 // through a code buffer (and k_apx_double's scattered quad reads) in one streaming pass.
 template <int G, bool GS>
 __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
