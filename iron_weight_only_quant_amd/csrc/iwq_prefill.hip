@@ -781,6 +781,15 @@ __device__ __forceinline__ u32x4 lds_rd_u(uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
   return v;
 }
+// A value read by inline asm is only valid once its lgkmcnt wait has retired, which the compiler
+// cannot see: passes before the scheduler (CSE, hoisting) may move a cheap use of it (a shift of a
+// code dword) above the wait.  landed(v) after the wait re-defines v there (volatile asm keeps its
+// order with the volatile wait), so every later use depends on the post-wait value.
+template <class T>
+__device__ __forceinline__ void landed(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
 #define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
 
@@ -907,6 +916,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   IWQ_RD_A(0, la[0]); IWQ_RD_A(1, la[0]); IWQ_RD_A(2, la[0]); IWQ_RD_A(3, la[0]);
   IWQ_RD_A(4, la[0]); IWQ_RD_A(5, la[0]); IWQ_RD_A(6, la[0]); IWQ_RD_A(7, la[0]);
   IWQ_LGKM(0);
+  landed(wc);
   IWQ_PIN();
   {
     const uint32_t t8 = NIB ? wc[0] >> 8 : 0u;
@@ -928,7 +938,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     const int kd = kt + 3 < nk ? kt + 3 : nk - 1;  // DMA source K-step (clamped: see above)
     const int sd = kt % NSTAGE;
     const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
-    const u32x4 wn = lds_rd_u<0>(lc + sn);
+    u32x4 wn = lds_rd_u<0>(lc + sn);
     // slice 3 of this stage; rolling reads of the next stage's slice 0; the refill of stage kt
     // spread one DMA piece per MFMA gap (each costs the issuing wave ~60-185 cycles: back to back
     // after the barrier they left the MFMA pipe idle); the next slice's dequant once the code read
@@ -941,6 +951,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     IWQ_PIN(); IWQ_MF(2); IWQ_RD_A(2, na); issue1(kd, sd, 2); IWQ_PIN();
     IWQ_PIN(); IWQ_MF(3); IWQ_RD_A(3, na); issue1(kd, sd, 3); IWQ_PIN();
     IWQ_LGKM(4);
+    landed(wn);
     IWQ_PIN(); IWQ_MF(4); IWQ_RD_A(4, na); issue1(kd, sd, 4); p0 = dqp(wn[0], t8, 0); if (NIB) t8 = wn[0] >> 8; IWQ_PIN();
     IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, na); p1 = dqp(wn[0], t8, 1); IWQ_PIN();
     IWQ_PIN(); IWQ_MF(6); IWQ_RD_A(6, na); p2 = dqp(wn[0], t8, 2); IWQ_PIN();
@@ -977,6 +988,228 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 }
 #undef IWQ_LGKM
 #undef IWQ_PIN
+
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_b32v: k_w4a16_b32w's hand-ordered stream on 8 waves as 2 (M) x 4 (N), 128 rows x 64
+// columns per wave (4 x 2 tiles): half the LDS A reads of the 1 x 8 form (17 instead of 33
+// ds_read_b128 per wave per K-step, each A fragment feeding 2 MFMAs) for twice the dequant VALU
+// (each weight dequantized by 2 waves).  Same staging (LDS-DMA, 3 stages, early barrier), k order
+// and accumulation order as 74: bit-identical.
+// ---------------------------------------------------------------------------------------------
+template <bool NIB>
+__global__ __launch_bounds__(THR) void k_w4a16_b32v(PrefillArgs a) {
+  constexpr int STAGE = XS + CS;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  // staging exactly as k_w4a16_b32w (X rows / code columns per wave, lane-linear LDS destinations)
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int scol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + scol) * crow + (((lane & 1) ^ cswz(scol)) << 4);
+  auto issue = [&](int kt, int stg) {
+    uint8_t* base = smem + stg * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * STAGE;
+    if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+
+  // this lane's 2 MFMA columns and their per-channel parameters
+  h2 zz[2], zl[2], zh[2];
+  float sfl[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const _Float16 sc = gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    sfl[nt] = (float)sc;
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[4];
+  const int arow = wm * 128 + r32;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) la[s2] = lbase + (uint32_t)(arow * 128 + (((4 * h + s2) ^ xswz(arow)) << 4));
+  const int ccl = wn * 64 + r32;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));  // + 1024 nt
+
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    if constexpr (NIB) {
+      const uint32_t t8 = w >> 8;
+      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl[nt];
+      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh[nt];
+      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl[nt];
+      return as_h2(and_or(t8, m1_s, mg54)) - zh[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+  };
+
+  f16x acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  h8 af[4], bcur[2];
+  u32x4 wc[2];
+  h2 pn[2][4];
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+#define IWQ_MF(I) \
+  acc[(I) >> 1][(I) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[(I) >> 1], bcur[(I) & 1], acc[(I) >> 1][(I) & 1], 0, 0, 0)
+#define IWQ_BSET()                                                                                 \
+  _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                  \
+    bcur[nt] = h8{pn[nt][0].x, pn[nt][0].y, pn[nt][1].x, pn[nt][1].y, pn[nt][2].x, pn[nt][2].y,     \
+                  pn[nt][3].x, pn[nt][3].y};
+  // one slice: step i = MFMA (mt = i / 2, nt = i % 2); before each even step the A fragment mt has
+  // landed (3 newer reads outstanding); after each odd step the rolling read of fragment mt of the
+  // next slice (address NADDR); pair i of the next slice's dequant (code dwords wc[.][S1])
+#define IWQ_SLICE(NADDR, S1)                                                                       \
+  {                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                               \
+      if ((i & 1) == 0) IWQ_LGKM(3);                                                               \
+      IWQ_PIN();                                                                                   \
+      IWQ_MF(i);                                                                                   \
+      if (i & 1) af[i >> 1] = lds_rd<0>((NADDR) + 4096u * (uint32_t)(i >> 1));                     \
+      pn[i >> 2][i & 3] = dqp(wc[i >> 2][S1], i & 3, i >> 2);                                      \
+      IWQ_PIN();                                                                                   \
+    }                                                                                              \
+    IWQ_BSET()                                                                                     \
+  }
+
+  // prologue: stages 0, 1, 2 (K-steps clamped to nk - 1)
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  issue(nk > 2 ? 2 : nk - 1, 2);
+  IWQ_PIN();
+  wc[0] = lds_rd_u<0>(lc);
+  wc[1] = lds_rd_u<1024>(lc);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) af[mt] = lds_rd<0>(la[0] + 4096u * (uint32_t)mt);
+  IWQ_LGKM(0);
+  landed(wc[0]);
+  landed(wc[1]);
+  IWQ_PIN();
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pn[nt][j] = dqp(wc[nt][0], j, nt);
+  IWQ_BSET()
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, 1)
+    IWQ_SLICE(la[2] + so, 2)
+    IWQ_SLICE(la[3] + so, 3)
+    asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
+    const int sd = kt % NSTAGE;
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
+    u32x4 wq[2];
+    wq[0] = lds_rd_u<0>(lc + sn);
+    wq[1] = lds_rd_u<1024>(lc + sn);
+    const uint32_t na = la[0] + sn;
+    // slice 3 of this stage: rolling reads of the next stage's slice 0 (after the 2 code reads),
+    // the refill DMA one piece per step, the next slice's dequant once the codes have landed
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i == 2) {  // code reads older than the one A read issued since
+        IWQ_LGKM(1);
+        landed(wq[0]);
+        landed(wq[1]);
+      }
+      IWQ_PIN();
+      IWQ_MF(i);
+      if (i & 1) af[i >> 1] = lds_rd<0>(na + 4096u * (uint32_t)(i >> 1));
+      if (i < 5) issue1(kd, sd, i);
+      if (i == 2 || i == 3) {
+        const int q = (i - 2) * 2;
+        pn[0][q] = dqp(wq[0][0], q, 0);
+        pn[0][q + 1] = dqp(wq[0][0], q + 1, 0);
+      } else if (i >= 4) {
+        pn[1][i - 4] = dqp(wq[1][0], i - 4, 1);
+      }
+      IWQ_PIN();
+    }
+    IWQ_BSET()
+    wc[0] = wq[0];
+    wc[1] = wq[1];
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, 1)
+    IWQ_SLICE(la[2] + so, 2)
+    IWQ_SLICE(la[3] + so, 3)
+    IWQ_LGKM(0);
+    IWQ_PIN();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) IWQ_MF(i);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_BSET
+#undef IWQ_MF
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 128 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = opaque(acc[mt][nt][r] * sfl[nt]);
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + b);
+      }
+    }
+  }
+}
+
+template <bool NIB>
+hipError_t launch_v(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  hipLaunchKernelGGL((k_w4a16_b32v<NIB>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  return hipGetLastError();
+}
 
 template <bool NIB>
 hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
@@ -1155,7 +1388,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }                                                                             \
     IWQ_PIN();                                                                    \
   }                                                                               \
-  if (!DMA && STG) IWQ_LGKM(5); else IWQ_LGKM(0);
+  if (!DMA && STG) {                                                                              \
+    if constexpr (MT == 8) IWQ_LGKM(4); /* writes at steps 7..13 follow the last read */          \
+    else IWQ_LGKM(5);                   /* all 5 writes follow the reads */                       \
+  } else {                                                                                        \
+    IWQ_LGKM(0);                                                                                  \
+  }
 
   // runtime-j staged write (j is a compile-time constant after unrolling)
 #define IWQ_GWRITE_RT(J, SO)                  \
@@ -1196,6 +1434,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) A0[mt] = lds_rd<0>(la[0] + 4096u * (uint32_t)mt);
   IWQ_LGKM(0);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) landed(wc[nt]);
   IWQ_PIN();
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -1229,6 +1469,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (i == S0) {
         if constexpr (MT == 8) IWQ_LGKM(8);
         else IWQ_LGKM(4);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) landed(wq[nt]);
       }
       if (i >= S0) {
 #pragma unroll
@@ -2037,6 +2279,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 77: return launch_w4h<true, 2>(a, st);   // the same on NIB codes
     case 78: return launch_w4h<false, 1>(a, st);        // 1 x 4 waves of 256 x 64
     case 79: return launch_w4h<false, 2, true>(a, st);  // 2 x 2, LDS-DMA staging (3 stages)
+    case 70: return launch_v<false>(a, st);             // 2 x 4 waves, hand-ordered stream
+    case 71: return launch_v<true>(a, st);              // the same on NIB codes
     case 80: return launch_w4b<false>(a, st);           // 2 x 2, weights dequantized once into LDS
     case 81: return launch_w4b<true>(a, st);            // the same on NIB codes
     default: return launch_w<false>(a, st);

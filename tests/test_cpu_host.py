@@ -193,3 +193,46 @@ def test_tied_weight_detection():
     assert _tied([("d", d), ("e", e)]) == set()
     assert _tied([("f", f), ("d", d), ("e", e)]) == {"d", "e"}
     assert _tied([("d", d), ("e", e), ("f", f)]) == {"f"}
+
+
+def _lint():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "check_lds_waits", os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "check_lds_waits.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_lds_wait_lint_model():
+    """The lint's LDS-queue model: a use of an asm ds_read's registers before a wait that retires
+    it is flagged; counted waits that retire it (writes queued behind it) are not."""
+    L = _lint()
+    ok = ["ds_read_b128 v[4:7], v1 offset:0", "ds_write_b128 v2, v[8:11] offset:0",
+          "s_waitcnt lgkmcnt(1)", "v_mfma_f32_32x32x16_f16 a[0:15], v[4:7], v[12:15], a[0:15]"]
+    assert L.check_kernel(ok) == []
+    early = ["ds_read_b128 v[4:7], v1 offset:0", "ds_write_b128 v2, v[8:11] offset:0",
+             "s_waitcnt lgkmcnt(2)", "v_lshrrev_b32_e32 v20, 8, v5"]
+    assert len(L.check_kernel(early)) == 1
+    # a write retired by the wait does not retire a read issued after it
+    order = ["ds_write_b128 v2, v[8:11] offset:0", "ds_read_b128 v[4:7], v1 offset:0",
+             "s_waitcnt lgkmcnt(1)", "v_mov_b32_e32 v30, v6"]
+    assert len(L.check_kernel(order)) == 1
+
+
+def test_lds_wait_lint_prefill_kernels():
+    """Every hand-ordered prefill kernel (inline-asm LDS access, hand-counted lgkmcnt) as compiled
+    for gfx950: no register of an LDS read is touched before its wait retires it."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not available")
+    L = _lint()
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "p.s")
+        L.compile_asm(out)
+        text = open(out).read()
+    names = L.KERNELS.findall(text)
+    assert len(names) >= 8
+    for name in names:
+        i = text.index(name + ":")
+        assert L.check_kernel(text[i:text.index(".Lfunc_end", i)].split("\n")) == [], name
