@@ -790,13 +790,23 @@ __device__ __forceinline__ void landed(T& v) {
   asm volatile("" : "+v"(v));
 }
 
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_rd_d(uint32_t addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+
 #define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
 
-template <bool NIB>
+// GROUPED (group % 64 == 0): each K-step lies in one group, so a lane needs ONE (s, z) per K-step;
+// they ride with the stage (one more DMA piece per wave, b32e's parameter image) and the dequant
+// applies s per weight (RN16((q - z) s), the reference's fp16 weight; no epilogue scale).
+template <bool NIB, bool GROUPED = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
-  constexpr int STAGE = XS + CS;
-  constexpr int PER_STAGE = 5;
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PER_STAGE = GROUPED ? 6 : 5;
   __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -817,27 +827,41 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   }
   const int ccol = wid * 32 + (lane >> 1);
   const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  // grouped: waves 0-3 stage the scales of columns 64 (wid & 3) + lane, waves 4-7 the zero points
+  // (dword slots col / TN + col of the parameter image, as k_w4a16_b32e)
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
   auto issue = [&](int kt, int stg) {
     uint8_t* base = smem + stg * STAGE;
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
   };
-  // one DMA piece (i < 4: X rows, 4: codes) of K-step kt into stage stg
+  // one DMA piece (i < 4: X rows, 4: codes, 5: parameters) of K-step kt into stage stg
   auto issue1 = [&](int kt, int stg, int i) {
     uint8_t* base = smem + stg * STAGE;
     if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
-    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    else if (i == 4) glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    else if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
   };
 
-  // this lane's column and its per-channel parameters
+  // this lane's column and its parameters (per channel: once; grouped: per K-step, set_params)
   const int col = n0 + wid * 32 + r32;
-  const _Float16 sc = gp<_Float16>(a.scales)[col];
-  const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
-  const float sfl = (float)sc;
-  const h2 zz = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
-  const h2 zl = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
-  const h2 zh = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  float sfl = 1.0f;
+  h2 s2{}, zz{}, zl{}, zh{};
+  auto set_params = [&](_Float16 sc, float zf) {
+    sfl = (float)sc;
+    s2 = h2{sc, sc};
+    zz = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  if constexpr (!GROUPED)
+    set_params(gp<_Float16>(a.scales)[col], a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym);
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
   const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
   const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
@@ -854,18 +878,31 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   for (int s = 0; s < 4; ++s) la[s] = lbase + (uint32_t)(r32 * 128 + (((4 * h + s) ^ xswz(r32)) << 4));
   const int ccl = wid * 32 + r32;
   const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));
+  const uint32_t lp = lbase + XS + CS + (uint32_t)(ccl * 4);  // grouped: scale slot (zero: + 4 TN)
+  uint32_t psv = 0, pzv = 0;                                   // grouped: the raw parameter dwords
+  auto params_landed = [&]() {
+    if constexpr (GROUPED) {
+      landed(psv);
+      landed(pzv);
+      set_params(__builtin_bit_cast(_Float16, (uint16_t)psv),
+                 a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pzv) : a.zsym);
+    }
+  };
 
   // dequant pair j (weights 2j, 2j+1 of the 8 in code dword w), natural k order
   auto dqp = [&](uint32_t w, uint32_t t8, int j) -> h2 {
+    h2 d;
     if constexpr (NIB) {
-      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl;
-      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh;
-      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl;
-      return as_h2(and_or(t8, m1_s, mg54)) - zh;
+      if (j == 0) d = as_h2(and_or(w, m0_s, mg64)) - zl;
+      else if (j == 1) d = as_h2(and_or(w, m1_s, mg54)) - zh;
+      else if (j == 2) d = as_h2(and_or(t8, m0_s, mg64)) - zl;
+      else d = as_h2(and_or(t8, m1_s, mg54)) - zh;
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
-      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz;
+      d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz;
     }
+    if constexpr (GROUPED) d = d * s2;  // RN16((q - z) s)
+    return d;
   };
 
   f16x acc[8];
@@ -908,15 +945,21 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   // prologue: stages 0, 1, 2 (K-steps clamped to nk - 1: re-loads of stages nobody reads again)
   issue(0, 0);
   issue(nk > 1 ? 1 : 0, 1);
-  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  if constexpr (GROUPED) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   issue(nk > 2 ? 2 : nk - 1, 2);
   IWQ_PIN();
   wc = lds_rd_u<0>(lc);
+  if constexpr (GROUPED) {
+    psv = lds_rd_d<0>(lp);
+    pzv = lds_rd_d<TN * 4>(lp);
+  }
   IWQ_RD_A(0, la[0]); IWQ_RD_A(1, la[0]); IWQ_RD_A(2, la[0]); IWQ_RD_A(3, la[0]);
   IWQ_RD_A(4, la[0]); IWQ_RD_A(5, la[0]); IWQ_RD_A(6, la[0]); IWQ_RD_A(7, la[0]);
   IWQ_LGKM(0);
   landed(wc);
+  params_landed();
   IWQ_PIN();
   {
     const uint32_t t8 = NIB ? wc[0] >> 8 : 0u;
@@ -932,13 +975,18 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     // stage kt+1 landed (this wave's part: only stage kt+2's 5 pieces may still fly; near the end
     // those are re-loads of the last K-step into a stage nobody reads again, so the count is
     // constant), every read of stage kt retired
-    asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    if constexpr (GROUPED) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     IWQ_PIN();
     const int kd = kt + 3 < nk ? kt + 3 : nk - 1;  // DMA source K-step (clamped: see above)
     const int sd = kt % NSTAGE;
     const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
     u32x4 wn = lds_rd_u<0>(lc + sn);
+    if constexpr (GROUPED) {  // older than the 4 A reads below: retired by the same lgkmcnt(4)
+      psv = lds_rd_d<0>(lp + sn);
+      pzv = lds_rd_d<TN * 4>(lp + sn);
+    }
     // slice 3 of this stage; rolling reads of the next stage's slice 0; the refill of stage kt
     // spread one DMA piece per MFMA gap (each costs the issuing wave ~60-185 cycles: back to back
     // after the barrier they left the MFMA pipe idle); the next slice's dequant once the code read
@@ -952,8 +1000,9 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     IWQ_PIN(); IWQ_MF(3); IWQ_RD_A(3, na); issue1(kd, sd, 3); IWQ_PIN();
     IWQ_LGKM(4);
     landed(wn);
+    params_landed();
     IWQ_PIN(); IWQ_MF(4); IWQ_RD_A(4, na); issue1(kd, sd, 4); p0 = dqp(wn[0], t8, 0); if (NIB) t8 = wn[0] >> 8; IWQ_PIN();
-    IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, na); p1 = dqp(wn[0], t8, 1); IWQ_PIN();
+    IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, na); if (GROUPED) issue1(kd, sd, 5); p1 = dqp(wn[0], t8, 1); IWQ_PIN();
     IWQ_PIN(); IWQ_MF(6); IWQ_RD_A(6, na); p2 = dqp(wn[0], t8, 2); IWQ_PIN();
     IWQ_PIN(); IWQ_MF(7); IWQ_RD_A(7, na); p3 = dqp(wn[0], t8, 3); IWQ_PIN();
     bcur = h8{p0.x, p0.y, p1.x, p1.y, p2.x, p2.y, p3.x, p3.y};
@@ -981,7 +1030,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = opaque(acc[mt][r] * sfl);
+      const float v = GROUPED ? acc[mt][r] : opaque(acc[mt][r] * sfl);
       if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + bcol);
     }
   }
@@ -1211,10 +1260,10 @@ hipError_t launch_v(const PrefillArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool NIB>
+template <bool NIB, bool GROUPED = false>
 hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
-  hipLaunchKernelGGL((k_w4a16_b32w<NIB>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  hipLaunchKernelGGL((k_w4a16_b32w<NIB, GROUPED>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2227,9 +2276,9 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
   return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || group % TK == 0);
 }
 
-// variants (flags bits 16..23 of iwq_w4a16_gemm, for A/B): 0 default = 74 per channel (1 x 8 waves,
-// hand-ordered stream; +1-5 % over 45 and bit-identical to it, profiles/r02_ab_gemm_w18*.jsonl),
-// 45 grouped (interleaved A/B on the Llama-2-7B shapes at M = 8192, profiles/r02_ab_gemm_*.jsonl);
+// variants (flags bits 16..23 of iwq_w4a16_gemm, for A/B): 0 default = 74 (1 x 8 waves, hand-ordered
+// stream, bit-identical to 45): per channel +1-5 % over 45 (profiles/r02_ab_gemm_w18*.jsonl), grouped
+// (g % 64 == 0) +7-8 % (r02_ab_gemm_b32w_grouped.jsonl; interleaved A/B, Llama-2-7B shapes, M = 8192);
 // 60-69, 74, 75: see DESIGN.md section 5 (round 2); per channel: 40 exact
 // (scale per element), 41 factored, 42 factored + interleave, 43 factored + setprio,
 // 44 exact + interleave, 45 early barrier factored, 46 early barrier exact, 47 / 48 the same on
@@ -2250,7 +2299,9 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
       case 66: return launch_e<true, false, 2, false, true>(a, st);
       case 68: return launch_e<true, false, 2, false, false, true>(a, st);
       case 69: return launch_e<true, false, 2, false, true, true>(a, st);
-      default: return launch_e<true, false>(a, st);
+      case 74: return launch_w<false, true>(a, st);  // 1 x 8 waves, hand-ordered stream
+      case 75: return launch_w<true, true>(a, st);   // the same on NIB codes
+      default: return launch_w<false, true>(a, st);  // 74: +7-8 % over 45 (r02_ab_gemm_b32w_grouped.jsonl)
     }
   }
   switch (variant) {
