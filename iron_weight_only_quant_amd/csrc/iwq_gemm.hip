@@ -1239,20 +1239,22 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     }
     return IWQ_OK;
   } else if (((variant == 0 && M >= 256) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) ||
-              (variant > 81 && variant < 96)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+              (variant > 81 && variant < 97)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel
     // scale factored into the epilogue); the round-1 k_w4a16_big below stays reachable as variant 2.
     // With a workspace and fewer 256 x 256 tiles than CUs it splits K (variant 80 + S forces S ranges).
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     hipError_t e;
-    const int nsplit = (variant == 0 || variant > 81) ? prefill_splitk_count(M, N, K, variant > 81 ? (int)variant - 80 : 0) : 1;
+    // variant 96: the automatic split on the round-2 first split kernel (A/B)
+    const int force = (variant > 81 && variant < 96) ? (int)variant - 80 : 0;
+    const int nsplit = (variant == 0 || variant > 81) ? prefill_splitk_count(M, N, K, force) : 1;
     if (nsplit > 1 && workspace && workspace_bytes >= prefill_splitk_bytes(M, N, nsplit)) {
       p.ws = static_cast<float*>(workspace);
       p.nsplit = nsplit;
-      e = prefill_splitk_launch(p, st);
+      e = prefill_splitk_launch(p, st, variant == 96);
     } else {
-      if (variant > 81) return IWQ_ERR_WORKSPACE;
+      if (variant > 81 && variant < 96) return IWQ_ERR_WORKSPACE;
       e = prefill_b32_launch(p, (int)variant, st);
     }
     if (e != hipSuccess) {

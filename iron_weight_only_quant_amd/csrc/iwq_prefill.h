@@ -40,6 +40,6 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
 // and the launch (partial tiles to a.ws, then one reduce kernel: fixed split order, deterministic)
 int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force);
 int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit);
-hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st);
+hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st, bool legacy = false);
 
 }  // namespace iwq

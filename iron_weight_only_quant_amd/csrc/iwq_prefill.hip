@@ -803,7 +803,9 @@ __device__ __forceinline__ uint32_t lds_rd_d(uint32_t addr) {
 // GROUPED (group % 64 == 0): each K-step lies in one group, so a lane needs ONE (s, z) per K-step;
 // they ride with the stage (one more DMA piece per wave, b32e's parameter image) and the dequant
 // applies s per weight (RN16((q - z) s), the reference's fp16 weight; no epilogue scale).
-template <bool NIB, bool GROUPED = false>
+// SPLIT: one K range of a split-K launch (k_w4a16_b32e's SPLIT: tile / range from blockIdx, the raw
+// accumulators to the workspace in b32e's 2 x 4 wave layout, so k_splitk_reduce is shared).
+template <bool NIB, bool GROUPED = false, bool SPLIT = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
   constexpr int PER_STAGE = GROUPED ? 6 : 5;
@@ -813,9 +815,19 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, h = lane >> 5;
   const int tiles_n = a.N / TN;
-  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  int64_t t;
+  int kbase = 0, nk = a.K / TK, split = 0;
+  if constexpr (SPLIT) {
+    const int64_t tiles = (int64_t)gridDim.x / a.nsplit;
+    const int64_t b = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+    split = (int)(b / tiles);
+    t = b - (int64_t)split * tiles;
+    kbase = split * a.kps;
+    nk = min(a.kps, nk - kbase);  // >= 1 by construction (prefill_splitk_count)
+  } else {
+    t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  }
   const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
-  const int nk = a.K / TK;
   const int64_t crow = a.K / 2;
 
   const _Float16* xsrc[4];
@@ -823,10 +835,10 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int row = (wid * 4 + i) * 8 + (lane >> 3);
     const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
-    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+    xsrc[i] = a.x + (int64_t)gm * a.lda + kbase * TK + (((lane & 7) ^ xswz(row)) << 3);
   }
   const int ccol = wid * 32 + (lane >> 1);
-  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + kbase * (TK / 2) + (((lane & 1) ^ cswz(ccol)) << 4);
   // grouped: waves 0-3 stage the scales of columns 64 (wid & 3) + lane, waves 4-7 the zero points
   // (dword slots col / TN + col of the parameter image, as k_w4a16_b32e)
   const _Float16* psrc = nullptr;
@@ -839,14 +851,14 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+    if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
   };
   // one DMA piece (i < 4: X rows, 4: codes, 5: parameters) of K-step kt into stage stg
   auto issue1 = [&](int kt, int stg, int i) {
     uint8_t* base = smem + stg * STAGE;
     if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     else if (i == 4) glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    else if constexpr (GROUPED) glds2(psrc + (kt * TK) / a.group, base + XS + CS + wid * 256);
+    else if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
   };
 
   // this lane's column and its parameters (per channel: once; grouped: per K-step, set_params)
@@ -1024,6 +1036,17 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 #undef IWQ_MF
 #undef IWQ_RD_A
 
+  if constexpr (SPLIT) {
+    // tile mt of this wave = tile (mt % 4, wid % 2) of b32e's wave (mt / 4) * 4 + wid / 2
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int we = (mt >> 2) * 4 + (wid >> 1);
+      float* dst = a.ws + ((t * a.nsplit + split) * 8 + we) * 8192 + (((mt & 3) * 2 + (wid & 1)) * 16) * 64 + lane;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gp<float>(dst)[r * 64] = acc[mt][r];
+    }
+    return;
+  }
   const float bcol = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) {
@@ -2256,14 +2279,17 @@ int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit) {
   return ((M + TM - 1) / TM) * (N / TN) * (int64_t)nsplit * 65536 * 4;
 }
 
-hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st) {
+hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool legacy) {
   PrefillArgs a = a0;
   const int64_t tiles = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const int nk = a.K / TK;
   a.kps = (nk + a.nsplit - 1) / a.nsplit;
   const dim3 grid((unsigned)(tiles * a.nsplit));
-  if (a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32e<true, false, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
-  else hipLaunchKernelGGL((k_w4a16_b32e<false, true, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  // the partials: 74's hand-ordered kernel (legacy: k_w4a16_b32e, the round-2 first version)
+  if (legacy && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32e<true, false, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  else if (legacy) hipLaunchKernelGGL((k_w4a16_b32e<false, true, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  else if (a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<false, true, true>), grid, dim3(THR), 0, st, a);
+  else hipLaunchKernelGGL((k_w4a16_b32w<false, false, true>), grid, dim3(THR), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const dim3 rgrid((unsigned)tiles, 65536 / 4 / 256);

@@ -889,12 +889,17 @@ def test_w4a16_prefill_splitk(K, M, sym, group):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    for v in (0, 82, 84, 88, 95):
+    ys = {}
+    for v in (0, 82, 84, 88, 95, 96):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (v, float(err.max()))
         y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y2), v
+        ys[v] = y
+    # partials from the hand-ordered kernel (default) and the first split kernel (96): same k order,
+    # same reduce -> same bits
+    assert torch.equal(ys[0], ys[96])
     xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
     for v in (84, 95):
         y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
