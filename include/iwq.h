@@ -70,7 +70,11 @@ enum iwq_status {
 #define IWQ_FLAG_BATCH_CODES 0x100u  /* batched entry: every entry carries out_codes              */
 #define IWQ_FLAG_TILED_CODES 0x200u  /* iwq_w4a16_gemm: codes are in the decode tile layout
                                         (iwq_tile_codes); M <= 16 only                            */
-/* bits 16..23: kernel tuning variant of the batched fp16/g128/asym kernel (0 = default; A/B only) */
+/* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
+ * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
+ * (40-49 / 60-81 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first split-K
+ * kernel; iwq_prefill.hip / iwq_gemm.hip list them).  NIB-layout variants (66, 67, 69, 71, 75, 77,
+ * 81) expect codes repacked so that nibble p of a code dword holds k = (0,2,4,6,1,3,5,7)[p]. */
 #define IWQ_FLAG_VARIANT(v) (((unsigned)(v) & 0xFFu) << 16)
 
 /* Bytes of device workspace iwq_quantize_minmax needs for this problem (0 if none). */
