@@ -1106,7 +1106,7 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
-  if (g <= 0 || K % g != 0 || M < 256 || !prefill_b32_supported(M, N, K, (int)(K / g), (int)g)) return 0;
+  if (g <= 0 || K % g != 0 || !prefill_split_preferred(M, N, K, (int)(K / g), (int)g)) return 0;
   return prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
 }
 
@@ -1158,6 +1158,11 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   a.gshift = (g & (g - 1)) == 0 ? __builtin_ctzll((unsigned long long)g) : -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const unsigned variant = (flags >> 16) & 0xFFu;
+  // default at M > 16: the split-K prefill where it is modelled faster (M >= 256: whenever a split
+  // helps; 16 < M < 256: against the mid-M kernel) and the caller gave the workspace it needs
+  const bool split_pref = variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+                          prefill_split_preferred(M, N, K, a.gpr, a.group) &&
+                          workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
     if (M > 16) return IWQ_ERR_ARG;
     switch (variant) {  // same shapes as the row-major variants of the same number (A/B)
@@ -1224,12 +1229,8 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }
-  } else if (((variant == 0 && M < 512 && !(M >= 256 && workspace &&
-                                            prefill_b32_supported(M, N, K, a.gpr, a.group) &&
-                                            prefill_splitk_count(M, N, K, 0) > 1 &&
-                                            workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0)))) ||
-              (variant >= 50 && variant < 60)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
-             mid_supported(M, N, K, a.gpr, a.group)) {
+  } else if (((variant == 0 && M < 512 && !split_pref) || (variant >= 50 && variant < 60)) &&
+             !(flags & IWQ_FLAG_FORCE_GENERIC) && mid_supported(M, N, K, a.gpr, a.group)) {
     // 16 < M < 512 (M < 256, or no split-K workspace): the weight-streaming mid-M kernel
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     const hipError_t e = mid_launch(p, (int)variant, false, st);
@@ -1238,7 +1239,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
-  } else if (((variant == 0 && M >= 256) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) ||
+  } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) ||
               (variant > 81 && variant < 97)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel

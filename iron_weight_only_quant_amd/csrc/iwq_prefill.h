@@ -41,5 +41,7 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
 int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force);
 int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit);
 hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st, bool legacy = false);
+// split prefill preferred over the mid-M kernel (M >= 256: whenever a split helps)
+bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group);
 
 }  // namespace iwq

@@ -2247,18 +2247,20 @@ static int cu_count() {
 // in ceil(T S / CUs) rounds of ceil(nk / S) K-steps at ~1.4 us each; a split adds the fp32 partial
 // tiles (256 KiB per workgroup, written and read back: ~0.105 us per workgroup at ~5 TB/s) and the
 // reduce launch (~4 us).  The smallest modelled time wins (S = 1 on ties).
+static double splitk_model_us(int64_t tiles, int64_t nk, int64_t c) {
+  const int64_t cus = cu_count();
+  const double t = (double)((tiles * c + cus - 1) / cus) * (double)((nk + c - 1) / c) * 1.4;
+  return c == 1 ? t : t + 4.0 + 0.105 * (double)(tiles * c);
+}
+
 int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force) {
   const int64_t tiles = ((M + TM - 1) / TM) * (N / TN);
   const int64_t nk = K / TK;
-  const int64_t cus = cu_count();
   int64_t s = 1;
   if (force > 1) {
     s = force;
   } else {
-    auto model = [&](int64_t c) {
-      const double t = (double)((tiles * c + cus - 1) / cus) * (double)((nk + c - 1) / c) * 1.4;
-      return c == 1 ? t : t + 4.0 + 0.105 * (double)(tiles * c);
-    };
+    auto model = [&](int64_t c) { return splitk_model_us(tiles, nk, c); };
     double best = model(1);
     for (int64_t c = 2; c <= 32 && c <= nk / 2; ++c) {
       const double tc = model(c);
@@ -2272,6 +2274,21 @@ int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force) {
   if (s < 2) return 1;
   const int64_t kps = (nk + s - 1) / s;
   return (int)((nk + kps - 1) / kps);  // no empty range
+}
+
+// 16 < M < 256: the split 256 x 256 prefill (rows past M computed and dropped) against the mid-M
+// weight-streaming kernel, modelled as ~6 us + 0.45 ns per weight element per 64-row block (fitted
+// to profiles/r02_ab_midm_split.jsonl, M = 64 / 128 / 200 on the Llama-2-7B shapes: the mid kernel
+// wins q_proj up to M = 128, the split kernel gate_proj from M = 128 and everything at M = 200)
+bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group) {
+  if (M <= 16 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
+  const int s = prefill_splitk_count(M, N, K, 0);
+  if (s <= 1) return false;
+  if (M >= 256) return true;
+  const int64_t tiles = ((M + TM - 1) / TM) * (N / TN);
+  const double split_us = splitk_model_us(tiles, K / TK, s);
+  const double mid_us = 6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K;
+  return split_us < mid_us;
 }
 
 int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit) {

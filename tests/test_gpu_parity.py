@@ -872,7 +872,7 @@ def test_w4a16_prefill_b32(K, M, sym, group):
         assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
 
 
-@pytest.mark.parametrize("M", [256, 300, 512, 1024])
+@pytest.mark.parametrize("M", [200, 256, 300, 512, 1024])
 @pytest.mark.parametrize("sym", [False, True])
 @pytest.mark.parametrize("group", [-2, 128])
 def test_w4a16_prefill_splitk(K, M, sym, group):
@@ -898,23 +898,48 @@ def test_w4a16_prefill_splitk(K, M, sym, group):
         assert torch.equal(y, y2), v
         ys[v] = y
     # partials from the hand-ordered kernel (default) and the first split kernel (96): same k order,
-    # same reduce -> same bits
-    assert torch.equal(ys[0], ys[96])
+    # same reduce -> same bits (below M = 256 this small weight takes the mid-M kernel by default)
+    if M >= 256:
+        assert torch.equal(ys[0], ys[96])
     xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
     for v in (84, 95):
         y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, r.out[:, :M].t().contiguous()), v
 
 
+def test_w4a16_midm_split_default(K):
+    """16 < M < 256 on a gate_proj-shaped weight: the default takes the split prefill the model
+    prefers (M = 128: 4 K ranges) -- same bits as forcing 4 ranges, within tolerance of fp32."""
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the modelled split count is for 256 CUs")
+    N, Kd, M = 11008, 4096, 128
+    torch.manual_seed(6)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 97)
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    ref = x.float() @ r.out.float().t()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
+    y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
+    assert torch.equal(y0, y4)
+    assert bool(((y0.float() - ref).abs() <= tol).all())
+
+
 def test_w4a16_splitk_workspace_rule(K):
     """iwq_w4a16_gemm_workspace_bytes: the split the time model picks (iwq_prefill.hip
-    prefill_splitk_count, 256 CUs), sized tiles x ranges x 256 KiB; none below M = 256, where the
-    prefill kernel does not run (N % 256), or where splitting does not pay."""
+    prefill_splitk_count, 256 CUs), sized tiles x ranges x 256 KiB; none where the prefill kernel
+    does not run (N % 256), where splitting does not pay, or (16 < M < 256) where the mid-M kernel
+    is modelled faster (prefill_split_preferred)."""
     lib = K.L.load()
     if torch.cuda.get_device_properties(0).multi_processor_count != 256:
         pytest.skip("expected split counts are for 256 CUs")
     tile = 65536 * 4
-    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 4096, 4096, -2) == 0  # M < 256: mid-M kernel
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 4096, 4096, -2) == 0  # mid-M kernel modelled faster
+    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 0
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 172 * tile  # 43 tiles x 4
+    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 4096, 11008, -2) == 176 * tile  # 16 tiles x 11
+    assert lib.iwq_w4a16_gemm_workspace_bytes(16, 11008, 4096, -2) == 0  # decode GEMV
     assert lib.iwq_w4a16_gemm_workspace_bytes(256, 4096, 4096, -2) == 16 * 8 * tile
     assert lib.iwq_w4a16_gemm_workspace_bytes(512, 4096, 4096, -2) == 32 * 5 * tile
     assert lib.iwq_w4a16_gemm_workspace_bytes(512, 11008, 4096, 128) == 86 * 2 * tile
