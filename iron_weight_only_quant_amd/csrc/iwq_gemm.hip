@@ -330,8 +330,12 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   const int64_t crow = a.K / 2;
   const int arow = r16 < a.M ? r16 : a.M - 1;
   const int xpitch = a.K * 2 + 16;                       // LDS row pitch (bytes), +16 vs bank conflicts
-  const uint8_t* cbase = TILED ? a.codes + (int64_t)(blockIdx.x * T + tile) * nks * 1024 + lane * 16
-                               : a.codes + (int64_t)n * crow + q * 16;
+  // PROBE 2 (A/B only, wrong results): k-major tile order, (kt * tiles + tile) KiB -- at any moment
+  // the chip reads one contiguous window instead of one stream per tile
+  const uint8_t* cbase = PROBE == 2 ? a.codes + (int64_t)(blockIdx.x * T + tile) * 1024 + lane * 16
+                         : TILED ? a.codes + (int64_t)(blockIdx.x * T + tile) * nks * 1024 + lane * 16
+                                 : a.codes + (int64_t)n * crow + q * 16;
+  const int64_t kstride = PROBE == 2 ? (int64_t)(a.N / 16) * 1024 : (TILED ? 1024 : BK / 2);
   const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
   const bool perch = a.gpr == 1;                          // one scale/zero per column: hoisted
 
@@ -346,7 +350,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   u32x4 xa[XLDS ? 1 : PF][4];
   auto load = [&](int j, int u) {
     const int kt = ks + j * S;
-    bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * (TILED ? 1024 : BK / 2)));
+    bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * kstride));
     if (!perch) {
       const int kk = kt * BK + 32 * q;
       const int64_t gi = (int64_t)n * a.gpr + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group);
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
           af = __builtin_bit_cast(h8, pa);
         }
         h8 bf;
-        if constexpr (PROBE == 1) {  // A/B probe only: no dequantization (wrong results)
+        if constexpr (PROBE >= 1) {  // A/B probe only: no dequantization (wrong results)
           const uint32_t w = bc[u][s];
           bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
         } else {
@@ -1184,6 +1188,9 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 23: launch_gemv_ct<3, 8, 2, true>(a, st); break;
       case 24: launch_gemv_ct<1, 8, 4, true>(a, st); break;
       case 100: launch_gemv<2, 8, 1, 1, true>(a, st, true); break;  // probe: no dequant
+      case 102: launch_gemv<2, 8, 1, 2, true>(a, st, true); break;  // probe: k-major order
+      case 103: launch_gemv<2, 16, 1, 2, true>(a, st, true); break;
+      case 104: launch_gemv<2, 16, 1, 1, true>(a, st, true); break;
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
