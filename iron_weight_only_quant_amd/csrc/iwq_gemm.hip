@@ -83,6 +83,16 @@ __device__ __forceinline__ h8 dequant8(uint32_t w, h2 z1024, h2 z64, h2 s, const
   return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
 }
 
+// (q - z) exactly, the per-channel scale factored out into the epilogue (decode kernels, PC)
+__device__ __forceinline__ h8 dequant8_ns(uint32_t w, h2 z1024, h2 z64, const DqConst& c) {
+  const uint32_t w8 = w >> 8;
+  const h2 d0 = as_h2(and_or(w, c.m0, c.k0)) - z1024;
+  const h2 d1 = as_h2(and_or(w, c.m1, c.k1)) - z64;
+  const h2 d2 = as_h2(and_or(w8, c.m0, c.k0)) - z1024;
+  const h2 d3 = as_h2(and_or(w8, c.m1, c.k1)) - z64;
+  return h8{d0.x, d0.y, d1.x, d1.y, d2.x, d2.y, d3.x, d3.y};
+}
+
 __device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
   const int64_t xcd = bid % 8, i = bid / 8;
   const int64_t q = nblocks / 8, r = nblocks % 8;
@@ -316,7 +326,10 @@ constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X imag
 // TILED: codes in the decode tile layout (iwq_tile_codes): the 1 KiB a wave loads for one 128-k
 // step of its 16 columns is contiguous (lane l = 16 q + r at byte 16 l), instead of 16 column rows x
 // 64 B at a K/2 stride -- one DRAM-friendly 1 KiB burst per load instruction.
-template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false>
+// PC (per channel, a.gpr == 1): B = (q - z) exactly and the fp32 result is scaled once in the
+// epilogue, y = RN16(s * sum x (q - z) + b), as the prefill kernels' FACTOR path (4 fewer VALU per
+// 8 weights; A = I still gives W_deq exactly: s (q - z) is exact in fp32)
+template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false, bool PC = false>
 __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   constexpr int WPB = S * T;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
@@ -337,7 +350,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
                                  : a.codes + (int64_t)n * crow + q * 16;
   const int64_t kstride = PROBE == 2 ? (int64_t)(a.N / 16) * 1024 : (TILED ? 1024 : BK / 2);
   const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
-  const bool perch = a.gpr == 1;                          // one scale/zero per column: hoisted
+  constexpr bool perch = PC;                              // one scale/zero per column: hoisted
 
   _Float16 sc0 = (_Float16)0.f, zz0 = (_Float16)0.f;
   if (perch) {
@@ -408,6 +421,8 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
         if constexpr (PROBE >= 1) {  // A/B probe only: no dequantization (wrong results)
           const uint32_t w = bc[u][s];
           bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
+        } else if constexpr (PC) {
+          bf = dequant8_ns(bc[u][s], z1024, z64, dq);
         } else {
           bf = dequant8(bc[u][s], z1024, z64, s2, dq);
         }
@@ -428,6 +443,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < S; ++k) v += red[(k * T + t) * 256 + e];
+      if constexpr (PC) v = opaque(v * (float)gp<_Float16>(a.scales)[col]);  // no fma_mix fold
       if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
       gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
     }
@@ -439,7 +455,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
 // codes (M = 16: 4x the code bytes from L2).  Here each wave applies one A fragment to CT column
 // tiles (CT code loads per k-step, CT accumulators), so X traffic per code byte drops CT-fold.
 // Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits.
-template <int PF, int S, int CT, bool XLDS, bool TILED>
+template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false>
 __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63;
@@ -455,7 +471,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   const uint8_t* cbase = TILED ? a.codes + (int64_t)tile0 * tstride + lane * 16
                                : a.codes + (int64_t)(tile0 * 16 + r16) * crow + q * 16;
   const _Float16* xrow = a.x + (int64_t)arow * a.lda + 32 * q;
-  const bool perch = a.gpr == 1;
+  constexpr bool perch = PC;
 
   _Float16 sc0[CT], zz0[CT];
 #pragma unroll
@@ -538,8 +554,9 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
         }
 #pragma unroll
         for (int c = 0; c < CT; ++c)
-          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
-                                                          acc[c], 0, 0, 0);
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+              af, PC ? dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq) : dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
+              acc[c], 0, 0, 0);
       }
       if (j + PF < nj) load(j + PF, u);
     }
@@ -557,6 +574,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < S; ++k) v += red[(k * CT + c) * 256 + e];
+      if constexpr (PC) v = opaque(v * (float)gp<_Float16>(a.scales)[col]);  // no fma_mix fold
       if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
       gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
     }
@@ -585,28 +603,34 @@ inline int gemv_auto_ct(int64_t M, int64_t N, int64_t K) {
 }
 
 template <int PF, int S, int CT, bool TILED>
-void launch_gemv_ct(const GemmArgs& a, hipStream_t st) {
+void launch_gemv_ct(const GemmArgs& a, hipStream_t st, bool allow_pc = true) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * CT));
   const size_t red = (size_t)S * CT * 256 * 4;
+  const bool pc = a.gpr == 1 && allow_pc;
   if (xbytes <= XLDS_MAX) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
-    hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED>), dim3(blocks), dim3(S * 64), lds, st, a);
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, true>), dim3(blocks), dim3(S * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED>), dim3(blocks), dim3(S * 64), lds, st, a);
   } else {
-    hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED>), dim3(blocks), dim3(S * 64), red, st, a);
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, true>), dim3(blocks), dim3(S * 64), red, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED>), dim3(blocks), dim3(S * 64), red, st, a);
   }
 }
 
 template <int PF, int S, int T, int PROBE = 0, bool TILED = false>
-void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds) {
+void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds, bool allow_pc = true) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * T));
   const size_t red = (size_t)S * T * 256 * 4;
+  const bool pc = a.gpr == 1 && PROBE == 0 && allow_pc;
   if (allow_lds && xbytes <= XLDS_MAX) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
-    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, true>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), lds, st, a);
   } else {
-    hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), red, st, a);
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED, true>), dim3(blocks), dim3(S * T * 64), red, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), red, st, a);
   }
 }
 
@@ -1191,6 +1215,8 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 102: launch_gemv<2, 8, 1, 2, true>(a, st, true); break;  // probe: k-major order
       case 103: launch_gemv<2, 16, 1, 2, true>(a, st, true); break;
       case 104: launch_gemv<2, 16, 1, 1, true>(a, st, true); break;
+      case 25: launch_gemv<2, 8, 1, 0, true>(a, st, true, false); break;  // per-element scale (A/B)
+      case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false); break;
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
