@@ -1134,7 +1134,10 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
-  if (g <= 0 || K % g != 0 || !prefill_split_preferred(M, N, K, (int)(K / g), (int)g)) return 0;
+  if (g <= 0 || K % g != 0) return 0;
+  int ns = 0;
+  if (prefill_short_split(M, N, K, (int)(K / g), (int)g, &ns)) return prefill_splitk_bytes_s(M, N, 2, ns);
+  if (!prefill_split_preferred(M, N, K, (int)(K / g), (int)g)) return 0;
   return prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
 }
 
@@ -1188,7 +1191,11 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   const unsigned variant = (flags >> 16) & 0xFFu;
   // default at M > 16: the split-K prefill where it is modelled faster (M >= 256: whenever a split
   // helps; 16 < M < 256: against the mid-M kernel) and the caller gave the workspace it needs
-  const bool split_pref = variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+  int short_ns = 0;
+  const bool short_pref = variant == 0 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+                          prefill_short_split(M, N, K, a.gpr, a.group, &short_ns) &&
+                          workspace_bytes >= prefill_splitk_bytes_s(M, N, 2, short_ns);
+  const bool split_pref = !short_pref && variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
                           prefill_split_preferred(M, N, K, a.gpr, a.group) &&
                           workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
@@ -1262,11 +1269,28 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }
-  } else if (((variant == 0 && M < 512 && !split_pref) || (variant >= 50 && variant < 60)) &&
+  } else if (((variant == 0 && M < 512 && !split_pref && !short_pref) || (variant >= 50 && variant < 60)) &&
              !(flags & IWQ_FLAG_FORCE_GENERIC) && mid_supported(M, N, K, a.gpr, a.group)) {
     // 16 < M < 512 (M < 256, or no split-K workspace): the weight-streaming mid-M kernel
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     const hipError_t e = mid_launch(p, (int)variant, false, st);
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
+  } else if ((short_pref || (variant >= 110 && variant < 150)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
+             prefill_b32_supported(M, N, K, a.gpr, a.group)) {
+    // short-tile split prefill: the default's plan, or forced for A/B (110-125: 128-row tiles,
+    // 130-145: 64-row tiles, S = v - 108 / v - 128)
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    const int mtw = short_pref ? 2 : (variant < 130 ? 4 : 2);
+    int ns = short_pref ? short_ns : (int)variant - (variant < 130 ? 108 : 128);
+    if (ns > K / 64) ns = (int)(K / 64);
+    if (!workspace || workspace_bytes < prefill_splitk_bytes_s(M, N, mtw, ns)) return IWQ_ERR_WORKSPACE;
+    p.ws = static_cast<float*>(workspace);
+    p.nsplit = ns;
+    const hipError_t e = prefill_splitk_launch_s(p, mtw, st);
     if (e != hipSuccess) {
       iwq::last_hip_error() = (int)e;
       return IWQ_ERR_HIP;

@@ -43,5 +43,10 @@ int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit);
 hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st, bool legacy = false);
 // split prefill preferred over the mid-M kernel (M >= 256: whenever a split helps)
 bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group);
+// short-tile split prefill (k_w4a16_b32s, mtw 2 or 4 tiles of 32 rows per wave)
+int64_t prefill_splitk_bytes_s(int64_t M, int64_t N, int mtw, int nsplit);
+hipError_t prefill_splitk_launch_s(const PrefillArgs& a, int mtw, hipStream_t st);
+// default plan for 16 < M <= 128: the short-tile split (64-row tiles, *ns ranges) or not
+bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns);
 
 }  // namespace iwq

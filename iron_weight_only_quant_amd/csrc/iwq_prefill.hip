@@ -1062,6 +1062,244 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 #undef IWQ_PIN
 
 // ---------------------------------------------------------------------------------------------
+// k_w4a16_b32s: k_w4a16_b32w on SHORT row tiles for prompt-sized M (16 < M <= 128): TMS = 32 MTW
+// rows x 256 columns (MTW = 2 or 4 tiles of 32x32 per wave, 8 waves as 1 x 8), always split along K
+// (the short tile alone would leave most CUs idle), partials in the workspace in this kernel's own
+// layout [tile][split][wave][mt][reg][lane] for k_splitk_reduce_s.  Same hand-ordered stream,
+// staging, swizzles and k order as 74 (fewer MFMAs per K-step: the dequant VALU per MFMA doubles at
+// MTW = 4 and quadruples at MTW = 2).
+// ---------------------------------------------------------------------------------------------
+template <int MTW, bool GROUPED>
+__global__ __launch_bounds__(THR) void k_w4a16_b32s(PrefillArgs a) {
+  static_assert(MTW == 2 || MTW == 4, "64- or 128-row tiles");
+  constexpr int TMS = 32 * MTW;
+  constexpr int XSS = TMS * TK * 2;              // X bytes per stage
+  constexpr int NXP = MTW / 2;                   // X DMA pieces per wave (8 rows x 128 B each)
+  constexpr int STAGE = XSS + CS + (GROUPED ? PS : 0);
+  constexpr int NPC = NXP + 1 + (GROUPED ? 1 : 0);  // DMA pieces per wave per stage
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTAGE * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / TN;
+  const int64_t tiles = (int64_t)gridDim.x / a.nsplit;
+  const int64_t b = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int split = (int)(b / tiles);
+  const int64_t t = b - (int64_t)split * tiles;
+  const int kbase = split * a.kps;
+  const int nk = min(a.kps, a.K / TK - kbase);  // >= 1 by construction
+  const int m0 = (int)(t / tiles_n) * TMS, n0 = (int)(t % tiles_n) * TN;
+  const int64_t crow = a.K / 2;
+
+  const _Float16* xsrc[NXP];
+#pragma unroll
+  for (int i = 0; i < NXP; ++i) {
+    const int row = (wid * NXP + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + kbase * TK + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + kbase * (TK / 2) + (((lane & 1) ^ cswz(ccol)) << 4);
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
+  }
+  // DMA piece i of K-step kt into stage stg: i < NXP X rows, NXP codes, NXP + 1 parameters
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * STAGE;
+    if (i < NXP) glds16(xsrc[i] + kt * TK, base + (wid * NXP + i) * 1024);
+    else if (i == NXP) glds16(csrc + kt * (TK / 2), base + XSS + wid * 1024);
+    else if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XSS + CS + wid * 256);
+  };
+  auto issue = [&](int kt, int stg) {
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) issue1(kt, stg, i);
+  };
+
+  h2 s2{}, zz{};
+  auto set_params = [&](_Float16 sc, float zf) {
+    s2 = h2{sc, sc};
+    zz = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  const int col = n0 + wid * 32 + r32;
+  if constexpr (!GROUPED)
+    set_params(gp<_Float16>(a.scales)[col], a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym);
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  uint32_t magic_v;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[4];
+#pragma unroll
+  for (int s2i = 0; s2i < 4; ++s2i) la[s2i] = lbase + (uint32_t)(r32 * 128 + (((4 * h + s2i) ^ xswz(r32)) << 4));
+  const int ccl = wid * 32 + r32;
+  const uint32_t lc = lbase + XSS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));
+  const uint32_t lp = lbase + XSS + CS + (uint32_t)(ccl * 4);
+  uint32_t psv = 0, pzv = 0;
+  auto params_landed = [&]() {
+    if constexpr (GROUPED) {
+      landed(psv);
+      landed(pzv);
+      set_params(__builtin_bit_cast(_Float16, (uint16_t)psv),
+                 a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pzv) : a.zsym);
+    }
+  };
+  auto dqp = [&](uint32_t w, int j) -> h2 {
+    const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+    h2 d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz;
+    if constexpr (GROUPED) d = d * s2;
+    return d;
+  };
+
+  f16x acc[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  h8 af[MTW];
+  h8 bcur;
+  u32x4 wc;
+  h2 p[4];
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+#define IWQ_MF(MT) acc[MT] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[MT], bcur, acc[MT], 0, 0, 0)
+#define IWQ_BSET() bcur = h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y};
+  // one slice: MFMA mt (its fragment landed: MTW - 1 newer reads outstanding), then the rolling read
+  // of fragment mt of the next slice at NADDR; the next slice's 4 dequant pairs (dword W) spread
+#define IWQ_SLICE(NADDR, W)                                                                        \
+  {                                                                                                \
+    const uint32_t wq = (W);                                                                       \
+    _Pragma("unroll") for (int mt = 0; mt < MTW; ++mt) {                                           \
+      if constexpr (MTW == 4) IWQ_LGKM(3); else IWQ_LGKM(1);                                       \
+      IWQ_PIN();                                                                                   \
+      IWQ_MF(mt);                                                                                  \
+      af[mt] = lds_rd<0>((NADDR) + 4096u * (uint32_t)mt);                                          \
+      _Pragma("unroll") for (int j = 0; j < 4 / MTW; ++j) p[mt * (4 / MTW) + j] = dqp(wq, mt * (4 / MTW) + j); \
+      IWQ_PIN();                                                                                   \
+    }                                                                                              \
+    IWQ_BSET()                                                                                     \
+  }
+
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  if constexpr (NPC == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (NPC == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  issue(nk > 2 ? 2 : nk - 1, 2);
+  IWQ_PIN();
+  wc = lds_rd_u<0>(lc);
+  if constexpr (GROUPED) {
+    psv = lds_rd_d<0>(lp);
+    pzv = lds_rd_d<TN * 4>(lp);
+  }
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt) af[mt] = lds_rd<0>(la[0] + 4096u * (uint32_t)mt);
+  IWQ_LGKM(0);
+  landed(wc);
+  params_landed();
+  IWQ_PIN();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] = dqp(wc[0], j);
+  IWQ_BSET()
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, wc[1])
+    IWQ_SLICE(la[2] + so, wc[2])
+    IWQ_SLICE(la[3] + so, wc[3])
+    if constexpr (NPC == 2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else if constexpr (NPC == 3) asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
+    const int sd = kt % NSTAGE;
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
+    u32x4 wn = lds_rd_u<0>(lc + sn);
+    if constexpr (GROUPED) {
+      psv = lds_rd_d<0>(lp + sn);
+      pzv = lds_rd_d<TN * 4>(lp + sn);
+    }
+    // slice 3: rolling reads of the next stage's slice 0, the refill DMA spread over the steps, the
+    // next slice's dequant once the code / parameter reads (older than the W A reads) have landed
+    constexpr int W = MTW / 2;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) {
+      if (mt == W) {
+        if constexpr (W == 2) IWQ_LGKM(2); else IWQ_LGKM(1);
+        landed(wn);
+        params_landed();
+      }
+      IWQ_PIN();
+      IWQ_MF(mt);
+      af[mt] = lds_rd<0>(la[0] + sn + 4096u * (uint32_t)mt);
+#pragma unroll
+      for (int i = 0; i < NPC; ++i)
+        if (i % MTW == mt) issue1(kd, sd, i);
+      if (mt >= W) {
+#pragma unroll
+        for (int j = 0; j < 4 / (MTW - W); ++j) p[(mt - W) * (4 / (MTW - W)) + j] = dqp(wn[0], (mt - W) * (4 / (MTW - W)) + j);
+      }
+      IWQ_PIN();
+    }
+    IWQ_BSET()
+    wc = wn;
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) % NSTAGE) * STAGE);
+    IWQ_SLICE(la[1] + so, wc[1])
+    IWQ_SLICE(la[2] + so, wc[2])
+    IWQ_SLICE(la[3] + so, wc[3])
+    IWQ_LGKM(0);
+    IWQ_PIN();
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) IWQ_MF(mt);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_BSET
+#undef IWQ_MF
+#undef IWQ_LGKM
+#undef IWQ_PIN
+  float* dst = a.ws + ((t * a.nsplit + split) * 8 + wid) * (MTW * 1024) + lane;
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) gp<float>(dst)[(mt * 16 + r) * 64] = acc[mt][r];
+}
+
+// sum of k_w4a16_b32s's split partials in range order + epilogue (FACTOR: per-channel scale)
+template <bool FACTOR, int MTW>
+__global__ __launch_bounds__(256) void k_splitk_reduce_s(PrefillArgs a) {
+  constexpr int TE = MTW * 8192;  // partial-tile elements
+  const int tiles_n = a.N / TN;
+  const int64_t t = blockIdx.x;
+  const int m0 = (int)(t / tiles_n) * (32 * MTW), n0 = (int)(t % tiles_n) * TN;
+  const int e = (blockIdx.y * 256 + threadIdx.x) * 4;
+  const int wave = e / (MTW * 1024), rem = e % (MTW * 1024);
+  const int mt = rem >> 10, reg = (rem >> 6) & 15, lane0 = rem & 63;
+  const int row = m0 + mt * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane0 >> 5);
+  const int col = n0 + wave * 32 + (lane0 & 31);
+  if (row >= a.M) return;
+  const IWQ_GLOBAL f4* src = gp<f4>(a.ws + (t * a.nsplit) * TE + e);
+  f4 sum = src[0];
+  for (int sp = 1; sp < a.nsplit; ++sp) sum += src[(int64_t)sp * (TE / 4)];
+  _Float16 o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float bb = a.bias ? (float)gp<_Float16>(a.bias)[col + j] : 0.0f;
+    const float v = FACTOR ? opaque(sum[j] * (float)gp<_Float16>(a.scales)[col + j]) : sum[j];
+    o[j] = (_Float16)(v + bb);
+  }
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  *reinterpret_cast<IWQ_GLOBAL u32x2v*>(gp<_Float16>(a.y) + (int64_t)row * a.ldy + col) =
+      u32x2v{as_u32(h2{o[0], o[1]}), as_u32(h2{o[2], o[3]})};
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_w4a16_b32v: k_w4a16_b32w's hand-ordered stream on 8 waves as 2 (M) x 4 (N), 128 rows x 64
 // columns per wave (4 x 2 tiles): half the LDS A reads of the 1 x 8 form (17 instead of 33
 // ds_read_b128 per wave per K-step, each A fragment feeding 2 MFMAs) for twice the dequant VALU
@@ -2291,6 +2529,24 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
   return split_us < mid_us;
 }
 
+// 16 < M <= 128 where the mid kernel's modelled time exceeds ~24 us: the short-tile split (64-row
+// tiles) with S chosen for ~192 workgroups (>= 4 K-steps per range).  Fitted to profiles/
+// r02_ab_gemm_short_split.jsonl (M = 32 / 64 / 128 on the Llama-2-7B shapes: every split form has a
+// ~20 us floor -- two launches and the reduce -- so the mid kernel keeps q_proj; gate / down at
+// M = 64: 39.1 / 31.6 -> 23.2 / 23.7 us, at M = 128: 38.2 / 37.5 -> 28 / 25 us).
+bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out) {
+  if (M <= 16 || M > 128 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
+  const double mid_us = 6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K;
+  if (mid_us < 24.0) return false;
+  const int64_t tiles = ((M + 63) / 64) * (N / TN);
+  const int64_t nk = K / TK;
+  int64_t ns = (192 + tiles / 2) / tiles;
+  if (ns > nk / 4) ns = nk / 4;
+  if (ns < 2) ns = 2;
+  if (ns_out) *ns_out = (int)ns;
+  return true;
+}
+
 int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit) {
   if (nsplit <= 1) return 0;
   return ((M + TM - 1) / TM) * (N / TN) * (int64_t)nsplit * 65536 * 4;
@@ -2312,6 +2568,39 @@ hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool leg
   const dim3 rgrid((unsigned)tiles, 65536 / 4 / 256);
   if (a.gpr != 1) hipLaunchKernelGGL((k_splitk_reduce<false>), rgrid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((k_splitk_reduce<true>), rgrid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// short-tile split (k_w4a16_b32s): MTW 32-row tiles per wave (2 or 4), nsplit K ranges
+int64_t prefill_splitk_bytes_s(int64_t M, int64_t N, int mtw, int nsplit) {
+  return ((M + 32 * mtw - 1) / (32 * mtw)) * (N / TN) * (int64_t)nsplit * (mtw * 8192) * 4;
+}
+
+hipError_t prefill_splitk_launch_s(const PrefillArgs& a0, int mtw, hipStream_t st) {
+  PrefillArgs a = a0;
+  const int64_t tiles = ((int64_t)(a.M + 32 * mtw - 1) / (32 * mtw)) * (a.N / TN);
+  const int nk = a.K / TK;
+  a.kps = (nk + a.nsplit - 1) / a.nsplit;
+  a.nsplit = (nk + a.kps - 1) / a.kps;  // no empty range
+  const dim3 grid((unsigned)(tiles * a.nsplit));
+  const bool grouped = a.gpr != 1;
+  if (mtw == 2) {
+    if (grouped) hipLaunchKernelGGL((k_w4a16_b32s<2, true>), grid, dim3(THR), 0, st, a);
+    else hipLaunchKernelGGL((k_w4a16_b32s<2, false>), grid, dim3(THR), 0, st, a);
+  } else {
+    if (grouped) hipLaunchKernelGGL((k_w4a16_b32s<4, true>), grid, dim3(THR), 0, st, a);
+    else hipLaunchKernelGGL((k_w4a16_b32s<4, false>), grid, dim3(THR), 0, st, a);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const dim3 rgrid((unsigned)tiles, (unsigned)(mtw * 8));
+  if (mtw == 2) {
+    if (grouped) hipLaunchKernelGGL((k_splitk_reduce_s<false, 2>), rgrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_splitk_reduce_s<true, 2>), rgrid, dim3(256), 0, st, a);
+  } else {
+    if (grouped) hipLaunchKernelGGL((k_splitk_reduce_s<false, 4>), rgrid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_splitk_reduce_s<true, 4>), rgrid, dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -429,6 +429,9 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     v = (int(flags) >> 16) & 0xFF
     if 81 < v < 96 and N % 256 == 0:
         ws_bytes = max(ws_bytes, ((M + 255) // 256) * (N // 256) * (v - 80) * 65536 * 4)
+    if 110 <= v < 150 and N % 256 == 0:  # short-tile split (A/B): 128- / 64-row tiles, S ranges
+        mtw, ns = (4, v - 108) if v < 130 else (2, v - 128)
+        ws_bytes = max(ws_bytes, ((M + 32 * mtw - 1) // (32 * mtw)) * (N // 256) * ns * mtw * 8192 * 4)
     ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
     with L.on_device(x.device):
         st = lib.iwq_w4a16_gemm_ws(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),

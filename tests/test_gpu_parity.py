@@ -907,9 +907,37 @@ def test_w4a16_prefill_splitk(K, M, sym, group):
         assert torch.equal(y, r.out[:, :M].t().contiguous()), v
 
 
+@pytest.mark.parametrize("M", [17, 64, 100, 128, 200])
+@pytest.mark.parametrize("group", [-2, 128])
+def test_w4a16_short_tile_split(K, M, group):
+    """Short-tile split prefill (k_w4a16_b32s: 128- / 64-row tiles, variants 110-145 force the tile
+    and the K ranges): within the fp16 tolerance of an fp32 GEMM, deterministic, and A = I picks
+    W_deq^T exactly."""
+    N, Kd = 512, 4352
+    torch.manual_seed(7)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 98)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (110, 112, 117, 130, 132, 140):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        err = (y.float() - ref).abs()
+        assert bool((err <= tol).all()), (v, float(err.max()))
+        y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y2), v
+    xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
+    for v in (112, 132):
+        y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, r.out[:, :M].t().contiguous()), v
+
+
 def test_w4a16_midm_split_default(K):
-    """16 < M < 256 on a gate_proj-shaped weight: the default takes the split prefill the model
-    prefers (M = 128: 4 K ranges) -- same bits as forcing 4 ranges, within tolerance of fp32."""
+    """16 < M < 256 on a gate_proj-shaped weight: the default takes the split the plan prefers
+    (M = 128: the short-tile split, 64-row tiles, 2 K ranges; M = 200: the 256-row split, 4 K
+    ranges) -- same bits as forcing that plan, within tolerance of fp32."""
     if torch.cuda.get_device_properties(0).multi_processor_count != 256:
         pytest.skip("the modelled split count is for 256 CUs")
     N, Kd, M = 11008, 4096, 128
@@ -921,9 +949,13 @@ def test_w4a16_midm_split_default(K):
     ref = x.float() @ r.out.float().t()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
-    y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
+    y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(130))
     assert torch.equal(y0, y4)
     assert bool(((y0.float() - ref).abs() <= tol).all())
+    x2 = (torch.randn(200, Kd, device=DEV) * 0.5).half()
+    z0 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N)
+    z4 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
+    assert torch.equal(z0, z4)
 
 
 def test_w4a16_splitk_workspace_rule(K):
@@ -936,8 +968,11 @@ def test_w4a16_splitk_workspace_rule(K):
         pytest.skip("expected split counts are for 256 CUs")
     tile = 65536 * 4
     assert lib.iwq_w4a16_gemm_workspace_bytes(128, 4096, 4096, -2) == 0  # mid-M kernel modelled faster
-    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 0
-    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 172 * tile  # 43 tiles x 4
+    short = 2 * 8192 * 4  # one 64-row partial tile (prefill_short_split)
+    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 4096, -2) == 0  # mid-M kernel
+    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 43 * 4 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 11008, -2) == 16 * 12 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 86 * 2 * short
     assert lib.iwq_w4a16_gemm_workspace_bytes(200, 4096, 11008, -2) == 176 * tile  # 16 tiles x 11
     assert lib.iwq_w4a16_gemm_workspace_bytes(16, 11008, 4096, -2) == 0  # decode GEMV
     assert lib.iwq_w4a16_gemm_workspace_bytes(256, 4096, 4096, -2) == 16 * 8 * tile

@@ -1,4 +1,4 @@
-"""ISA lint for the hand-ordered prefill kernels (iwq_prefill.hip: k_w4a16_b32w / b32v / w4h / w4b).
+"""ISA lint for the hand-ordered prefill kernels (iwq_prefill.hip: k_w4a16_b32w / b32v / b32s / w4h / w4b).
 
 Those kernels issue their LDS reads and writes as inline asm and count the lgkmcnt waits by hand,
 which the compiler cannot see: a register an asm ds_read fills is only valid once a wait has retired
@@ -19,7 +19,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "iron_weight_only_quant_amd", "csrc")
-KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|w4h|w4b)\w*):", re.M)
+KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b)\w*):", re.M)
 
 
 def compile_asm(out):
