@@ -46,7 +46,7 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 // short-tile split prefill (k_w4a16_b32s, mtw 2 or 4 tiles of 32 rows per wave)
 int64_t prefill_splitk_bytes_s(int64_t M, int64_t N, int mtw, int nsplit);
 hipError_t prefill_splitk_launch_s(const PrefillArgs& a, int mtw, hipStream_t st);
-// default plan for 16 < M <= 128: the short-tile split (64-row tiles, *ns ranges) or not
+// default plan for 16 < M < 256: the short-tile split (64-row tiles, *ns ranges) or not
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns);
 
 }  // namespace iwq

@@ -2529,18 +2529,23 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
   return split_us < mid_us;
 }
 
-// 16 < M <= 128 where the mid kernel's modelled time exceeds ~24 us: the short-tile split (64-row
-// tiles) with S chosen for ~192 workgroups (>= 4 K-steps per range).  Fitted to profiles/
+// 16 < M < 256 where the mid kernel's modelled time exceeds ~24 us: the short-tile split (64-row
+// tiles) with S = floor(256 / tiles) ranges (2..12, >= 4 K-steps each).  Fitted to profiles/
 // r02_ab_gemm_short_split.jsonl (M = 32 / 64 / 128 on the Llama-2-7B shapes: every split form has a
 // ~20 us floor -- two launches and the reduce -- so the mid kernel keeps q_proj; gate / down at
 // M = 64: 39.1 / 31.6 -> 23.2 / 23.7 us, at M = 128: 38.2 / 37.5 -> 28 / 25 us).
+// 128 < M < 256: the short split also wins where it stays under ~128 tiles (q / down: 20 % / 12 %
+// over the 256-row split at M = 160-250, profiles/r02_ab_gemm_short_split_hi.jsonl); wider weights
+// (gate) keep the 256-row split.
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out) {
-  if (M <= 16 || M > 128 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
+  if (M <= 16 || M >= 256 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
   const double mid_us = 6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K;
   if (mid_us < 24.0) return false;
   const int64_t tiles = ((M + 63) / 64) * (N / TN);
+  if (M > 128 && tiles > 128) return false;
   const int64_t nk = K / TK;
-  int64_t ns = (192 + tiles / 2) / tiles;
+  int64_t ns = 256 / tiles;  // at most ~256 workgroups: best or within ~7 % in every sweep
+  if (ns > 12) ns = 12;
   if (ns > nk / 4) ns = nk / 4;
   if (ns < 2) ns = 2;
   if (ns_out) *ns_out = (int)ns;

@@ -970,10 +970,11 @@ def test_w4a16_splitk_workspace_rule(K):
     assert lib.iwq_w4a16_gemm_workspace_bytes(128, 4096, 4096, -2) == 0  # mid-M kernel modelled faster
     short = 2 * 8192 * 4  # one 64-row partial tile (prefill_short_split)
     assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 4096, -2) == 0  # mid-M kernel
-    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 43 * 4 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 43 * 5 * short
     assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 11008, -2) == 16 * 12 * short
     assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 86 * 2 * short
-    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 4096, 11008, -2) == 176 * tile  # 16 tiles x 11
+    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 4096, 11008, -2) == 64 * 4 * short  # short: 4 x 16 tiles
+    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 11008, 4096, -2) == 43 * 4 * tile  # wide: 256-row split
     assert lib.iwq_w4a16_gemm_workspace_bytes(16, 11008, 4096, -2) == 0  # decode GEMV
     assert lib.iwq_w4a16_gemm_workspace_bytes(256, 4096, 4096, -2) == 16 * 8 * tile
     assert lib.iwq_w4a16_gemm_workspace_bytes(512, 4096, 4096, -2) == 32 * 5 * tile
