@@ -2539,7 +2539,8 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 // (gate) keep the 256-row split.
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out) {
   if (M <= 16 || M >= 256 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
-  const double mid_us = 6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K;
+  // grouped scales cost the mid kernel ~1.4x (profiles/r02_ab_gemm_g128_mid.jsonl)
+  const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * (gpr != 1 ? 1.4 : 1.0);
   if (mid_us < 24.0) return false;
   const int64_t tiles = ((M + 63) / 64) * (N / TN);
   if (M > 128 && tiles > 128) return false;
