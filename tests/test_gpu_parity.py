@@ -1018,6 +1018,9 @@ def test_w4a16_prefill_short_k(K, Kd):
     for v in (70, 74, 76, 78, 79, 80):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y45), v
+    for v in (110, 112, 130, 132):  # short-tile splits: 1-3 K-steps per range
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
+        assert bool(((y.float() - ref).abs() <= tol).all()), v
     nib = nib_layout(r.codes, N, Kd)
     for v in (71, 75, 77, 81):
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
