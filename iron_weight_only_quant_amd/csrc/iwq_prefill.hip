@@ -805,7 +805,7 @@ __device__ __forceinline__ uint32_t lds_rd_d(uint32_t addr) {
 // applies s per weight (RN16((q - z) s), the reference's fp16 weight; no epilogue scale).
 // SPLIT: one K range of a split-K launch (k_w4a16_b32e's SPLIT: tile / range from blockIdx, the raw
 // accumulators to the workspace in b32e's 2 x 4 wave layout, so k_splitk_reduce is shared).
-template <bool NIB, bool GROUPED = false, bool SPLIT = false>
+template <bool NIB, bool GROUPED = false, bool SPLIT = false, int EPI = 0>
 __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
   constexpr int PER_STAGE = GROUPED ? 6 : 5;
@@ -1045,6 +1045,15 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) gp<float>(dst)[r * 64] = acc[mt][r];
     }
+    return;
+  }
+  if constexpr (EPI == 9) {  // DIAGNOSTIC (A/B only, wrong results): no output stores
+    float t0 = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t0 += acc[mt][r];
+    if (t0 == 12345.678f) gp<_Float16>(a.y)[col] = (_Float16)t0;
     return;
   }
   const float bcol = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
@@ -2663,6 +2672,11 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 68: return launch_e<false, true, 2, false, false, true>(a, st);  // C^T epilogue
     case 69: return launch_e<false, true, 2, false, true, true>(a, st);   // NIB + C^T epilogue
     case 74: return launch_w<false>(a, st);   // 1 x 8 waves, hand-ordered stream
+    case 72: {  // DIAGNOSTIC: 74 without the output stores (wrong results; epilogue cost)
+      const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+      hipLaunchKernelGGL((k_w4a16_b32w<false, false, false, 9>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+      return hipGetLastError();
+    }
     case 75: return launch_w<true>(a, st);    // 1 x 8 waves, hand-ordered stream, NIB codes
     case 76: return launch_w4h<false, 2>(a, st);  // 2 x 2 waves of 128^2, register-staged, hand-ordered
     case 77: return launch_w4h<true, 2>(a, st);   // the same on NIB codes
