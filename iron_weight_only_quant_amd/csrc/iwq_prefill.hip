@@ -1057,14 +1057,41 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     return;
   }
   const float bcol = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+  if constexpr (EPI == 1) {  // the first epilogue (A/B variant 73): per-store 64-bit address + row check
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
+    for (int mt = 0; mt < 8; ++mt) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float v = GROUPED ? acc[mt][r] : opaque(acc[mt][r] * sfl);
-      if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + bcol);
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = GROUPED ? acc[mt][r] : opaque(acc[mt][r] * sfl);
+        if (row < a.M) gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)(v + bcol);
+      }
     }
+    return;
+  }
+  // the row offset of a store is uniform (tile row x ldy: scalar math, the store's SGPR base); the
+  // lane part (4 h rows + column) is one 32-bit VGPR offset; full tiles skip the row check
+  // (measured: the per-store address math and exec-mask branches were the epilogue's cost)
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;  // row pitch, bytes
+  char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * h) * a.ldy + col) * 2;  // this lane
+  auto out = [&](int mt, int r) {
+    const float v = GROUPED ? acc[mt][r] : opaque(acc[mt][r] * sfl);
+    return (_Float16)(v + bcol);
+  };
+  if (m0 + TM <= a.M) {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        *gp<_Float16>(static_cast<void*>(yl + (int64_t)(mt * 32 + (r & 3) + 8 * (r >> 2)) * ld2)) = out(mt, r);
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = mt * 32 + (r & 3) + 8 * (r >> 2);
+        if (m0 + rr + 4 * h < a.M) *gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2)) = out(mt, r);
+      }
   }
 }
 #undef IWQ_LGKM
@@ -2675,6 +2702,11 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 72: {  // DIAGNOSTIC: 74 without the output stores (wrong results; epilogue cost)
       const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
       hipLaunchKernelGGL((k_w4a16_b32w<false, false, false, 9>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+      return hipGetLastError();
+    }
+    case 73: {  // 74 with the first epilogue (A/B)
+      const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+      hipLaunchKernelGGL((k_w4a16_b32w<false, false, false, 1>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
       return hipGetLastError();
     }
     case 75: return launch_w<true>(a, st);    // 1 x 8 waves, hand-ordered stream, NIB codes
