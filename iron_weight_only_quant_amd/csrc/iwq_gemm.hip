@@ -1296,7 +1296,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
-  } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) ||
+  } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) || variant == 97 ||
               (variant > 81 && variant < 97)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel
@@ -1306,7 +1306,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     hipError_t e;
     // variant 96: the automatic split on the round-2 first split kernel (A/B)
     const int force = (variant > 81 && variant < 96) ? (int)variant - 80 : 0;
-    const int nsplit = (variant == 0 || variant > 81) ? prefill_splitk_count(M, N, K, force) : 1;
+    const int nsplit = (variant == 0 || (variant > 81 && variant < 97)) ? prefill_splitk_count(M, N, K, force) : 1;
     if (nsplit > 1 && workspace && workspace_bytes >= prefill_splitk_bytes(M, N, nsplit)) {
       p.ws = static_cast<float*>(workspace);
       p.nsplit = nsplit;

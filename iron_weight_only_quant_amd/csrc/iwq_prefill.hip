@@ -1069,29 +1069,68 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     }
     return;
   }
-  // the row offset of a store is uniform (tile row x ldy: scalar math, the store's SGPR base); the
-  // lane part (4 h rows + column) is one 32-bit VGPR offset; full tiles skip the row check
-  // (measured: the per-store address math and exec-mask branches were the epilogue's cost)
-  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;  // row pitch, bytes
-  char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * h) * a.ldy + col) * 2;  // this lane
   auto out = [&](int mt, int r) {
     const float v = GROUPED ? acc[mt][r] : opaque(acc[mt][r] * sfl);
     return (_Float16)(v + bcol);
   };
-  if (m0 + TM <= a.M) {
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;  // row pitch, bytes
+  if (EPI != 2 || (a.ldy & 3) || (reinterpret_cast<uintptr_t>(a.y) & 7)) {
+    // default: one 2-B store per value from a per-lane row pointer, the row offsets uniform multiples
+    // of the pitch (scalar), the row check only on the partial last M tile (measured: the first
+    // epilogue's per-store 64-bit address math and exec-mask branches were its cost)
+    char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * h) * a.ldy + col) * 2;
+    if (m0 + TM <= a.M) {
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
+      for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        *gp<_Float16>(static_cast<void*>(yl + (int64_t)(mt * 32 + (r & 3) + 8 * (r >> 2)) * ld2)) = out(mt, r);
-  } else {
+        for (int r = 0; r < 16; ++r)
+          *gp<_Float16>(static_cast<void*>(yl + (int64_t)(mt * 32 + (r & 3) + 8 * (r >> 2)) * ld2)) = out(mt, r);
+    } else {
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
+      for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = mt * 32 + (r & 3) + 8 * (r >> 2);
-        if (m0 + rr + 4 * h < a.M) *gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2)) = out(mt, r);
+        for (int r = 0; r < 16; ++r) {
+          const int rr = mt * 32 + (r & 3) + 8 * (r >> 2);
+          if (m0 + rr + 4 * h < a.M) *gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2)) = out(mt, r);
+        }
+    }
+    return;
+  }
+  // A/B variant 97 (measured 1-2 % SLOWER than the default, profiles/r02_ab_gemm_epilogue.jsonl):
+  // each quad of lanes (4 consecutive columns) transposes its 4 x 4 blocks (rows
+  // 8 g + 4 h + j, j = 0..3, of tile mt) in registers -- two quad DPP exchanges -- so lane i of the
+  // quad holds row 8 g + 4 h + i, 4 consecutive columns: one 8-B store per 4 values instead of four
+  // 2-B stores, from a per-lane row pointer with uniform (scalar) row offsets
+  const int qi = lane & 3;
+  char* yq = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * h + qi) * a.ldy + (col - qi)) * 2;
+  const bool full = m0 + TM <= a.M;
+  typedef uint32_t u32x2s __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint32_t p0 = as_u32(h2{out(mt, 4 * g), out(mt, 4 * g + 1)});      // rows 0, 1 at col qi
+      const uint32_t p1 = as_u32(h2{out(mt, 4 * g + 2), out(mt, 4 * g + 3)});  // rows 2, 3
+      // stage 1 (lanes qi ^ 2): lanes 0, 1 collect rows 0, 1 of cols qi, qi + 2; lanes 2, 3 rows 2, 3
+      const uint32_t snd1 = qi < 2 ? p1 : p0;
+      const uint32_t rcv1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd1, 0x4E, 0xF, 0xF, false);
+      const uint32_t lo = qi < 2 ? p0 : rcv1, hi = qi < 2 ? rcv1 : p1;  // cols qi & 1 / (qi & 1) + 2
+      // stage 2 (lanes qi ^ 1, 16-bit halves): even lanes keep the first row of the pair, odd the second
+      const uint32_t snd2 = (qi & 1) ? __builtin_amdgcn_perm(hi, lo, 0x05040100u)   // (lo.x, hi.x)
+                                     : __builtin_amdgcn_perm(hi, lo, 0x07060302u);  // (lo.y, hi.y)
+      const uint32_t rcv2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)snd2, 0xB1, 0xF, 0xF, false);
+      u32x2s d;
+      if (qi & 1) {  // row qi: c0 = rcv2.x, c1 = lo.y, c2 = rcv2.y, c3 = hi.y
+        d.x = __builtin_amdgcn_perm(lo, rcv2, 0x07060100u);
+        d.y = __builtin_amdgcn_perm(hi, rcv2, 0x07060302u);
+      } else {       // row qi: c0 = lo.x, c1 = rcv2.x, c2 = hi.x, c3 = rcv2.y
+        d.x = __builtin_amdgcn_perm(rcv2, lo, 0x05040100u);
+        d.y = __builtin_amdgcn_perm(rcv2, hi, 0x07060100u);
       }
+      const int rr = mt * 32 + 8 * g;
+      if (full || m0 + rr + 4 * h + qi < a.M)
+        *gp<u32x2s>(static_cast<void*>(yq + (int64_t)rr * ld2)) = d;
+    }
   }
 }
 #undef IWQ_LGKM
@@ -2702,6 +2741,11 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 72: {  // DIAGNOSTIC: 74 without the output stores (wrong results; epilogue cost)
       const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
       hipLaunchKernelGGL((k_w4a16_b32w<false, false, false, 9>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+      return hipGetLastError();
+    }
+    case 97: {  // 74 with the quad-transposed 8-B store epilogue (A/B)
+      const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+      hipLaunchKernelGGL((k_w4a16_b32w<false, false, false, 2>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
       return hipGetLastError();
     }
     case 73: {  // 74 with the first epilogue (A/B)

@@ -822,7 +822,7 @@ def test_w4a16_prefill_big_identity(K):
 # element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
 # The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
-B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80), (47,), (48,))
+B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80, 97), (47,), (48,))
 B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
