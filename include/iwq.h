@@ -248,12 +248,14 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
                    unsigned flags, void* stream);
 
 /*
- * iwq_w4a16_gemm with a caller-provided fp32 workspace (16-B aligned).  For M >= 256 where the
- * prefill kernel's 256 x 256 output tiles leave CUs idle (a time model picks S, see
- * iwq_prefill.hip prefill_splitk_count), K is split into S ranges: each
- * workgroup writes its fp32 partial tile to the workspace and a second kernel sums the S partials in
- * range order (deterministic) and applies scale / bias -- within the fp16 output tolerance of the
- * unsplit kernel, not bit-identical to it.  A NULL or too small workspace runs iwq_w4a16_gemm.
+ * iwq_w4a16_gemm with a caller-provided fp32 workspace (16-B aligned).  Where the prefill kernel's
+ * output tiles would leave CUs idle, K is split into S ranges: each workgroup writes its fp32
+ * partial tile to the workspace and a second kernel sums the S partials in range order
+ * (deterministic) and applies scale / bias -- within the fp16 output tolerance of the unsplit
+ * kernel, not bit-identical to it.  M >= 256: 256 x 256 tiles, S from a time model
+ * (iwq_prefill.hip prefill_splitk_count); 16 < M < 256: 64-row tiles where the mid-M kernel is
+ * modelled slower (prefill_short_split), else the 256-row split where it pays
+ * (prefill_split_preferred).  A NULL or too small workspace runs iwq_w4a16_gemm.
  * iwq_w4a16_gemm_workspace_bytes: the size that enables the split for this problem (0: none needed).
  */
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group);
