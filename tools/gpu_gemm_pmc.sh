@@ -5,6 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"; export TMPDIR=/tmp
 VARS=${VARS:-0,45,47}
 SHAPES=${SHAPES:-"4096x4096 4096x11008"}
+GRPS=${GRPS:--2}   # weight groups to profile, e.g. "-2 128" (per channel and g128)
 if [ -z "$NO_AB" ]; then
   timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" > "$OUT/ab_gemm_pc.jsonl" 2>&1 || exit $?
   timeout -k 10 300 python tools/ab_gemm.py --variants "$VARS" --group 128 > "$OUT/ab_gemm_g128.jsonl" 2>&1 || exit $?
@@ -14,13 +15,15 @@ P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES SQ_WAIT_INST_
 P2="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE"
 for shape in $SHAPES; do
   N=${shape%x*}; K=${shape#*x}
+  for g in $GRPS; do
   for arm in ref $(echo $VARS | tr ',' ' '); do
     if [ $arm = ref ]; then A="--ref"; else A="--variant $arm"; fi
     for p in 1 2; do
       eval C=\$P$p
-      D=$OUT/pmc_${N}x${K}_${arm}_p$p
-      timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $C --output-format csv -d $D -o run -- python3 $ROOT/tools/gemm_pmc.py --n $N --k $K $A > $D.log 2>&1 || { echo "pmc fail $D"; exit 3; }
+      D=$OUT/pmc_${N}x${K}_g${g}_${arm}_p$p
+      timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $C --output-format csv -d $D -o run -- python3 $ROOT/tools/gemm_pmc.py --n $N --k $K --group $g $A > $D.log 2>&1 || { echo "pmc fail $D"; exit 3; }
     done
+  done
   done
 done
 cd $ROOT
