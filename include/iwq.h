@@ -70,6 +70,9 @@ enum iwq_status {
 #define IWQ_FLAG_BATCH_CODES 0x100u  /* batched entry: every entry carries out_codes              */
 #define IWQ_FLAG_TILED_CODES 0x200u  /* iwq_w4a16_gemm: codes are in the decode tile layout
                                         (iwq_tile_codes); M <= 16 only                            */
+#define IWQ_FLAG_NIB_CODES 0x400u    /* iwq_w4a16_gemm: codes are in the NIB layout (iwq_nib_codes);
+                                        M >= 256 only (the prefill kernel and its split-K form);
+                                        IWQ_ERR_ARG with a variant, TILED or FORCE_GENERIC        */
 /* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
  * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
  * (40-49 / 60-81 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first split-K
@@ -270,6 +273,14 @@ int iwq_w4a16_gemm_ws(const void* x, int64_t M, int64_t K, int64_t lda, const vo
  * 64 kt + 16 (l / 16) + i.  N % 16 == 0, K % 128 == 0; out holds N * K / 2 bytes.
  */
 int iwq_tile_codes(const void* codes, int64_t N, int64_t K, void* out, void* stream);
+/* Row-major packed codes (the layout above, [N, K/2] bytes) -> the NIB layout read by iwq_w4a16_gemm
+ * with IWQ_FLAG_NIB_CODES: in every code dword (8 consecutive k of one row) nibble p holds
+ * k = (0,2,4,6,1,3,5,7)[p], so the prefill kernel builds natural-order fp16 pairs with 9 VALU per 8
+ * weights instead of 12 (variants 66 / 75).  A one-time repack at quantize time,
+ * replacing no reference call (the reference keeps no packed codes, quant_linear.py:451-458); the
+ * forward it feeds replaces QuantLinear.forward (quant_linear.py:960-972) at M >= 256.
+ * K % 32 == 0, 16-B aligned codes / out; out may equal codes (in place).  Async on `stream`. */
+int iwq_nib_codes(const void* codes, int64_t N, int64_t K, void* out, void* stream);
 
 /*
  * Packed codes -> fp16 W_deq [N, K] (contiguous: ld_out == K, 16-B aligned), bit-identical to the

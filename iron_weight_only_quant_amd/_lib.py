@@ -24,6 +24,7 @@ IWQ_ERR_WORKSPACE, IWQ_ERR_CODES, IWQ_ERR_HIP, IWQ_ERR_ARG, IWQ_ERR_FORMAT = 6, 
 IWQ_FLAG_FORCE_GENERIC = 0x1
 IWQ_FLAG_BATCH_CODES = 0x100
 IWQ_FLAG_TILED_CODES = 0x200
+IWQ_FLAG_NIB_CODES = 0x400
 
 EXPORTS = (
     "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",
@@ -31,7 +32,7 @@ EXPORTS = (
     "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
     "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
     "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
-    "iwq_dequant_packed", "iwq_quantize_fp_batched", "iwq_tile_codes",
+    "iwq_dequant_packed", "iwq_quantize_fp_batched", "iwq_tile_codes", "iwq_nib_codes",
     "iwq_w4a16_gemm_workspace_bytes", "iwq_w4a16_gemm_ws", "iwq_fp4_grid_packed", "iwq_dequant_fp_packed",
 )
 
@@ -121,6 +122,8 @@ def load():
         lib.iwq_quantize_fp_batched.restype = i32
         lib.iwq_tile_codes.argtypes = [vp, i64, i64, vp, vp]
         lib.iwq_tile_codes.restype = i32
+        lib.iwq_nib_codes.argtypes = [vp, i64, i64, vp, vp]
+        lib.iwq_nib_codes.restype = i32
         lib.iwq_dequant_packed.argtypes = [vp, vp, vp, i32, i64, i64, i64, vp, i64, vp]
         lib.iwq_dequant_packed.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]

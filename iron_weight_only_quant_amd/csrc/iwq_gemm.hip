@@ -647,6 +647,29 @@ __global__ __launch_bounds__(256) void k_tile_codes(const uint8_t* codes, uint8_
   }
 }
 
+// row-major packed codes -> the NIB layout of the prefill kernels (iwq_prefill.hip, variant 75): in
+// every code dword (8 consecutive k) byte j = low nibbles of k = 4j', 4j'+2 ... i.e. nibble p holds
+// k = (0,2,4,6,1,3,5,7)[p].  Per dword: the 4 low nibbles L (k even) and the 4 high nibbles H (k odd)
+// are each compressed from one-per-byte to two-per-byte (x | x >> 4, bytes 0 and 2), L into the low
+// half-dword, H into the high one.  One thread per 16 B; safe in place (each thread reads its own 16 B
+// before writing them).
+__device__ __forceinline__ uint32_t nib_dword(uint32_t w) {
+  const uint32_t l = w & 0x0F0F0F0Fu, h = (w >> 4) & 0x0F0F0F0Fu;
+  const uint32_t pl = l | (l >> 4), ph = h | (h >> 4);
+  return (pl & 0xFFu) | ((pl >> 8) & 0xFF00u) | ((ph & 0xFFu) << 16) | ((ph << 8) & 0xFF000000u);
+}
+
+__global__ __launch_bounds__(256) void k_nib_codes(const uint8_t* codes, uint8_t* out, int64_t nchunks) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks; i += (int64_t)gridDim.x * 256) {
+    u32x4 v = *gp<u32x4>(codes + i * 16);
+    v[0] = nib_dword(v[0]);
+    v[1] = nib_dword(v[1]);
+    v[2] = nib_dword(v[2]);
+    v[3] = nib_dword(v[3]);
+    *gp<u32x4>(out + i * 16) = v;
+  }
+}
+
 // Persistent form of k_w4a16_gemv: the grid is the resident set of workgroups and each one walks
 // column groups c = blockIdx.x, blockIdx.x + gridDim.x, ...  X is staged into LDS ONCE per
 // workgroup, and each wave's code ring runs across column-group boundaries (the first PF steps of
@@ -1095,6 +1118,23 @@ int iwq_tile_codes(const void* codes, int64_t N, int64_t K, void* out, void* str
   return IWQ_OK;
 }
 
+int iwq_nib_codes(const void* codes, int64_t N, int64_t K, void* out, void* stream) {
+  if (!codes || !out) return IWQ_ERR_ARG;
+  if (N <= 0 || K <= 0 || K % 32 != 0) return IWQ_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(codes) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u)) return IWQ_ERR_ARG;
+  const int64_t nchunks = N * (K / 2) / 16;
+  int64_t blocks = (nchunks + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_nib_codes, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(codes), static_cast<uint8_t*>(out), nchunks);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    iwq::last_hip_error() = (int)e;
+    return IWQ_ERR_HIP;
+  }
+  return IWQ_OK;
+}
+
 int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros, int n_bits, int64_t group,
                        int64_t N, int64_t K, void* out, int64_t ld_out, void* stream) {
   if (!codes || !scales || !out) return IWQ_ERR_ARG;
@@ -1198,6 +1238,28 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   const bool split_pref = !short_pref && variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
                           prefill_split_preferred(M, N, K, a.gpr, a.group) &&
                           workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
+  if (flags & IWQ_FLAG_NIB_CODES) {
+    // NIB-layout codes (iwq_nib_codes): the prefill kernel only (74's NIB twin, variant 75, and its
+    // split-K form), M >= 256; every other path reads the row-major layout
+    if ((flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_FORCE_GENERIC)) || variant != 0 || M < 256 ||
+        !prefill_b32_supported(M, N, K, a.gpr, a.group))
+      return IWQ_ERR_ARG;
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    const int nsplit = prefill_splitk_count(M, N, K, 0);
+    hipError_t e;
+    if (nsplit > 1 && workspace && workspace_bytes >= prefill_splitk_bytes(M, N, nsplit)) {
+      p.ws = static_cast<float*>(workspace);
+      p.nsplit = nsplit;
+      e = prefill_splitk_launch(p, st, false, true);
+    } else {
+      e = prefill_b32_launch(p, 75, st);
+    }
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
+  }
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
     if (M > 16) return IWQ_ERR_ARG;
     switch (variant) {  // same shapes as the row-major variants of the same number (A/B)

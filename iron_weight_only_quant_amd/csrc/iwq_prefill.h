@@ -40,7 +40,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
 // and the launch (partial tiles to a.ws, then one reduce kernel: fixed split order, deterministic)
 int prefill_splitk_count(int64_t M, int64_t N, int64_t K, int force);
 int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit);
-hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st, bool legacy = false);
+// nib: codes in the NIB layout (iwq_nib_codes), partials from 74's NIB twin
+hipError_t prefill_splitk_launch(const PrefillArgs& a, hipStream_t st, bool legacy = false, bool nib = false);
 // split prefill preferred over the mid-M kernel (M >= 256: whenever a split helps)
 bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group);
 // short-tile split prefill (k_w4a16_b32s, mtw 2 or 4 tiles of 32 rows per wave)

@@ -2633,7 +2633,7 @@ int64_t prefill_splitk_bytes(int64_t M, int64_t N, int nsplit) {
   return ((M + TM - 1) / TM) * (N / TN) * (int64_t)nsplit * 65536 * 4;
 }
 
-hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool legacy) {
+hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool legacy, bool nib) {
   PrefillArgs a = a0;
   const int64_t tiles = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const int nk = a.K / TK;
@@ -2642,6 +2642,8 @@ hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool leg
   // the partials: 74's hand-ordered kernel (legacy: k_w4a16_b32e, the round-2 first version)
   if (legacy && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32e<true, false, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
   else if (legacy) hipLaunchKernelGGL((k_w4a16_b32e<false, true, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
+  else if (nib && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<true, true, true>), grid, dim3(THR), 0, st, a);
+  else if (nib) hipLaunchKernelGGL((k_w4a16_b32w<true, false, true>), grid, dim3(THR), 0, st, a);
   else if (a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<false, true, true>), grid, dim3(THR), 0, st, a);
   else hipLaunchKernelGGL((k_w4a16_b32w<false, false, true>), grid, dim3(THR), 0, st, a);
   hipError_t e = hipGetLastError();

@@ -363,12 +363,24 @@ GEMV_MAX_M = 16  # iwq_w4a16_gemm takes the weight-streaming decode kernel up to
 # is faster (profiles/r02_ab_gemm_splitk_auto.jsonl vs the dequant pass of r02_gemm_sweep.jsonl:
 # at M = 1024 fused / dequant+hipBLASLt = 1.10 q_proj, 0.96 gate_proj, 0.84 down_proj)
 FUSED_MAX_M = 1024
+# from this many rows the prefill kernel can read NIB-layout codes (nib_codes; iwq_w4a16_gemm with
+# IWQ_FLAG_NIB_CODES): 74's NIB twin (variant 75), +0.5-1.2 % per channel at M = 8192 over the
+# current 74 (+4.5-5 % over the round-2 first 74; profiles/r02_ab_gemm_nib_product.jsonl)
+NIB_MIN_M = 256
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
     g = K if group == -2 else group
     return (x.is_cuda and x.dtype == torch.float16 and 2 <= n_bits <= 4 and N % 128 == 0 and K % 128 == 0
             and g > 0 and g % 32 == 0 and K % g == 0)
+
+
+def nib_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
+    """Shapes the NIB-layout prefill path takes (iwq_w4a16_gemm with IWQ_FLAG_NIB_CODES): N % 256,
+    K % 64, per channel or g % 64 == 0, on top of w4a16_gemm_supported."""
+    g = K if group == -2 else group
+    return (w4a16_gemm_supported(x, N, K, n_bits, group) and N % 256 == 0 and K % 64 == 0
+            and (g == K or g % 64 == 0))
 
 
 def _check_packed(what, dev, codes, scales, zeros, n_bits, group, N, K, bias=None):
@@ -400,12 +412,15 @@ def _check_packed(what, dev, codes, scales, zeros, n_bits, group, N, K, bias=Non
 
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
-               tiled: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+               tiled: bool = False, out: Optional[torch.Tensor] = None, nib: bool = False) -> torch.Tensor:
     """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA).
     tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only.
+    nib: `codes` is in the NIB layout (nib_codes), M >= NIB_MIN_M only (the prefill kernel).
     out: optional contiguous fp16 [M, N] destination (rows of x flattened)."""
     if tiled:
         flags |= L.IWQ_FLAG_TILED_CODES
+    if nib:
+        flags |= L.IWQ_FLAG_NIB_CODES
     L.require_device(x)
     if x.dtype != torch.float16:
         raise TypeError(f"w4a16_gemm: x must be float16, got {x.dtype}")
@@ -425,6 +440,8 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
         y = out.view(M, N)
     # split-K workspace (prefill kernel with fewer 256 x 256 tiles than CUs; variants 82-95 force 2-15
     # K ranges for A/B): fp32 partial tiles, from torch's caching allocator
+    if nib and M < NIB_MIN_M:
+        raise ValueError(f"w4a16_gemm: NIB-layout codes need M >= {NIB_MIN_M} rows, got {M}")
     ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if not tiled else 0
     v = (int(flags) >> 16) & 0xFF
     if 81 < v < 96 and N % 256 == 0:
@@ -455,6 +472,24 @@ def tile_codes(codes: torch.Tensor, N: int, K: int) -> torch.Tensor:
     return out
 
 
+def nib_codes(codes: torch.Tensor, N: int, K: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row-major packed 4-bit codes -> the NIB layout (iwq_nib_codes: nibble p of each code dword holds
+    k = (0,2,4,6,1,3,5,7)[p]) read by w4a16_gemm(..., nib=True) at M >= NIB_MIN_M: the prefill
+    kernel's dequant takes 9 instead of 12 VALU per 8 weights.  out may be `codes` (in place)."""
+    L.require_device(codes)
+    if codes.dtype != torch.uint8 or not codes.is_contiguous() or codes.numel() != N * K // 2 or K % 32:
+        raise ValueError(f"nib_codes: codes must be contiguous uint8 with N*K/2 = {N * K // 2} elements, K % 32 == 0")
+    if out is None:
+        out = torch.empty(N * K // 2, dtype=torch.uint8, device=codes.device)
+    elif out.dtype != torch.uint8 or not out.is_contiguous() or out.numel() != N * K // 2 or out.device != codes.device:
+        raise ValueError("nib_codes: out must be contiguous uint8 of N*K/2 elements on codes' device")
+    lib = L.load()
+    with L.on_device(codes.device):
+        st = lib.iwq_nib_codes(L.ptr(codes), int(N), int(K), L.ptr(out), L.stream_handle(codes.device))
+    _raise_for(st, "iwq_nib_codes")
+    return out.view(codes.shape)
+
+
 def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor], n_bits: int,
                    group: int, N: int, K: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Packed codes -> fp16 W_deq [N, K], bit-identical to the reference's dequantized weight."""
@@ -475,17 +510,22 @@ def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[to
 
 def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                  n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None,
-                 tiled_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 tiled_codes: Optional[torch.Tensor] = None,
+                 nib_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
     decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), the mid-M
     weight-streaming kernel and the split-K prefill kernel up to FUSED_MAX_M rows, dequant-once +
     hipBLASLt (F.linear) above,
-    where the library GEMM on a freshly dequantized weight beats the fused kernels."""
+    where the library GEMM on a freshly dequantized weight beats the fused kernels.
+    nib_codes: the same codes in the NIB layout (nib_codes(codes)), read by the prefill kernel at
+    M >= NIB_MIN_M."""
     K = x.shape[-1]
     M = x.numel() // K
     if M <= FUSED_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
         if tiled_codes is not None and M <= GEMV_MAX_M:
             return w4a16_gemm(x, tiled_codes, scales, zeros, n_bits, group, N, bias, tiled=True)
+        if nib_codes is not None and M >= NIB_MIN_M and nib_supported(x, N, K, n_bits, group):
+            return w4a16_gemm(x, nib_codes, scales, zeros, n_bits, group, N, bias, nib=True)
         return w4a16_gemm(x, codes, scales, zeros, n_bits, group, N, bias)
     w = dequant_packed(codes, scales, zeros, n_bits, group, N, K)
     return torch.nn.functional.linear(x, w, bias)

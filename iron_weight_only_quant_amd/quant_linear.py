@@ -63,7 +63,7 @@ class QuantLinear(nn.Module):
                  double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
                  fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
                  fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, fused_forward: bool = False,
-                 _init_weight: bool = True):
+                 nib_prefill: bool = False, _init_weight: bool = True):
         super().__init__()
         raw_format = weight_format.lower()
         fmt = "bfp" if raw_format.startswith("bfp") else raw_format
@@ -79,7 +79,7 @@ class QuantLinear(nn.Module):
             fp6_hi_align_start=fp6_hi_align_start, fp6_hi_align_exp_field=fp6_hi_align_exp_field,
             fp6_tail_pad_bits=fp6_tail_pad_bits, fp4_hi_align_start=fp4_hi_align_start,
             fp4_hi_align_exp_field=fp4_hi_align_exp_field, fp4_tail_pad_bits=fp4_tail_pad_bits,
-            fused_forward=fused_forward, keep_codes=keep_codes or bool(fused_forward))
+            fused_forward=fused_forward, keep_codes=keep_codes or bool(fused_forward), nib_prefill=nib_prefill)
 
         if _init_weight:
             self.weight = nn.Parameter(torch.Tensor(out_features, in_features))
@@ -93,18 +93,19 @@ class QuantLinear(nn.Module):
         # the reference's buffers (quant_linear.py:451-458), registered without the per-name checks
         self._buffers.update(quantized=torch.tensor(False), scales=None, zeros=None, weight_fp4=None,
                              weight_fp6=None, weight_fp8=None, weight_bfp_mantissa=None,
-                             weight_bfp_exponent=None, qweight=None, qweight_tiled=None)
+                             weight_bfp_exponent=None, qweight=None, qweight_tiled=None,
+                             qweight_nib=None)
         # the packed codes are a derived cache of (weight, scales, zeros), not part of the reference's
         # state: kept out of state_dict (a strict load of a reference checkpoint must match), and
         # dropped whenever a state_dict is loaded so the forward never runs on stale codes
-        self._non_persistent_buffers_set.update(("qweight", "qweight_tiled"))
+        self._non_persistent_buffers_set.update(("qweight", "qweight_tiled", "qweight_nib"))
         self.register_load_state_dict_post_hook(QuantLinear._drop_codes_after_load)
         if _init_weight:
             self.reset_parameters()
 
     @staticmethod
     def _drop_codes_after_load(module, incompatible_keys):
-        module._buffers.update(qweight=None, qweight_tiled=None)
+        module._buffers.update(qweight=None, qweight_tiled=None, qweight_nib=None)
 
     def reset_parameters(self):
         nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
@@ -145,10 +146,19 @@ class QuantLinear(nn.Module):
                     and self.w_bit <= 4 and w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0):
                 # decode batches read the codes in the GEMV tile layout (1 KiB contiguous per load)
                 tiled = kernels.tile_codes(res.codes, w.shape[0], w.shape[1])
+            nib = None
+            if (self.fused_forward is True and self.nib_prefill and res.codes is not None
+                    and self.quant_dim == 0
+                    and 2 <= self.w_bit <= 4 and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0
+                    and (self.w_group_size == -2 or (self.w_group_size > 0 and self.w_group_size % 64 == 0))):
+                # opt-in: prefill batches (M >= 256) read a NIB-layout copy (9 instead of 12 dequant
+                # VALU per 8 weights; +0.5-1.2 % per channel, +-0 g128 at M = 8192, for 0.5 B per
+                # weight more device memory: DESIGN.md section 5)
+                nib = kernels.nib_codes(res.codes, w.shape[0], w.shape[1])
             # registered buffers (see __init__), written without nn.Module.__setattr__'s per-name checks
             self._buffers.update(scales=res.scales.view(-1, 1),
                                  zeros=res.zeros.view(-1, 1) if res.zeros is not None else None,
-                                 qweight=res.codes, qweight_tiled=tiled,
+                                 qweight=res.codes, qweight_tiled=tiled, qweight_nib=nib,
                                  weight_fp4=None, weight_fp6=None, weight_fp8=None)
             self.quantized.fill_(True)
 
@@ -236,6 +246,12 @@ class QuantLinear(nn.Module):
                                           None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                           self.w_group_size, self.out_features, self.bias, tiled=True)
         if fused and self.qweight is not None and self._fused_ok(input):
+            if (self.qweight_nib is not None and input.numel() // self.in_features >= kernels.NIB_MIN_M
+                    and kernels.nib_supported(input, self.out_features, self.in_features, self.w_bit,
+                                              self.w_group_size)):
+                return kernels.w4a16_gemm(input, self.qweight_nib, self.scales.view(-1),
+                                          None if self.zeros is None else self.zeros.view(-1), self.w_bit,
+                                          self.w_group_size, self.out_features, self.bias, nib=True)
             return kernels.w4a16_gemm(input, self.qweight, self.scales.view(-1),
                                       None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                       self.w_group_size, self.out_features, self.bias)
@@ -264,7 +280,7 @@ class QuantLinear(nn.Module):
                     double_approximate: bool = False, fp6_hi_align_start: int = 4, fp6_hi_align_exp_field: int = 7,
                     fp6_tail_pad_bits: int = 2, fp4_hi_align_start: int = 1, fp4_hi_align_exp_field: int = 1,
                     fp4_tail_pad_bits: int = 0, *, keep_codes: bool = False, fused_forward: bool = False,
-                    quantize: bool = True):
+                    nib_prefill: bool = False, quantize: bool = True):
         """quant_linear.py:974-1033.  `quantize=False` is used by the batched model transform,
         which has already quantized the weight in one multi-tensor launch."""
         assert isinstance(linear_layer, nn.Linear), "Input layer must be nn.Linear"
@@ -276,7 +292,7 @@ class QuantLinear(nn.Module):
                 fp6_hi_align_start=fp6_hi_align_start, fp6_hi_align_exp_field=fp6_hi_align_exp_field,
                 fp6_tail_pad_bits=fp6_tail_pad_bits, fp4_hi_align_start=fp4_hi_align_start,
                 fp4_hi_align_exp_field=fp4_hi_align_exp_field, fp4_tail_pad_bits=fp4_tail_pad_bits,
-                keep_codes=keep_codes, fused_forward=fused_forward, _init_weight=False)
+                keep_codes=keep_codes, fused_forward=fused_forward, nib_prefill=nib_prefill, _init_weight=False)
         # aliases the original storage (quant_linear.py:1021-1024); straight into _parameters
         q._parameters["weight"] = nn.Parameter(linear_layer.weight.data.detach(), requires_grad=False)
         if linear_layer.bias is not None:

@@ -84,6 +84,18 @@ def test_decode_entries_host_validation(lib):
     assert gemm(d, 1, 256, 256, d, d, d, 4, 96, 128, None, d, 128, 0, None) == 2       # K % group
     assert gemm(d, 1, 256, 256, d, d, d, 5, 128, 128, None, d, 128, 0, None) == 4     # n_bits
     assert lib.iwq_dequant_packed(d, d, d, 4, 128, 128, 100, d, 100, None) != 0
+    # NIB layout: a prefill-only (M >= 256) format; no variant / tile layout / generic path with it
+    nibf = L.IWQ_FLAG_NIB_CODES
+    assert gemm(d, 255, 256, 256, d, d, d, 4, 128, 256, None, d, 256, nibf, None) == 9
+    assert gemm(d, 256, 256, 256, d, d, d, 4, 128, 256, None, d, 256, nibf | (75 << 16), None) == 9
+    assert gemm(d, 256, 256, 256, d, d, d, 4, 128, 256, None, d, 256, nibf | L.IWQ_FLAG_TILED_CODES, None) == 9
+    assert gemm(d, 256, 256, 256, d, d, d, 4, 128, 256, None, d, 256, nibf | L.IWQ_FLAG_FORCE_GENERIC, None) == 9
+    assert gemm(d, 256, 256, 256, d, d, d, 4, 128, 128, None, d, 128, nibf, None) == 9   # N % 256
+    assert gemm(d, 256, 256, 256, d, d, d, 4, 32, 256, None, d, 256, nibf, None) == 9    # g % 64
+    assert lib.iwq_nib_codes(None, 16, 128, d, None) == 9          # IWQ_ERR_ARG
+    assert lib.iwq_nib_codes(d, 16, 48, d, None) == 1              # K % 32 (IWQ_ERR_SHAPE)
+    assert lib.iwq_nib_codes(d, 0, 128, d, None) == 1
+    assert lib.iwq_nib_codes(d, 16, 128, vp(4100), None) == 9      # 16-B alignment
 
 
 def test_batch_plan_host(lib):

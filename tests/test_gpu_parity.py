@@ -698,6 +698,28 @@ def test_quantlinear_fused_forward(K):
     torch.testing.assert_close(y, ref, rtol=1e-2, atol=2e-3)
 
 
+@pytest.mark.parametrize("group", [-2, 128])
+def test_quantlinear_fused_forward_nib(K, group):
+    """fused_forward=True, nib_prefill=True keeps a NIB-layout copy of the codes (non-persistent,
+    dropped on load) and
+    reads it at M >= 256: the same bits as the row-major codes; below 256 rows the row-major codes."""
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    lin = torch.nn.Linear(1024, 512, bias=False).half().to(DEV)
+    q0 = QuantLinear.from_linear(lin, w_bit=4, w_group_size=group, symmetric=False, fused_forward=True)
+    assert q0.qweight_nib is None  # opt-in
+    q = QuantLinear.from_linear(lin, w_bit=4, w_group_size=group, symmetric=False, fused_forward=True,
+                                nib_prefill=True)
+    assert q.qweight_nib is not None and "qweight_nib" not in q.state_dict()
+    assert torch.equal(q.qweight_nib, K.nib_codes(q.qweight, 512, 1024))
+    z = None if q.zeros is None else q.zeros.view(-1)
+    for shape in ((2, 150, 1024), (100, 1024)):
+        x = torch.randn(*shape, device=DEV).half()
+        ref = K.w4a16_gemm(x, q.qweight, q.scales.view(-1), z, 4, group, 512)
+        assert torch.equal(q(x), ref), shape
+    q.load_state_dict(q.state_dict())
+    assert q.qweight_nib is None
+
+
 @pytest.mark.parametrize("bits,group,sym", [(4, -2, False), (4, 128, False), (4, 128, True), (3, 64, False),
                                             (2, 32, True), (4, 96, False)])
 def test_dequant_packed_bit_exact(K, bits, group, sym):
@@ -870,6 +892,58 @@ def test_w4a16_prefill_b32(K, M, sym, group):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
+
+
+def test_nib_codes_layout(K):
+    """iwq_nib_codes (one HIP pass, in place or not) == the torch restatement of the NIB layout, and
+    decoding it back with the nibble permutation (0,2,4,6,1,3,5,7) returns the row-major codes."""
+    torch.manual_seed(11)
+    for N, Kd in ((256, 4096), (48, 96), (11008, 4096)):
+        codes = torch.randint(0, 256, (N, Kd // 2), dtype=torch.uint8, device=DEV)
+        ref = nib_layout(codes, N, Kd)
+        got = K.nib_codes(codes, N, Kd)
+        assert torch.equal(got, ref), (N, Kd)
+        perm = (0, 2, 4, 6, 1, 3, 5, 7)
+        g32 = got.view(torch.int32).view(N, Kd // 8).cpu().numpy().view("uint32")
+        nib = np.stack([(g32 >> (4 * p)) & 0xF for p in range(8)], axis=-1)
+        back = np.empty_like(nib)
+        back[..., list(perm)] = nib
+        c = codes.cpu().numpy().reshape(N, Kd // 2)
+        rm = np.stack([c & 0xF, c >> 4], axis=-1).reshape(N, Kd // 8, 8)
+        assert np.array_equal(back, rm)
+        inplace = codes.clone()
+        K.nib_codes(inplace, N, Kd, out=inplace)
+        assert torch.equal(inplace, ref)
+
+
+@pytest.mark.parametrize("M", [256, 300, 1024, 4096])
+@pytest.mark.parametrize("group", [-2, 128, 64])
+def test_w4a16_nib_default(K, M, group):
+    """iwq_w4a16_gemm with IWQ_FLAG_NIB_CODES (74's NIB twin, split-K or not by the same rule)
+    returns the default row-major path's bits; below 256 rows the NIB layout is refused."""
+    N, Kd = (2048, 4096) if M == 4096 else (512, 4352)
+    torch.manual_seed(12)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 95)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    nib = K.nib_codes(r.codes, N, Kd)
+    y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
+    y1 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, nib=True)
+    assert torch.equal(y0, y1)
+    # without a workspace the NIB path runs unsplit: 74 vs 75 on the same shapes
+    y74 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(74))
+    y75 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(75))
+    assert torch.equal(y74, y75)
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool(((y1.float() - ref).abs() <= tol).all())
+    with pytest.raises(ValueError):
+        K.w4a16_gemm(x[:255], nib, r.scales, r.zeros, 4, group, N, b, nib=True)
+    if M <= K.FUSED_MAX_M:  # above, w4a16_linear dequantizes once and calls hipBLASLt
+        yl = K.w4a16_linear(x, r.codes, r.scales, r.zeros, 4, group, N, b, nib_codes=nib)
+        assert torch.equal(yl, y0)
 
 
 @pytest.mark.parametrize("M", [200, 256, 300, 512, 1024])

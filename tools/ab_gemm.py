@@ -58,7 +58,12 @@ def main():
         y = torch.empty(a.m, N, dtype=torch.float16, device="cuda")
         arms = {"hipblaslt": lambda: torch.nn.functional.linear(x, r.out)}
         nib = nib_layout(r.codes, N, K)
-        for v in [int(t) for t in a.variants.split(",")]:
+        toks = a.variants.split(",")
+        if "nib" in toks:  # the product NIB path: iwq_nib_codes + IWQ_FLAG_NIB_CODES, default dispatch
+            toks.remove("nib")
+            nc = kernels.nib_codes(r.codes, N, K)
+            arms["nib"] = lambda nc=nc: kernels.w4a16_gemm(x, nc, r.scales, r.zeros, 4, a.group, N, out=y, nib=True)
+        for v in [int(t) for t in toks]:
             fl = kernels.gemm_variant_flags(v)
             cd = nib if v in NIB_VARIANTS else r.codes
             arms[f"v{v}"] = (lambda fl=fl, cd=cd: kernels.w4a16_gemm(x, cd, r.scales, r.zeros, 4, a.group, N,
