@@ -8,14 +8,18 @@ zero_point=True, out-of-place) in ONE persistent multi-tensor launch, writing th
 weights plus fp16 scales/zeros.  Inputs are generated on the device (oracle/synth.py's counter
 generator) and resident in HBM before the timed region.
 
-Multi-GPU (torchrun, one rank per GPU): every rank quantizes its own 7B-sized shard of layers
-(weak scaling, no data-path collective; the layers are independent).
-value = total fp16 input bytes of all ranks / max-over-ranks time.
+Multi-GPU, one rank per GPU: `python bench.py --gpus N` with no WORLD_SIZE in the environment spawns
+N fresh rank processes itself (before any GPU call); under torchrun the ranks come from the
+environment.  The model's 224 (7B) / 560 (70B) weights are bin-packed by bytes over the ranks
+(shard.plan_shards) and every rank quantizes its bin with ONE batched launch: strong scaling, no
+data-path collective (the layers are independent).  value = the model's fp16 input
+bytes / max-over-ranks time.  For the 7B model at N > 1 the weak-scaling figure (every rank
+quantizes a full 7B) is reported beside it ("weak").
 
 Also reported: "roofline" for the quantize kernel (algorithmic bytes / measured HIP-event time vs
-8 TB/s), "traffic" from a committed rocprofv3 PMC summary when present, and "cpu_baseline": the
-reference's CPU arithmetic (oracle/torch_ref.py, pinned to the reference) timed on a bounded
-sample on rank 0.
+8 TB/s), "traffic" from a committed rocprofv3 PMC summary stamped with the kernel sources' hash
+(dropped when the sources changed since), and "cpu_baseline": the reference's CPU arithmetic
+(oracle/torch_ref.py, pinned to the reference) timed on a bounded sample on rank 0.
 """
 import argparse
 import json
@@ -43,10 +47,16 @@ def parse():
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--symmetric", action="store_true")
     ap.add_argument("--model", default="llama2-7b", choices=["llama2-7b", "llama2-70b", "opt-125m"],
-                    help="llama2-7b: every rank quantizes a full 7B set (weak scaling, configs[1]); "
-                         "llama2-70b: the 560 weights are bin-packed over the ranks (strong scaling, configs[3])")
+                    help="the model's Linear weights are bin-packed over the ranks (strong scaling); "
+                         "llama2-7b = configs[1], llama2-70b = configs[3]")
+    ap.add_argument("--weak", action="store_true",
+                    help="headline = weak scaling instead: every rank quantizes the full model")
+    ap.add_argument("--no-weak", action="store_true", help="7B at N > 1: skip the secondary weak-scaling figure")
     ap.add_argument("--gather", action="store_true",
-                    help="also time the all_gather of packed codes+scales to rank 0 (RCCL), reported separately")
+                    help="also time the rooted gather of packed codes+scales to rank 0 (RCCL), reported separately")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank plumbing (spawn, shard plan, rooted gather) over gloo; "
+                         "no GPU, no kernels, no timing")
     ap.add_argument("--scatter", action="store_true",
                     help="strong scaling of the chosen model: its weights start on rank 0 and are scattered to "
                          "their owners over RCCL point-to-point first (timed separately as scatter_ms, never in value)")
@@ -67,24 +77,83 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: start N fresh rank processes of this same command (one
+    per GPU, rendezvous on 127.0.0.1) and return the first failing exit code (0 if all succeed).
+    Nothing here touches the GPU, and the children are new interpreters (no fork of a process
+    with HIP state, no exec).  If a rank fails, the others are stopped by PID, not left waiting in
+    a collective."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def init_dist(args):
+    """Rank setup.  Returns (world, rank, local_rank, n_devices): one rank per GPU over RCCL; with
+    IWQ_DIST_BACKEND=gloo more ranks than GPUs rehearse the multi-rank path on a 1-GPU box (ranks
+    share devices round-robin, and n_devices says so).  --dry-run: gloo on the CPU, no device."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: world size {ws} != --gpus {args.gpus}")
+    if args.dry_run:
+        if ws > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        return ws, rank, local, 0
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1:
+        raise SystemExit("bench.py: no ROCm GPU visible")
     if ws > 1:
         import torch.distributed as dist
-        # one rank per GPU (RCCL); IWQ_DIST_BACKEND=gloo with more ranks than GPUs rehearses the
-        # multi-rank path on a 1-GPU box (ranks share devices round-robin)
         backend = os.environ.get("IWQ_DIST_BACKEND", "nccl")
-        dev = local % max(1, torch.cuda.device_count())
+        if backend == "nccl" and local >= n_dev:
+            raise SystemExit(f"bench.py: rank {rank} needs GPU {local} but only {n_dev} are visible "
+                             "(one rank per GPU over RCCL)")
+        dev = local % n_dev
         torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    return ws, rank, local
+        # distinct devices over all ranks (each rank's device index, gathered)
+        t = torch.tensor([dev], dtype=torch.int64, device=coll_device())
+        devs = [torch.zeros_like(t) for _ in range(ws)]
+        dist.all_gather(devs, t)
+        devs = [int(d.item()) for d in devs]
+        if backend == "nccl" and len(set(devs)) != ws:
+            raise SystemExit(f"bench.py: ranks share GPUs {devs}; one rank per GPU is required over RCCL")
+        return ws, rank, local, len(set(devs))
+    torch.cuda.set_device(0)
+    return ws, rank, local, 1
 
 
 def coll_device():
@@ -107,12 +176,13 @@ def max_over_ranks(x, ws):
     return float(t.item())
 
 
-def make_weights(model, rank, world):
-    """This rank's synthetic weights: the full model per rank (7B, weak scaling) or its bin-packed
-    shard (70B, strong scaling).  Seeds depend on the weight's global index (and rank for 7B)."""
+def make_weights(model, rank, world, weak=False):
+    """This rank's synthetic weights: its bin-packed shard of the model (strong scaling; seeds = the
+    weight's global index, so the union over ranks is the N=1 model) or, weak, a full model per rank
+    (seeds offset by rank)."""
     from iron_weight_only_quant_amd import kernels, shard
     shapes = shard.model_linear_shapes(model)
-    if model == "llama2-70b":
+    if not weak:
         owned = shard.plan_shards(shapes, world)[rank]
         seed_base = 0
     else:
@@ -191,44 +261,144 @@ def ppl_plumbing(bits, group, symmetric, chunks=8, seqlen=2048):
         return {"error": f"{type(e).__name__}: {e}"}
 
 
+def host_cpus():
+    """(usable CPUs, description): the smallest of os.cpu_count(), this process's affinity mask and
+    the cgroup CPU quota (on the GPU box os.cpu_count() is the whole machine while the job's share is
+    a quota), plus the CPU model from /proc/cpuinfo."""
+    n_os = os.cpu_count() or 1
+    try:
+        n_aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n_aff = n_os
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(n for n in (n_os, n_aff, quota) if n)
+    return usable, {"os_cpu_count": n_os, "affinity": n_aff, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
 def cpu_baseline(weights, bits, group, symmetric, budget_s):
-    """Reference CPU arithmetic on whole tensors of the same workload until the budget is spent."""
+    """Reference CPU arithmetic on whole tensors of the same workload until the budget is spent, on
+    every host CPU this job may use (torch intra-op threads = usable CPUs, recorded)."""
     from oracle.torch_ref import minmax_fake_quant_cpu
+    usable, info = host_cpus()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(usable)
     threads = torch.get_num_threads()
     done_bytes, spent, n = 0, 0.0, 0
-    for w in weights:
-        x = w.cpu()
-        t0 = time.perf_counter()
-        minmax_fake_quant_cpu(x, bits, not symmetric, group)
-        spent += time.perf_counter() - t0
-        done_bytes += x.numel() * 2
-        n += 1
-        if spent >= budget_s:
-            break
+    try:
+        for w in weights:
+            x = w.cpu()
+            t0 = time.perf_counter()
+            minmax_fake_quant_cpu(x, bits, not symmetric, group)
+            spent += time.perf_counter() - t0
+            done_bytes += x.numel() * 2
+            n += 1
+            if spent >= budget_s:
+                break
+    finally:
+        torch.set_num_threads(prev)
     return {"value": round(done_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of the 224 Llama-2-7B weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
+            "host": info,
+            "sample": f"{n} of the Llama-2-7B weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
                       f"oracle/torch_ref.py (reference quant_funcs.py:16-38 op sequence, torch CPU, "
-                      f"{threads} threads), {spent:.1f} s"}
+                      f"{threads} threads on {info['cpu_model']}), {spent:.1f} s"}
 
 
 def time_gather(plan, names, all_shapes, args, ws_n):
-    """All_gather of the packed results (codes + scales/zeros) to rank 0 over RCCL, timed alone."""
+    """Rooted gather of the packed results (codes + scales/zeros) to rank 0 over RCCL, timed alone.
+    Returns (ms, bytes received by rank 0)."""
     from iron_weight_only_quant_amd import shard
     import torch.distributed as dist
-    order = sorted(range(len(names)), key=lambda i: names[i])  # gather_to_rank0 unpacks in name order
-    res = shard.ShardResult([names[i] for i in order], [plan.codes[i] for i in order],
-                            [plan.scales[i] for i in order], [plan.zeros[i] for i in order])
+    res = shard.ShardResult(list(names), list(plan.codes), list(plan.scales), list(plan.zeros))
     bins = shard.plan_shards(all_shapes, ws_n)
     names_per_rank = [[all_shapes[i][0] for i in b] for b in bins]
     shp = dict(all_shapes)
     shard.gather_to_rank0(res, shp, names_per_rank, args.bits, args.group, args.symmetric)  # warm
     torch.cuda.synchronize()
     dist.barrier()
+    stats = {}
     t0 = time.perf_counter()
-    shard.gather_to_rank0(res, shp, names_per_rank, args.bits, args.group, args.symmetric)
+    shard.gather_to_rank0(res, shp, names_per_rank, args.bits, args.group, args.symmetric, stats=stats)
     torch.cuda.synchronize()
     dist.barrier()
-    return round((time.perf_counter() - t0) * 1e3, 3)
+    ms = max_over_ranks((time.perf_counter() - t0) * 1e3, ws_n)
+    return round(ms, 3), stats.get("recv_bytes", 0)
+
+
+def dry_run(args, ws_n, rank):
+    """--dry-run: the multi-rank plumbing without a GPU (CPU tests): every rank builds zero-filled
+    packed results of its bin's sizes, the rooted gather moves them to rank 0, and rank 0 prints the
+    bytes that crossed (each non-root bin exactly once) next to the plan's totals."""
+    from iron_weight_only_quant_amd import shard
+    shapes = shard.model_linear_shapes(args.model)
+    bins = shard.plan_shards(shapes, ws_n)
+    mine = bins[rank]
+    nb = lambda shp: shard.packed_nbytes(shp, args.bits, args.group, args.symmetric)  # noqa: E731
+    names, codes, scales, zeros = [], [], [], []
+    for i in mine:
+        name, (r, c) = shapes[i]
+        G = r * c // args.group
+        names.append(name)
+        codes.append(torch.zeros(r * (c // 2) if args.bits <= 4 else r * c, dtype=torch.uint8))
+        scales.append(torch.zeros(G, dtype=torch.float16))
+        zeros.append(None if args.symmetric else torch.zeros(G, dtype=torch.float16))
+    res = shard.ShardResult(names, codes, scales, zeros)
+    sent, recv, got = 0, 0, 0
+    if ws_n > 1:
+        import torch.distributed as dist
+        stats = {}
+        out = shard.gather_to_rank0(res, dict(shapes), [[shapes[i][0] for i in b] for b in bins], args.bits,
+                                    args.group, args.symmetric, stats=stats)
+        t = torch.tensor([stats["sent_bytes"], stats["recv_bytes"]], dtype=torch.int64)
+        dist.all_reduce(t)
+        sent, recv = int(t[0]), int(t[1])
+        got = len(out) if out is not None else 0
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world": ws_n, "model": args.model, "tensors": len(shapes),
+                          "tensors_at_rank0": got,
+                          "plan_packed_bytes_per_rank": [sum(nb(shapes[i][1]) for i in b) for b in bins],
+                          "gather_sent_bytes": sent, "gather_recv_bytes": recv}), flush=True)
+
+
+def kernel_sources_sha():
+    """Hash of the sources that define the headline kernel (k_group): profiles/traffic.json is only
+    trusted while it carries the same hash."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in ("iron_weight_only_quant_amd/csrc/iwq_minmax.hip", "iron_weight_only_quant_amd/csrc/iwq_common.cuh",
+                "include/iwq.h"):
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def committed_traffic(path, numel, bits, group):
+    """HBM bytes per launch from the committed PMC record, if it was measured on this workload AND
+    on the current kernel sources; (bytes or None, reason)."""
+    if not os.path.exists(path):
+        return None, "no PMC record"
+    try:
+        tf = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "unreadable PMC record"
+    if tf.get("workload_numel") != numel or tf.get("bits") != bits or tf.get("group") != group:
+        return None, "PMC record is for another workload"
+    if tf.get("kernel_sources_sha") != kernel_sources_sha():
+        return None, "PMC record predates the current kernel sources"
+    return tf.get("hbm_bytes_per_launch"), "profiles/traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE, same sources)"
 
 
 def clock_ramp(plan, seconds):
@@ -242,21 +412,35 @@ def clock_ramp(plan, seconds):
         torch.cuda.synchronize()
 
 
-def copy_ceiling(plan, steps=5):
-    """In-run ceiling: a plain 16-B non-temporal copy of the same bytes (read w, write out; in place:
-    w onto itself, which leaves the values unchanged), same grid shape policy (probe variant 100).
-    Overwrites plan.outs; call before the timed warmup."""
+CEILING_PROBES = {100: "copy, nt 16-B load + nt store, grid-stride",
+                  101: "copy, plain 16-B load + store, grid-stride",
+                  102: "copy, 4 x 16 B in flight per lane (nt), grid-stride",
+                  118: "k_group's own walk and load/store stream, no arithmetic (same grid, same units)"}
+
+
+def copy_ceiling(plan, steps=5, rounds=3):
+    """In-run ceiling for a read+write stream of the same bytes: the best of several copy forms
+    (read w, write out; in place: w onto itself, values unchanged), interleaved over `rounds`.
+    The kernel's achieved rate is compared with the BEST of them.  Overwrites plan.outs; call before
+    the timed warmup."""
     stream = torch.cuda.current_stream()
-    plan.run(stream, variant=100)
+    nbytes = plan.numel * 4
+    best = {}
+    for v in CEILING_PROBES:
+        plan.run(stream, variant=v)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(steps):
-        plan.run(stream, variant=100)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
-    return round(plan.numel * 4 / (ms / 1e3) / 1e9, 1)
+    for _ in range(rounds):
+        for v in CEILING_PROBES:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(steps):
+                plan.run(stream, variant=v)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / steps
+            best[v] = min(best.get(v, ms), ms)
+    forms = {CEILING_PROBES[v]: round(nbytes / (ms / 1e3) / 1e9, 1) for v, ms in best.items()}
+    return {"GBps": max(forms.values()), "forms": forms}
 
 
 def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
@@ -372,32 +556,13 @@ def ab_variants(plan, variants, args):
               file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
-    ws_n, rank, _ = init_dist(args)
-    from iron_weight_only_quant_amd import kernels
-
-    strong = args.model == "llama2-70b" or args.scatter  # --scatter: the model is partitioned, not replicated
-    if strong:
-        args.inplace = True  # 70B fp16 = 137 GB: in place (QuantLinear semantics) so N=1 fits in 288 GB
-    scatter_ms = None
-    if args.scatter and ws_n > 1:
-        weights, names, all_shapes, scatter_ms = scatter_weights(args.model, rank, ws_n)
-    else:
-        weights, names, all_shapes = make_weights(args.model, rank, ws_n)
-    numel = sum(w.numel() for w in weights)
-    plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric,
-                             outs=weights if args.inplace else None, want_codes=args.gather)
-    stream = torch.cuda.current_stream()
-    if args.variants:
-        ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
-    clock_ramp(plan, args.ramp_seconds)
-    ceiling = copy_ceiling(plan)
+def timed_steps(plan, args, ws_n, stream):
+    """W untimed warmup steps, then EXACTLY K steps bracketed by barrier + synchronize on both sides.
+    Returns (kernel ms per launch from HIP events on the launch stream, max-over-ranks wall ms per step)."""
     for _ in range(args.warmup):
-        plan.run(variant=args.variant)
+        plan.run(stream, variant=args.variant)
     torch.cuda.synchronize()
     assert plan.nan_flag.item() == 0
-
     barrier(ws_n)
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -410,44 +575,101 @@ def main():
     torch.cuda.synchronize()
     barrier(ws_n)
     wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
-    wall_max = max_over_ranks(wall, ws_n)
-    ms_per_step = wall_max / args.steps * 1e3
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    return kernel_ms, max_over_ranks(wall, ws_n) / args.steps * 1e3
+
+
+def all_ranks_sum(x, ws_n):
+    if ws_n == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.int64, device=coll_device())
+    dist.all_reduce(t)
+    return int(t.item())
+
+
+def weak_secondary(args, ws_n, rank):
+    """7B at N > 1: every rank quantizes a full 7B (weak scaling), timed like the headline."""
+    from iron_weight_only_quant_amd import kernels
+    weights, _, _ = make_weights(args.model, rank, ws_n, weak=True)
+    plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
+    stream = torch.cuda.current_stream()
+    clock_ramp(plan, 0.2)
+    kernel_ms, ms = timed_steps(plan, args, ws_n, stream)
+    total = all_ranks_sum(plan.numel, ws_n)
+    del plan, weights
+    torch.cuda.empty_cache()
+    return {"scaling": "weak", "value": round(total * 2 / (ms / 1e3) / 1e9, 2), "ms_per_step": round(ms, 4),
+            "kernel_ms_rank0": round(kernel_ms, 4), "fp16_weights_total": total,
+            "workload": f"every rank quantizes all {len(make_shapes(args.model))} Linear weights of "
+                        f"{MODEL_NAME[args.model]}"}
+
+
+def make_shapes(model):
+    from iron_weight_only_quant_amd import shard
+    return shard.model_linear_shapes(model)
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    ws_n, rank, _, n_dev = init_dist(args)
+    if args.dry_run:
+        dry_run(args, ws_n, rank)
+        if ws_n > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    from iron_weight_only_quant_amd import kernels
+
+    weak = args.weak
+    # 70B fp16 = 137 GB: in place (QuantLinear semantics) so N=1 fits in 288 GB; --scatter likewise
+    if args.model == "llama2-70b" or args.scatter:
+        args.inplace = True
+    scatter_ms = None
+    if args.scatter and ws_n > 1:
+        weak = False
+        weights, names, all_shapes, scatter_ms = scatter_weights(args.model, rank, ws_n)
+    else:
+        weights, names, all_shapes = make_weights(args.model, rank, ws_n, weak=weak)
+    numel = sum(w.numel() for w in weights)
+    plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric,
+                             outs=weights if args.inplace else None, want_codes=args.gather)
+    stream = torch.cuda.current_stream()
+    if args.variants:
+        ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
+    clock_ramp(plan, args.ramp_seconds)
+    ceiling = copy_ceiling(plan) if ws_n == 1 else None
+    kernel_ms, ms_per_step = timed_steps(plan, args, ws_n, stream)
 
     other = None
-    if not strong:
+    if ws_n == 1 and not args.inplace:
         other = other_placement_kernel(weights, plan, args)
 
     shapes_rec = None
-    if not args.no_shapes and not strong:
+    if not args.no_shapes and ws_n == 1 and not args.inplace:
         shapes_rec = per_shape(plan, names, ws_n, args)
 
-    gather_ms = None
+    gather_ms, gather_bytes = None, None
     if args.gather and ws_n > 1:
-        gather_ms = time_gather(plan, names, all_shapes, args, ws_n)
+        gather_ms, gather_bytes = time_gather(plan, names, all_shapes, args, ws_n)
 
-    total_numel = numel
-    if ws_n > 1:
-        import torch.distributed as dist
-        t = torch.tensor([numel], dtype=torch.int64, device=coll_device())
-        dist.all_reduce(t)
-        total_numel = int(t.item())
-    in_bytes = numel * 2
+    total_numel = all_ranks_sum(numel, ws_n)
     groups = numel // args.group
     alg_bytes = numel * 2 + numel * 2 + groups * 2 * (1 if args.symmetric else 2)  # read w, write deq, s(,z)
     if args.gather:
         alg_bytes += numel // 2 if args.bits <= 4 else numel  # packed codes written too
     value = total_numel * 2 / (ms_per_step / 1e3) / 1e9
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = committed_traffic(args.traffic_file, numel, args.bits, args.group)
 
-    traffic = None
-    if os.path.exists(args.traffic_file):
-        try:
-            tf = json.load(open(args.traffic_file))
-            if tf.get("workload_numel") == numel and tf.get("bits") == args.bits and tf.get("group") == args.group:
-                traffic = tf.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    weak_rec = None
+    if ws_n > 1 and not weak and args.model == "llama2-7b" and not args.no_weak and not args.scatter:
+        del plan
+        weights = None
+        torch.cuda.empty_cache()
+        weak_rec = weak_secondary(args, ws_n, rank)
 
     cpu = None
     if rank == 0 and ws_n == 1 and not args.no_cpu_baseline:
@@ -458,31 +680,38 @@ def main():
         ppl = ppl_plumbing(args.bits, args.group, args.symmetric)
 
     if rank == 0:
+        placement = "in-place" if args.inplace else "out-of-place"
+        if weak:
+            workload = f"{MODEL_NAME[args.model]} all {len(all_shapes)} Linear weights on every GPU "
+        else:
+            workload = f"{MODEL_NAME[args.model]} {len(all_shapes)} Linear weights bin-packed over {ws_n} GPU(s) "
         rec = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": ws_n, "steps": args.steps,
+            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": n_dev, "ranks": ws_n,
+            "n_devices": n_dev, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": (f"{MODEL_NAME[args.model]} {len(all_shapes)} Linear weights bin-packed over "
-                                    f"{ws_n} GPU(s) " if strong else
-                                    f"{MODEL_NAME[args.model]} all {len(weights)} Linear weights per GPU ")
-                                   + f"({total_numel} fp16 weights total), INT{args.bits} g={args.group} "
+            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "config": {"workload": workload + f"({total_numel} fp16 weights in all), INT{args.bits} g={args.group} "
                                    f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
-                                   f"{'in-place' if args.inplace else 'out-of-place'} dequant + scales/zeros, "
-                                   f"one batched launch per step",
+                                   f"{placement} dequant + scales/zeros, one batched launch per rank per step",
                        "model": args.model, "bits": args.bits, "group": args.group,
                        "parallelism": f"layer-shard x{ws_n} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_group<f16,128,asym,batched>", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes, "in_run_copy_ceiling_GBps": ceiling,
+                         "alg_bytes_per_launch": alg_bytes, "ceiling": ceiling,
+                         "kernel_over_ceiling": (round(alg_bytes / (kernel_ms / 1e3) / 1e9 / ceiling["GBps"], 4)
+                                                 if ceiling else None),
                          "other_placement": other},
             "shapes": shapes_rec,
+            "weak": weak_rec,
             "cpu_baseline": cpu,
             "ppl_delta": None,
             "ppl_plumbing": ppl,
-            "gather_ms": gather_ms,
+            "gather_ms": gather_ms, "gather_bytes_to_rank0": gather_bytes,
             "scatter_ms": scatter_ms,
         }
+        if n_dev < ws_n:
+            rec["note"] = f"{ws_n} ranks shared {n_dev} GPU(s) (gloo rehearsal): one GPU's bandwidth, not a scaling point"
         print(json.dumps(rec), flush=True)
     if ws_n > 1:
         import torch.distributed as dist

@@ -125,6 +125,29 @@ int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entr
                                 unsigned flags, void* stream);
 
 /*
+ * Batched form for EVERY group mode (the RTN loop of quant_wrapper.py:52-82 for per-channel -2,
+ * per-tensor -1, quant_dim 1, and groups outside 8..512 powers of two); each tensor gets the bits
+ * of its own iwq_quantize_minmax call.  Contiguous weights, 1 <= n_bits <= 8 (2 symmetric).
+ *   iwq_batch_plan_ex  validates the host table and fills unit_begin in the mode's work items:
+ *     group 8..512 pow2, quant_dim 0  -> iwq_batch_plan (512-element units, ONE launch)
+ *     quant_dim 0, other group / -2   -> one wavefront per group of L = group (or cols) elements,
+ *                                        L % 8 == 0, L <= 16384, (cols * elem) % 16 == 0; every
+ *                                        entry of one table must share L (bucket by L; *h_group_len)
+ *     quant_dim 1 (group > 0 or -2)   -> blocks of each entry's column grid, cols % 8 == 0
+ *     -1 per-tensor                   -> 512-element units, rows * cols % 8 == 0; needs a workspace
+ *                                        of iwq_batch_workspace_bytes (one (min, max) key pair per
+ *                                        entry); three launches: key init, reduce, apply
+ *   iwq_quantize_minmax_batched_ex  launches it (group_len: *h_group_len of the plan).
+ */
+int iwq_batch_plan_ex(iwq_batch_entry* h_entries, int32_t n_entries, int dtype, int n_bits, int64_t group,
+                      int quant_dim, int64_t* h_total_units, int64_t* h_group_len);
+int64_t iwq_batch_workspace_bytes(int32_t n_entries, int64_t group, int quant_dim);
+int iwq_quantize_minmax_batched_ex(const iwq_batch_entry* d_entries, int32_t n_entries, int64_t total_units,
+                                   int64_t group_len, int dtype, int n_bits, int64_t group, int symmetric,
+                                   int quant_dim, void* workspace, int64_t workspace_bytes, uint32_t* nan_flag,
+                                   unsigned flags, void* stream);
+
+/*
  * FP4/FP6/FP8 weight formats (QuantLinear FP branches, quant_linear.py:724-883), fp16 weights only.
  * exp_bits/mant_bits as configure_fp_formats (quant_linear.py:84-110): E2M1 / E3M2 / E4M3 defaults.
  * symmetric 1: absmax / fp_max scales, no zeros; 0: mid-point zeros and half-span scales.
@@ -258,7 +281,10 @@ int iwq_w4a16_gemm(const void* x, int64_t M, int64_t K, int64_t lda, const void*
  * kernel, not bit-identical to it.  M >= 256: 256 x 256 tiles, S from a time model
  * (iwq_prefill.hip prefill_splitk_count); 16 < M < 256: 64-row tiles where the mid-M kernel is
  * modelled slower (prefill_short_split), else the 256-row split where it pays
- * (prefill_split_preferred).  A NULL or too small workspace runs iwq_w4a16_gemm.
+ * (prefill_split_preferred).  A NULL or too small workspace runs iwq_w4a16_gemm; so does a workspace
+ * that is not 16-B aligned, or a y that is not 8-B aligned or whose ldy is not a multiple of 4 (the
+ * split reduces store 4 outputs at a time).  From M = 256 with a workspace the prefill kernel runs
+ * even when the model picks one range (same bits as the IWQ_FLAG_NIB_CODES path).
  * iwq_w4a16_gemm_workspace_bytes: the size that enables the split for this problem (0: none needed).
  */
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group);

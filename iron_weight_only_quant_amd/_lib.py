@@ -34,6 +34,7 @@ EXPORTS = (
     "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
     "iwq_dequant_packed", "iwq_quantize_fp_batched", "iwq_tile_codes", "iwq_nib_codes",
     "iwq_w4a16_gemm_workspace_bytes", "iwq_w4a16_gemm_ws", "iwq_fp4_grid_packed", "iwq_dequant_fp_packed",
+    "iwq_batch_plan_ex", "iwq_batch_workspace_bytes", "iwq_quantize_minmax_batched_ex",
 )
 
 IWQ_CODEC_FP, IWQ_CODEC_GRID, IWQ_CODEC_APX, IWQ_CODEC_APX_DOUBLE = 0, 1, 2, 3
@@ -79,6 +80,14 @@ def load():
         lib.iwq_batch_plan.restype = i32
         lib.iwq_quantize_minmax_batched.argtypes = [vp, ctypes.c_int32, i64, i32, i32, i64, i32, vp, u32, vp]
         lib.iwq_quantize_minmax_batched.restype = i32
+        lib.iwq_batch_plan_ex.argtypes = [ctypes.POINTER(IwqBatchEntry), ctypes.c_int32, i32, i32, i64, i32,
+                                          ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        lib.iwq_batch_plan_ex.restype = i32
+        lib.iwq_batch_workspace_bytes.argtypes = [ctypes.c_int32, i64, i32]
+        lib.iwq_batch_workspace_bytes.restype = i64
+        lib.iwq_quantize_minmax_batched_ex.argtypes = [vp, ctypes.c_int32, i64, i64, i32, i32, i64, i32, i32, vp, i64,
+                                                       vp, u32, vp]
+        lib.iwq_quantize_minmax_batched_ex.restype = i32
         lib.iwq_fill_synthetic.argtypes = [vp, i64, i32, u64, i64, vp]
         lib.iwq_fill_synthetic.restype = i32
         lib.iwq_status_string.argtypes = [i32]

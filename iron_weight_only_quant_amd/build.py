@@ -6,9 +6,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
-SOURCES = ["iwq_minmax.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
+SOURCES = ["iwq_minmax.hip", "iwq_batched.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
            "iwq_fpunpack.hip"]
-DEPS = SOURCES + ["iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h"]
+DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Numerics: no FMA contraction, IEEE fp32 division, denormals preserved.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",

@@ -1210,6 +1210,13 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
   if (g <= 0 || g % 32 != 0 || K % g != 0) return IWQ_ERR_GROUP;
   if ((reinterpret_cast<uintptr_t>(x) & 15u) || (reinterpret_cast<uintptr_t>(codes) & 15u)) return IWQ_ERR_ARG;
+  // the split-K reduces store y in 8-B pieces (4 outputs) and read the fp32 partials with 16-B loads:
+  // a caller whose y / ldy cannot take that, or whose workspace is not 16-B aligned, gets the unsplit
+  // kernels (a workspace is only ever an optimisation)
+  if ((reinterpret_cast<uintptr_t>(y) & 7u) || (ldy % 4) != 0 || (reinterpret_cast<uintptr_t>(workspace) & 15u)) {
+    workspace = nullptr;
+    workspace_bytes = 0;
+  }
   if (M > 0x7FFFFFFF || N > 0x7FFFFFFF || K > 0x7FFFFFFF) return IWQ_ERR_SHAPE;
   GemmArgs a{};
   a.x = static_cast<const _Float16*>(x);
@@ -1331,9 +1338,15 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
         else launch_gemv<2, 8, 1>(a, st, true);
         break;
     }
-  } else if (((variant == 0 && M < 512 && !split_pref && !short_pref) || (variant >= 50 && variant < 60)) &&
+  } else if (((variant == 0 && !split_pref && !short_pref &&
+               (M < 256 || !prefill_b32_supported(M, N, K, a.gpr, a.group) ||
+                (M < 512 && prefill_splitk_count(M, N, K, 0) > 1))) ||
+              (variant >= 50 && variant < 60)) &&
              !(flags & IWQ_FLAG_FORCE_GENERIC) && mid_supported(M, N, K, a.gpr, a.group)) {
-    // 16 < M < 512 (M < 256, or no split-K workspace): the weight-streaming mid-M kernel
+    // 16 < M < 256, or 256 <= M < 512 where a K split would pay but the caller gave no workspace
+    // for it: the weight-streaming mid-M kernel.  From M = 256 the prefill kernel runs whenever the
+    // split model picks ONE range (wide weights: 70B gate/up, lm_head -- workspace or not), exactly
+    // like the NIB path, so both code layouts give the same bits.
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     const hipError_t e = mid_launch(p, (int)variant, false, st);
     if (e != hipSuccess) {

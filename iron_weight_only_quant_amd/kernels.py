@@ -442,15 +442,16 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
     # K ranges for A/B): fp32 partial tiles, from torch's caching allocator
     if nib and M < NIB_MIN_M:
         raise ValueError(f"w4a16_gemm: NIB-layout codes need M >= {NIB_MIN_M} rows, got {M}")
-    ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if not tiled else 0
-    v = (int(flags) >> 16) & 0xFF
-    if 81 < v < 96 and N % 256 == 0:
-        ws_bytes = max(ws_bytes, ((M + 255) // 256) * (N // 256) * (v - 80) * 65536 * 4)
-    if 110 <= v < 150 and N % 256 == 0:  # short-tile split (A/B): 128- / 64-row tiles, S ranges
-        mtw, ns = (4, v - 108) if v < 130 else (2, v - 128)
-        ws_bytes = max(ws_bytes, ((M + 32 * mtw - 1) // (32 * mtw)) * (N // 256) * ns * mtw * 8192 * 4)
-    ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
     with L.on_device(x.device):
+        # the size depends on the CU count of the device it is queried on: ask x's device
+        ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if not tiled else 0
+        v = (int(flags) >> 16) & 0xFF
+        if 81 < v < 96 and N % 256 == 0:
+            ws_bytes = max(ws_bytes, ((M + 255) // 256) * (N // 256) * (v - 80) * 65536 * 4)
+        if 110 <= v < 150 and N % 256 == 0:  # short-tile split (A/B): 128- / 64-row tiles, S ranges
+            mtw, ns = (4, v - 108) if v < 130 else (2, v - 128)
+            ws_bytes = max(ws_bytes, ((M + 32 * mtw - 1) // (32 * mtw)) * (N // 256) * ns * mtw * 8192 * 4)
+        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
         st = lib.iwq_w4a16_gemm_ws(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                    int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, L.ptr(ws), ws_bytes,
                                    int(flags), L.stream_handle(x.device))
@@ -531,14 +532,38 @@ def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zer
     return torch.nn.functional.linear(x, w, bias)
 
 
+def batch_supported(w: torch.Tensor, n_bits: int, group: int, quant_dim: int = 0) -> bool:
+    """Whether one weight can be an entry of a batched whole-model launch (BatchPlan) for this
+    configuration (include/iwq.h iwq_batch_plan_ex); otherwise quantize it with its own call."""
+    if not (w.is_cuda and w.dim() == 2 and w.is_contiguous() and w.dtype in L.DTYPE_CODE
+            and w.data_ptr() % 16 == 0 and 1 <= n_bits <= 8 and quant_dim in (0, 1)):
+        return False
+    rows, cols = w.shape
+    eb = w.element_size()
+    if group == -1:
+        return rows * cols % 8 == 0
+    if quant_dim == 1:
+        g = rows if group == -2 else group
+        return g > 0 and rows % g == 0 and cols % 8 == 0
+    if group in FAST_GROUPS:
+        return n_bits >= 2 and cols % group == 0
+    Lg = cols if group == -2 else group
+    return Lg > 0 and cols % Lg == 0 and Lg % 8 == 0 and Lg <= 16384 and (cols * eb) % 16 == 0
+
+
 class BatchPlan:
     """Device-resident work table for quantizing many weights in one launch (quant_wrapper.py:52-82).
 
-    Built once per set of tensors; `run()` may be replayed (e.g. by bench.py) without host work
-    beyond one kernel launch."""
+    Every group mode and quant_dim (include/iwq.h iwq_batch_plan_ex): per-group (power of two
+    8..512, quant_dim 0) is ONE persistent launch over all weights; per-channel / long groups run one
+    launch per distinct group length (one register class each: 2 for a Llama-2-7B), quant_dim 1 one
+    launch, per-tensor one key-init + reduce + apply triple.  Each weight gets exactly the bits of its
+    own quantize_minmax call.  Built once per set of tensors; `run()` may be replayed (e.g. by
+    bench.py) without host work beyond the launches."""
 
     def __init__(self, weights: List[torch.Tensor], n_bits: int, group: int, symmetric: bool,
-                 outs: Optional[List[torch.Tensor]] = None, want_scales: bool = True, want_codes: bool = False):
+                 outs: Optional[List[torch.Tensor]] = None, want_scales: bool = True, want_codes: bool = False,
+                 quant_dim: int = 0):
         if not weights:
             raise ValueError("empty batch")
         lib = L.load()
@@ -548,36 +573,49 @@ class BatchPlan:
             L.require_device(w)
             if w.device != dev or w.dtype != dt or w.dim() != 2 or not w.is_contiguous():
                 raise ValueError("batched weights must be contiguous 2-D tensors of one dtype on one device")
-            if w.shape[1] % group != 0:
-                raise AssertionError("last dimension not divisible by the group size")
-        if group not in FAST_GROUPS or not (2 <= n_bits <= 8):
-            raise ValueError("batched path supports power-of-two groups 8..512 and 2 <= n_bits <= 8")
+            group_geometry(w.shape[0], w.shape[1], group, quant_dim)  # the reference's errors first
+            if not batch_supported(w, n_bits, group, quant_dim):
+                raise ValueError(f"weight {tuple(w.shape)} cannot join a batched launch for group {group}, "
+                                 f"quant_dim {quant_dim}, n_bits {n_bits} (kernels.batch_supported)")
         self.device, self.dtype = dev, dt
         self.n_bits, self.group, self.symmetric = int(n_bits), int(group), bool(symmetric)
+        self.quant_dim = int(quant_dim)
         self.weights = weights
         self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
-        self.scales = _param_views(weights, group, dt, dev) if want_scales else [None] * len(weights)
-        self.zeros = (_param_views(weights, group, dt, dev) if (want_scales and not symmetric)
+        sizes = [group_geometry(w.shape[0], w.shape[1], group, quant_dim)[1] for w in weights]
+        self.scales = _param_views(sizes, dt, dev) if want_scales else [None] * len(weights)
+        self.zeros = (_param_views(sizes, dt, dev) if (want_scales and not symmetric)
                       else [None] * len(weights))
         self.codes = [torch.empty(codes_nbytes(w.shape[0], w.shape[1], n_bits), dtype=torch.uint8, device=dev)
                       if want_codes else None for w in weights]
         self.want_codes = want_codes
-        n = len(weights)
-        table = (L.IwqBatchEntry * n)()
-        for i, w in enumerate(weights):
-            table[i].w = w.data_ptr()
-            table[i].out_deq = self.outs[i].data_ptr() if self.outs[i] is not None else None
-            table[i].out_codes = self.codes[i].data_ptr() if self.codes[i] is not None else None
-            table[i].out_scales = self.scales[i].data_ptr() if self.scales[i] is not None else None
-            table[i].out_zeros = self.zeros[i].data_ptr() if self.zeros[i] is not None else None
-            table[i].rows, table[i].cols = w.shape
-        total = ctypes.c_int64(0)
-        _raise_for(lib.iwq_batch_plan(table, n, L.DTYPE_CODE[dt], self.n_bits, self.group, ctypes.byref(total)),
-                   "iwq_batch_plan")
-        self.total_units = total.value
-        host = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8)
-        self.d_table = host.to(dev)
-        self.n = n
+        # launches: per-channel / long groups need one register class per launch -> bucket by length
+        if quant_dim == 0 and group not in FAST_GROUPS and group != -1:
+            buckets = {}
+            for i, w in enumerate(weights):
+                buckets.setdefault(w.shape[1] if group == -2 else group, []).append(i)
+            index_sets = [buckets[k] for k in sorted(buckets)]
+        else:
+            index_sets = [list(range(len(weights)))]
+        self.launches = []
+        for idx in index_sets:
+            table = (L.IwqBatchEntry * len(idx))()
+            for k, i in enumerate(idx):
+                table[k].w = weights[i].data_ptr()
+                table[k].out_deq = self.outs[i].data_ptr() if self.outs[i] is not None else None
+                table[k].out_codes = self.codes[i].data_ptr() if self.codes[i] is not None else None
+                table[k].out_scales = self.scales[i].data_ptr() if self.scales[i] is not None else None
+                table[k].out_zeros = self.zeros[i].data_ptr() if self.zeros[i] is not None else None
+                table[k].rows, table[k].cols = weights[i].shape
+            total, glen = ctypes.c_int64(0), ctypes.c_int64(0)
+            _raise_for(lib.iwq_batch_plan_ex(table, len(idx), L.DTYPE_CODE[dt], self.n_bits, self.group,
+                                             self.quant_dim, ctypes.byref(total), ctypes.byref(glen)),
+                       "iwq_batch_plan_ex")
+            wsb = int(lib.iwq_batch_workspace_bytes(len(idx), self.group, self.quant_dim))
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None
+            d_table = torch.frombuffer(bytearray(bytes(table)), dtype=torch.uint8).to(dev)
+            self.launches.append((d_table, len(idx), total.value, glen.value, ws, wsb))
+        self.d_table, self.n, self.total_units = self.launches[0][0], len(weights), self.launches[0][2]
         self.nan_flag = torch.zeros(1, dtype=torch.int32, device=dev)
         self.numel = sum(w.numel() for w in weights)
 
@@ -586,10 +624,11 @@ class BatchPlan:
         flags = (L.IWQ_FLAG_BATCH_CODES if self.want_codes else 0) | ((int(variant) & 0xFF) << 16)
         sh = ctypes.c_void_p(stream.cuda_stream) if stream is not None else L.stream_handle(self.device)
         with L.on_device(self.device):
-            st = lib.iwq_quantize_minmax_batched(L.ptr(self.d_table), self.n, self.total_units,
-                                                 L.DTYPE_CODE[self.dtype], self.n_bits, self.group,
-                                                 int(self.symmetric), L.ptr(self.nan_flag), flags, sh)
-        _raise_for(st, "iwq_quantize_minmax_batched")
+            for d_table, n, total, glen, ws, wsb in self.launches:
+                st = lib.iwq_quantize_minmax_batched_ex(L.ptr(d_table), n, total, glen, L.DTYPE_CODE[self.dtype],
+                                                        self.n_bits, self.group, int(self.symmetric), self.quant_dim,
+                                                        L.ptr(ws), wsb, L.ptr(self.nan_flag), flags, sh)
+                _raise_for(st, "iwq_quantize_minmax_batched_ex")
 
 
 def fill_synthetic(t: torch.Tensor, seed: int, index_offset: int = 0):
@@ -614,10 +653,10 @@ def selftest_division(device="cuda"):
     return tuple(int(x) for x in counts.cpu())
 
 
-def _param_views(weights, group, dtype, dev):
-    """Per-tensor [G] parameter vectors as views of ONE allocation (one caching-allocator call
-    instead of one per layer: 224 / 560 for a 7B / 70B model); each view is contiguous."""
-    sizes = [w.numel() // group for w in weights]
+def _param_views(sizes, dtype, dev):
+    """Per-tensor [G] parameter vectors (sizes[i] elements each) as views of ONE allocation (one
+    caching-allocator call instead of one per layer: 224 / 560 for a 7B / 70B model); each view is
+    contiguous."""
     return list(torch.empty(sum(sizes), dtype=dtype, device=dev).split(sizes))
 
 
@@ -650,8 +689,9 @@ class FpBatchPlan:
             raise RuntimeError("decode table unavailable for this format (or building it inside a graph capture)")
         self.weights = weights
         self.outs = outs if outs is not None else [torch.empty_like(w) for w in weights]
-        self.scales = _param_views(weights, group, torch.float16, dev)
-        self.zeros = (_param_views(weights, group, torch.float16, dev) if not self.symmetric
+        sizes = [w.numel() // group for w in weights]
+        self.scales = _param_views(sizes, torch.float16, dev)
+        self.zeros = (_param_views(sizes, torch.float16, dev) if not self.symmetric
                       else [None] * len(weights))
         n = len(weights)
         table = (L.IwqBatchEntry * n)()

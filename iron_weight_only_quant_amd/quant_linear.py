@@ -141,26 +141,33 @@ class QuantLinear(nn.Module):
                                           want_codes=self.keep_codes and self.w_bit <= 8)
             if res.out is not w:
                 w.copy_(res.out)
-            tiled = None
-            if (self.fused_forward == "auto" and res.codes is not None and self.quant_dim == 0
-                    and self.w_bit <= 4 and w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0):
-                # decode batches read the codes in the GEMV tile layout (1 KiB contiguous per load)
-                tiled = kernels.tile_codes(res.codes, w.shape[0], w.shape[1])
-            nib = None
-            if (self.fused_forward is True and self.nib_prefill and res.codes is not None
-                    and self.quant_dim == 0
-                    and 2 <= self.w_bit <= 4 and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0
-                    and (self.w_group_size == -2 or (self.w_group_size > 0 and self.w_group_size % 64 == 0))):
-                # opt-in: prefill batches (M >= 256) read a NIB-layout copy (9 instead of 12 dequant
-                # VALU per 8 weights; +0.5-1.2 % per channel, +-0 g128 at M = 8192, for 0.5 B per
-                # weight more device memory: DESIGN.md section 5)
-                nib = kernels.nib_codes(res.codes, w.shape[0], w.shape[1])
-            # registered buffers (see __init__), written without nn.Module.__setattr__'s per-name checks
-            self._buffers.update(scales=res.scales.view(-1, 1),
-                                 zeros=res.zeros.view(-1, 1) if res.zeros is not None else None,
-                                 qweight=res.codes, qweight_tiled=tiled, qweight_nib=nib,
-                                 weight_fp4=None, weight_fp6=None, weight_fp8=None)
-            self.quantized.fill_(True)
+            self._set_int_result(res.scales, res.zeros, res.codes)
+
+    def _set_int_result(self, scales, zeros, codes):
+        """Install the INT branch's buffers (quant_linear.py:924-932) -- scales / zeros [G, 1] -- plus,
+        when the packed codes were kept, the derived layouts the fused forward reads.  Shared by
+        quantize_weight and quantize_model's batched launch."""
+        rows, cols = self.out_features, self.in_features
+        tiled = None
+        if (self.fused_forward == "auto" and codes is not None and self.quant_dim == 0
+                and self.w_bit <= 4 and rows % 16 == 0 and cols % 128 == 0):
+            # decode batches read the codes in the GEMV tile layout (1 KiB contiguous per load)
+            tiled = kernels.tile_codes(codes, rows, cols)
+        nib = None
+        if (self.fused_forward is True and self.nib_prefill and codes is not None
+                and self.quant_dim == 0
+                and 2 <= self.w_bit <= 4 and rows % 256 == 0 and cols % 64 == 0
+                and (self.w_group_size == -2 or (self.w_group_size > 0 and self.w_group_size % 64 == 0))):
+            # opt-in: prefill batches (M >= 256) read a NIB-layout copy (9 instead of 12 dequant
+            # VALU per 8 weights; +0.5-1.2 % per channel, +-0 g128 at M = 8192, for 0.5 B per
+            # weight more device memory: DESIGN.md section 5)
+            nib = kernels.nib_codes(codes, rows, cols)
+        # registered buffers (see __init__), written without nn.Module.__setattr__'s per-name checks
+        self._buffers.update(scales=scales.view(-1, 1),
+                             zeros=zeros.view(-1, 1) if zeros is not None else None,
+                             qweight=codes, qweight_tiled=tiled, qweight_nib=nib,
+                             weight_fp4=None, weight_fp6=None, weight_fp8=None)
+        self.quantized.fill_(True)
 
     def quantize_weight_approximate(self):
         """quant_linear.py:470-632 on the GPU: symmetric absmax FP codes per group of w_group_size,

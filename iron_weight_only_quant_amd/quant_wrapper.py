@@ -6,9 +6,11 @@ weight storage; weight-only runs need 0 < w_bit < 16 and a_bit None or >= 16 (:1
 
 MI355X-first difference: instead of quantizing layer after layer (one ~16-op ATen chain plus an
 empty_cache per layer, :52-82), all eligible layers that live on one GPU and share a dtype are
-quantized by ONE persistent multi-tensor launch (kernels.BatchPlan) when the group size is a
-power of two in [8, 512] (INT: kernels.BatchPlan; FP4/FP6/FP8 and the single-aligned approximate
-decode on fp16 weights: kernels.FpBatchPlan); any other configuration uses one launch per layer.
+quantized by batched multi-tensor launches: INT in every group mode (kernels.BatchPlan: ONE launch
+for power-of-two groups 8..512, one per distinct row length for per-channel / long groups, one for
+quant_dim 1, three for per-tensor), FP4/FP6/FP8 and the single-aligned approximate decode on fp16
+weights with power-of-two groups (kernels.FpBatchPlan, one launch).  Layers a batch cannot take
+(strided, unaligned, rows longer than 16384 per channel, ...) use one launch per layer.
 """
 import torch
 
@@ -46,6 +48,12 @@ def _qkw(args, w_format):
         fp4_hi_align_start=getattr(args, "fp4_hi_align_start", 1),
         fp4_hi_align_exp_field=getattr(args, "fp4_hi_align_exp_field", 1),
         fp4_tail_pad_bits=getattr(args, "fp4_tail_pad_bits", 0),
+        # MI355X additions (not in the reference's args): the packed-code forward of QuantLinear
+        # (False = the reference's F.linear on the dequantized weight, "auto" = packed GEMV for
+        # decode batches, True = always the fused kernels) and its opt-in NIB prefill layout
+        fused_forward=getattr(args, "fused_forward", False),
+        nib_prefill=getattr(args, "nib_prefill", False),
+        keep_codes=getattr(args, "keep_codes", False),
     )
 
 
@@ -90,28 +98,28 @@ def quantize_model(model, args, quant_mix_gate=False, batched=True, verbose=True
     done = set()
     tied = _tied(layers) if batched else set()
     g = kw["w_group_size"]
-    if (batched and w_format == "int" and not kw["approximate"] and kw["quant_dim"] == 0
-            and g in kernels.FAST_GROUPS and 2 <= kw["w_bit"] <= 8 and layers):
+    qd = kw["quant_dim"]
+    if (batched and w_format == "int" and not kw["approximate"] and 1 <= kw["w_bit"] <= 8 and layers
+            and (g > 0 or g in (-1, -2)) and qd in (0, 1) and not (kw["symmetric"] and kw["w_bit"] < 2)):
         buckets = {}
         for n, m in layers:
             w = m.weight.data
-            if (n not in tied and w.device.type == "cuda" and w.dim() == 2 and w.is_contiguous()
-                    and w.shape[1] % g == 0 and w.dtype in (torch.float16, torch.bfloat16, torch.float32)
-                    and w.data_ptr() % 16 == 0):
+            if n not in tied and w.device.type == "cuda" and kernels.batch_supported(w, kw["w_bit"], g, qd):
                 buckets.setdefault((w.device, w.dtype), []).append((n, m))
+        want_codes = bool(kw["keep_codes"] or kw["fused_forward"])  # as QuantLinear.quantize_weight
         for (dev, dt), items in buckets.items():
             ws = [m.weight.data for _, m in items]
-            plan = kernels.BatchPlan(ws, kw["w_bit"], g, bool(kw["symmetric"]), outs=ws)
+            plan = kernels.BatchPlan(ws, kw["w_bit"], g, bool(kw["symmetric"]), outs=ws, want_codes=want_codes,
+                                     quant_dim=qd)
             plan.run()
             for i, (n, m) in enumerate(items):
                 q = QuantLinear.from_linear(m, quantize=False, **kw)
-                q._buffers.update(scales=plan.scales[i].view(-1, 1),
-                                  zeros=plan.zeros[i].view(-1, 1) if plan.zeros[i] is not None else None)
-                q.quantized.fill_(True)
+                q._set_int_result(plan.scales[i], plan.zeros[i], plan.codes[i])
                 _set_module(model, n, q)
                 done.add(n)
     if (batched and w_format in ("fp4", "fp6", "fp8") and kw["quant_dim"] == 0 and g in kernels.FAST_GROUPS
-            and not (kw["approximate"] and kw["double_approximate"]) and layers):
+            and not (kw["approximate"] and kw["double_approximate"]) and layers
+            and not (kw["keep_codes"] or kw["fused_forward"])):  # FP codes: per-layer path keeps them
         _batched_fp(model, layers, kw, w_format, done, tied)
     for n, m in layers:
         if n in done:

@@ -7,8 +7,9 @@ ranks (one process per GPU) and each rank quantizes its shard with ONE batched l
 exchange in the data path.  Optionally the fp16 weights start on rank 0 and are scattered to the
 ranks that own them (`scatter_from_rank0`: one point-to-point send per destination, all in flight
 together, so rank 0's xGMI links to the other GPUs run in parallel), and the packed results (int
-codes + fp16 scales/zeros, ~1/4 of the fp16 bytes) are gathered back to rank 0 with a single
-torch.distributed collective (RCCL over xGMI on MI355X, gloo in the CPU tests).
+codes + fp16 scales/zeros, ~1/4 of the fp16 bytes) are gathered back to rank 0 by the mirror
+image: one point-to-point send per rank, all receives posted together on rank 0 (RCCL over xGMI on
+MI355X, gloo in the CPU tests).
 """
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -85,8 +86,11 @@ def quantize_shard(named: Dict[str, torch.Tensor], n_bits: int, group: int, symm
 
 
 def _flatten(res: ShardResult) -> torch.Tensor:
+    """One rank's packed results back to back in name order (the order gather_to_rank0 unpacks)."""
     parts = []
-    for c, s, z in zip(res.codes, res.scales, res.zeros):
+    order = sorted(range(len(res.names)), key=lambda i: res.names[i])
+    for i in order:
+        c, s, z = res.codes[i], res.scales[i], res.zeros[i]
         parts.append(c.reshape(-1).view(torch.uint8))
         parts.append(s.reshape(-1).view(torch.uint8))
         if z is not None:
@@ -96,27 +100,56 @@ def _flatten(res: ShardResult) -> torch.Tensor:
     return torch.cat([p.to(parts[0].device) for p in parts])
 
 
-def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bins_names: List[List[str]],
-                    n_bits: int, group: int, symmetric: bool, dtype=torch.float16, pg=None):
-    """Gather every rank's packed results to rank 0 with one padded all_gather (RCCL/gloo).
+def packed_nbytes(shape: Tuple[int, int], n_bits: int, group: int, symmetric: bool, esz: int = 2) -> int:
+    """Bytes of one weight's packed result in the gather layout: codes, scales[, zeros]."""
+    rows, cols = shape
+    ncode = rows * (cols // 2) if n_bits <= 4 else rows * cols
+    G = rows * cols // group
+    return ncode + G * esz * (1 if symmetric else 2)
 
+
+def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bins_names: List[List[str]],
+                    n_bits: int, group: int, symmetric: bool, dtype=torch.float16, pg=None, stats=None):
+    """Rooted gather of every rank's packed results to rank 0: each rank r > 0 sends its flat
+    buffer once, rank 0 posts one receive per rank, all in flight together (batch_isend_irecv; on an
+    xGMI node the 7 links into rank 0 run in parallel).  Every bin's size follows from the shard
+    plan, so there is no size exchange, and each byte crosses the fabric exactly once (an all_gather
+    would deliver every shard to every rank: N x the bytes).
+
+    `stats` (a dict, optional) receives the bytes this rank sent / received.
     Returns {name: (codes, scales, zeros)} on rank 0, None elsewhere."""
     import torch.distributed as dist
     rank = dist.get_rank(pg)
     world = dist.get_world_size(pg)
+    esz = torch.tensor([], dtype=dtype).element_size()
+    sizes = [sum(packed_nbytes(shapes[n], n_bits, group, symmetric, esz) for n in all_bins_names[r])
+             for r in range(world)]
     flat = _flatten(res)
+    if flat.numel() != sizes[rank]:
+        raise ValueError(f"gather_to_rank0: rank {rank} holds {flat.numel()} packed bytes, the plan says {sizes[rank]}")
+    # gloo (CPU tests / 1-GPU rehearsal) has no device-memory point-to-point: stage through the host
+    staged = dist.get_backend(pg) == "gloo" and flat.is_cuda
+    if staged:
+        flat = flat.cpu()
     dev = flat.device
-    n = torch.tensor([flat.numel()], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=pg)
-    mx = int(max(int(s.item()) for s in sizes))
-    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    buf[: flat.numel()] = flat
-    outs = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(outs, buf, group=pg)
+    outs = [None] * world
+    if rank == 0:
+        outs[0] = flat
+        ops = []
+        for r in range(1, world):
+            outs[r] = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+            if sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, outs[r], r, group=pg))
+    else:
+        ops = [dist.P2POp(dist.isend, flat, 0, group=pg)] if sizes[rank] else []
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if stats is not None:
+        stats["sent_bytes"] = 0 if rank == 0 else sizes[rank]
+        stats["recv_bytes"] = sum(sizes[1:]) if rank == 0 else 0
     if rank != 0:
         return None
-    esz = torch.tensor([], dtype=dtype).element_size()
     result = {}
     for r in range(world):
         off = 0

@@ -147,3 +147,35 @@ def test_gloo_world2_scatter_from_rank0():
         for name, arr in res[r].items():
             i = [n for n, _ in shapes].index(name)
             assert np.array_equal(arr.view(np.uint16), synth(500 + i, shapes[i][1], "float16").view(np.uint16))
+
+
+def test_bench_gpus2_spawns_ranks_and_rooted_gather_moves_each_byte_once():
+    """`bench.py --gpus 2` (no WORLD_SIZE: the driver's command form) spawns two rank processes
+    itself; over gloo on the CPU (--dry-run) the rooted gather delivers every tensor to rank 0 and
+    moves exactly rank 1's packed bytes once (an all_gather would move them N times)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--model", "opt-125m"], capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the only JSON line
+    rec = json.loads(lines[0])
+    assert rec["world"] == 2 and rec["tensors"] == 72 and rec["tensors_at_rank0"] == 72
+    per_rank = rec["plan_packed_bytes_per_rank"]
+    shapes = shard.model_linear_shapes("opt-125m")
+    assert sum(per_rank) == sum(shard.packed_nbytes(s, 4, 128, False) for _, s in shapes)
+    assert rec["gather_sent_bytes"] == per_rank[1] == rec["gather_recv_bytes"]
+
+
+def test_bench_world_size_must_match_gpus():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--model", "opt-125m"], capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert r.returncode != 0 and "world size 1 != --gpus 2" in r.stderr

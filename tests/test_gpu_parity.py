@@ -946,6 +946,47 @@ def test_w4a16_nib_default(K, M, group):
         assert torch.equal(yl, y0)
 
 
+@pytest.mark.parametrize("M", [256, 384])
+@pytest.mark.parametrize("group", [-2, 128])
+def test_w4a16_nib_default_wide_unsplit(K, M, group):
+    """Wide weights (Llama-2-70B gate/up: N = 28672, K = 8192) at 256 <= M < 512: the split model
+    picks ONE range (224 tiles), and the row-major default must then take the unsplit prefill
+    kernel like the NIB path does (not the mid-M kernel): same bits, within tolerance of fp32."""
+    N, Kd = 28672, 8192
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 96)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    del w
+    torch.manual_seed(13)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    nib = K.nib_codes(r.codes, N, Kd)
+    y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N)
+    y1 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, nib=True)
+    assert torch.equal(y0, y1)
+    ref = x.float() @ r.out.float().t()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool(((y0.float() - ref).abs() <= tol).all())
+
+
+@pytest.mark.parametrize("M", [64, 512])
+def test_w4a16_split_misaligned_y(K, M):
+    """A y that is only 2-B aligned cannot take the split reduces' 8-B stores: the C-ABI then runs
+    the unsplit kernels instead (the workspace is dropped), and the result stays correct."""
+    N, Kd = 512, 4352
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 97)
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    torch.manual_seed(14)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    buf = torch.full((M * N + 1,), float("nan"), dtype=torch.float16, device=DEV)
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, out=buf[1:])
+    assert y.data_ptr() % 8 == 2
+    assert torch.isnan(buf[0])
+    ref = x.float() @ r.out.float().t()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool(((y.float() - ref).abs() <= tol).all())
+
+
 @pytest.mark.parametrize("M", [200, 256, 300, 512, 1024])
 @pytest.mark.parametrize("sym", [False, True])
 @pytest.mark.parametrize("group", [-2, 128])

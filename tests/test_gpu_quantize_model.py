@@ -1,0 +1,108 @@
+"""quantize_model (quant_wrapper.py:7-84) through the drop-in: the packed-code forward reachable
+from the model transform (args.fused_forward / nib_prefill, as QuantLinear's own flags), and the
+batched whole-model launch for every group mode (per-group, per-channel -2, per-tensor -1,
+quant_dim 1) bit-identical to the per-layer QuantLinear path and to the oracle."""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import iwq_oracle as O
+
+from .golden_util import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _model(specs, originals, dtype=torch.float16):
+    m = torch.nn.Sequential()
+    for n, (o, i, b) in specs.items():
+        lin = torch.nn.Linear(i, o, bias=b, dtype=dtype, device=DEV)
+        lin.weight.data.copy_(originals[n])
+        if b:
+            lin.bias.data.copy_(torch.linspace(-0.1, 0.1, o, dtype=dtype))
+        m.add_module(n, lin)
+    return m
+
+
+def _args(**kw):
+    base = dict(w_bit=4, a_bit=16, w_group_size=128, w_symmetric=False, w_format="int", quant_dim=0)
+    base.update(kw)
+    return SimpleNamespace(**base)
+
+
+@pytest.mark.parametrize("fused", ["auto", True])
+@pytest.mark.parametrize("group", [128, -2])
+@pytest.mark.parametrize("nib", [False, True])
+def test_quantize_model_fused_forward(fused, group, nib):
+    """quantize_model(..., fused_forward=...) keeps the packed codes (batched launch and per-layer
+    path alike, same bytes), and every replaced layer's forward matches F.linear on the dequantized
+    weight within the fp16 output tolerance for decode, mid and prefill batch sizes."""
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+    if nib and fused != True:  # noqa: E712 (the NIB layout is only kept for fused_forward=True)
+        pytest.skip("nib_prefill applies to fused_forward=True")
+    torch.manual_seed(5)
+    specs = {"l0": (512, 1024, True), "l1": (1024, 512, False), "lm_head": (640, 512, False)}
+    originals = {n: (torch.randn(o, i) * 0.02).half() for n, (o, i, _) in specs.items()}
+    models = {}
+    for batched in (True, False):
+        m = _model(specs, originals)
+        quantize_model(m, _args(w_group_size=group, fused_forward=fused, nib_prefill=nib), batched=batched,
+                       verbose=False)
+        models[batched] = m
+    for n in ("l0", "l1"):
+        a, b = getattr(models[True], n), getattr(models[False], n)
+        assert isinstance(a, QuantLinear) and a.fused_forward == fused
+        assert a.qweight is not None and torch.equal(a.qweight, b.qweight), n
+        assert (a.qweight_tiled is not None) == (fused == "auto")
+        assert (a.qweight_nib is not None) == (fused is True and nib)
+        if a.qweight_tiled is not None:
+            assert torch.equal(a.qweight_tiled, b.qweight_tiled)
+        ref = O.quantlinear_int(originals[n].numpy(), w_bit=4, w_group_size=group, symmetric=False)
+        assert bits_equal(a.weight.data.cpu().numpy(), ref.dequant)
+        assert np.array_equal(a.qweight.cpu().numpy(), O.pack_codes(ref.codes, 4).reshape(-1))
+        for M in (1, 8, 64, 300):
+            x = (torch.randn(M, a.in_features, device=DEV) * 0.5).half()
+            y = a(x)
+            yr = torch.nn.functional.linear(x.float(), a.weight.float(),
+                                            None if a.bias is None else a.bias.float())
+            tol = 2e-3 * yr.abs() + 2e-3
+            assert bool(((y.float() - yr).abs() <= tol).all()), (n, M)
+    assert not isinstance(models[True].lm_head, QuantLinear)
+
+
+@pytest.mark.parametrize("mode", [(-2, 0), (-1, 0), (128, 1), (-2, 1), (64, 1), (768, 0), (96, 0)])
+@pytest.mark.parametrize("bits,sym", [(4, False), (8, False), (3, True)])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_quantize_model_batched_all_group_modes(mode, bits, sym, dtype):
+    """Per-channel, per-tensor, quant_dim 1, long and non-power-of-two groups through quantize_model:
+    the batched launch(es) give every layer the per-layer path's bits, and the oracle's."""
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+    group, qd = mode
+    torch.manual_seed(7)
+    specs = {"a": (384, 3072, True), "b": (256, 1536, False), "c": (128, 2304, False), "d": (512, 1536, True)}
+    originals = {n: (torch.randn(o, i) * 0.02).to(dtype) for n, (o, i, _) in specs.items()}
+    originals["b"][3].fill_(0.5)  # a constant row (range 0 -> clamp 1e-5)
+    res = {}
+    for batched in (True, False):
+        m = _model(specs, originals, dtype)
+        quantize_model(m, _args(w_bit=bits, w_group_size=group, w_symmetric=sym, quant_dim=qd), batched=batched,
+                       verbose=False)
+        res[batched] = m
+    for n in specs:
+        a, b = getattr(res[True], n), getattr(res[False], n)
+        assert torch.equal(a.weight.data.view(torch.int16), b.weight.data.view(torch.int16)), n
+        assert torch.equal(a.scales.view(torch.int16), b.scales.view(torch.int16)), n
+        assert (a.zeros is None) == sym
+        if not sym:
+            assert torch.equal(a.zeros.view(torch.int16), b.zeros.view(torch.int16)), n
+        assert a.scales.shape == b.scales.shape
+        if dtype == torch.float16:
+            ref = O.quantlinear_int(originals[n].numpy(), w_bit=bits, w_group_size=group, symmetric=sym,
+                                    quant_dim=qd)
+            assert bits_equal(a.weight.data.cpu().numpy(), ref.dequant), n
+            assert bits_equal(a.scales.cpu().numpy(), ref.scales), n
