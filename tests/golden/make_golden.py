@@ -9,6 +9,8 @@ Produces (committed, data only):
   tests/golden/int_small.npz   full inputs + reference outputs for small shapes, all modes
   tests/golden/int_edge.npz    edge-row tensors (constant, zero, subnormal, one-sided, ties, +-0, ...)
   tests/golden/int_large.json  SHA-256 of reference outputs at Llama-2-7B shapes over oracle/synth inputs
+  tests/golden/int_large_70b.json  the same at the four Llama-2-70B Linear shapes (configs[3])
+                                   (`--only 70b` regenerates just this file)
 
 Reference entry points exercised:
   quant_funcs.pseudo_quantize_tensor                  (quant_funcs.py:4-46)
@@ -194,7 +196,39 @@ def large_cases():
     return res
 
 
+LARGE_70B = [("q_proj", (8192, 8192), 10), ("k_proj", (1024, 8192), 11), ("gate_proj", (28672, 8192), 12),
+             ("down_proj", (8192, 28672), 13)]
+
+
+def large70b_cases():
+    """Llama-2-70B shapes (BASELINE configs[3], 4-bit g=128): the config's own case on both reference
+    entry points, plus per-row and per-channel (down_proj's 28672-element rows exceed the GPU's
+    register-resident row kernel, so they cover the universal path at full size)."""
+    res = {"generator": "oracle/synth.py (seed, shape) fp16", "cases": []}
+    for name, shp, seed in LARGE_70B:
+        x = synth(seed, shp, "float16")
+        res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "input", "sha_input": sha(x)})
+        for bits, zp, g in ((4, True, 128), (4, True, -1)):
+            out = ref_qf(x, "float16", n_bits=bits, zero_point=zp, q_group_size=g)
+            res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "qf", "n_bits": bits,
+                                 "zero_point": zp, "q_group_size": g, "sha_deq": sha(out)})
+            del out
+        for bits, sym, g in ((4, False, 128), (4, True, 128), (4, False, -2)):
+            deq, s, z, _ = ref_ql(x, "float16", w_bit=bits, w_group_size=g, symmetric=sym)
+            res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "ql", "w_bit": bits,
+                                 "symmetric": sym, "w_group_size": g, "sha_deq": sha(deq), "sha_scales": sha(s),
+                                 "sha_zeros": None if z is None else sha(z)})
+            del deq, s, z
+        print("large70b", name, flush=True)
+    return res
+
+
 if __name__ == "__main__":
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "70b":
+        with open(os.path.join(HERE, "int_large_70b.json"), "w") as f:
+            json.dump(large70b_cases(), f, indent=1)
+        print("large70b done", flush=True)
+        sys.exit(0)
     np.savez_compressed(os.path.join(HERE, "int_small.npz"), **small_cases())
     print("small done", flush=True)
     np.savez_compressed(os.path.join(HERE, "int_edge.npz"), **edge_cases())
@@ -202,3 +236,6 @@ if __name__ == "__main__":
     with open(os.path.join(HERE, "int_large.json"), "w") as f:
         json.dump(large_cases(), f, indent=1)
     print("large done", flush=True)
+    with open(os.path.join(HERE, "int_large_70b.json"), "w") as f:
+        json.dump(large70b_cases(), f, indent=1)
+    print("large70b done", flush=True)

@@ -71,6 +71,52 @@ def test_ppl_seqlen_defaults_and_missing_dataset(tmp_path):
         ev.calculate_ppl("wikitext")
 
 
+GOLD_DIR = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["wikitext2", "ptb", "c4", "ptb_new", "c4_new"])
+def test_loaders_match_reference_get_loaders(name):
+    """ppl.load_local_tokens == the token ids the reference's own gptq/datautils.get_loaders returned
+    on the committed tiny datasets + tokenizer (tests/golden/make_golden_ppl.py): the joins, the
+    split choice, the c4 random windows (random.seed(0), 256 x seqlen) and the c4_new truncation."""
+    import os
+    from iron_weight_only_quant_amd.ppl import load_local_tokens
+    gold = np.load(os.path.join(GOLD_DIR, "ppl_tokens.npz"))
+    seqlen = int(gold["seqlen"])
+    fix = os.path.join(GOLD_DIR, "ppl_fixture")
+    ids = load_local_tokens(name, os.path.join(fix, "tokenizer"), seqlen, dataset_dir=os.path.join(fix, "datasets"))
+    assert ids.dim() == 2 and ids.shape[0] == 1
+    assert np.array_equal(ids.numpy().astype(np.int64), gold[name]), name
+
+
+def test_evaluator_dataset_map_and_hf_device_map():
+    """The evaluator's names map like main.py:45-49 (wikitext -> wikitext2, ptb -> get_ptb, c4 ->
+    get_c4), and an accelerate-dispatched model (hf_device_map) is fed on its embedding's device and
+    never moved (main.py:89-98) -- here 'cpu' while the evaluator's own device names a GPU."""
+    import os
+    gold = np.load(os.path.join(GOLD_DIR, "ppl_tokens.npz"))
+    seqlen = int(gold["seqlen"])
+    fix = os.path.join(GOLD_DIR, "ppl_fixture")
+    m = _tiny_opt()
+    tok_dir = os.path.join(fix, "tokenizer")
+    m.hf_device_map = {"model.decoder.embed_tokens": "cpu", "model.embed_tokens": "cpu", "lm_head": "cpu"}
+    moved = []
+    m.to = lambda *a, **k: moved.append(a) or m  # a dispatched model must not be moved
+    ev = SequentialPPLEvaluator(m, model_path=tok_dir, device="cuda:7", seqlen=seqlen,
+                                dataset_dir=os.path.join(fix, "datasets"))
+    assert ev.input_device() == (torch.device("cpu"), True)
+    vocab = 97
+    for name, key in (("wikitext", "wikitext2"), ("ptb", "ptb"), ("c4", "c4")):
+        toks = ev._load_tokens(name)
+        assert np.array_equal(toks.numpy(), gold[key]), name
+        ev.test_cache[key] = toks % vocab  # the tiny model's vocabulary
+        ppl, ntok, nch = ev.calculate_ppl(name, max_chunks=2)
+        assert nch == 2 and ntok == 2 * (seqlen - 1) and math.isfinite(ppl)
+    assert not moved
+    del m.hf_device_map["model.embed_tokens"]  # falls back to the map's first device
+    assert ev.input_device() == (torch.device("cpu"), True)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("w_bit,group", [(8, -2), (4, 128)])
 def test_ppl_delta_random_opt125m(w_bit, group):

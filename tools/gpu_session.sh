@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 WHAT=${1:-all}
 if [[ $WHAT == all || $WHAT == *tests* ]]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider
+  step pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread
 fi
 if [[ $WHAT == all || $WHAT == *smoke* ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"

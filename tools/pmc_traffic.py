@@ -12,6 +12,10 @@ import csv
 import json
 import os
 import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def counter(dirname, name, kernel):
@@ -41,6 +45,8 @@ def main():
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "dispatches": [nf, nw],
            "read_bytes_per_launch": read_bytes, "write_bytes_per_launch": write_bytes,
            "hbm_bytes_per_launch": read_bytes + write_bytes,
+           # bench.py trusts this record only while the headline kernel's sources are unchanged
+           "kernel_sources_sha": __import__("bench").kernel_sources_sha(),
            "correction": "FETCH_SIZE x 1024 x 2 (gfx950 half-count of 16B/lane streaming reads), WRITE_SIZE x 1024"}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(rec, open(a.out, "w"), indent=1)

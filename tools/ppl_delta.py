@@ -28,6 +28,9 @@ sys.path.insert(0, ROOT)
 def build_model(args):
     from transformers import AutoModelForCausalLM, OPTConfig, OPTForCausalLM, LlamaConfig, LlamaForCausalLM
     if args.model_path:
+        if args.device_map:  # utils.py:43-44: accelerate placement over the visible GPUs (e.g. a 70B)
+            return AutoModelForCausalLM.from_pretrained(args.model_path, torch_dtype=torch.float16,
+                                                        local_files_only=True, device_map=args.device_map)
         m = AutoModelForCausalLM.from_pretrained(args.model_path, torch_dtype=torch.float16, local_files_only=True)
         return m.cuda()
     torch.manual_seed(args.seed)
@@ -57,6 +60,11 @@ def main():
     ap.add_argument("--w_symmetric", action="store_true")
     ap.add_argument("--w_format", default="int")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device_map", default=None,
+                    help='e.g. "balanced" (the reference\'s placement, utils.py:43): the evaluator then feeds '
+                         'batches to the embedding\'s device (main.py:89-98)')
+    ap.add_argument("--fused_forward", default="false", choices=["false", "auto", "true"],
+                    help="QuantLinear forward on the packed codes (MI355X addition; false = the reference's F.linear)")
     args = ap.parse_args()
 
     from iron_weight_only_quant_amd.ppl import SequentialPPLEvaluator
@@ -71,10 +79,12 @@ def main():
     ev = SequentialPPLEvaluator(base, args.model_path, "cuda", seqlen=seqlen, tokens=tokens,
                                 dataset_dir=args.local_dataset_dir)
     ppl_fp16, ntok, nch = ev.calculate_ppl(args.dataset, max_chunks=args.max_chunks or None)
+    fused = {"false": False, "auto": "auto", "true": True}[args.fused_forward]
     for wb in args.w_bits:
-        model = copy.deepcopy(base)
+        # main.py:285-375 builds a fresh fp16 model per w_bit; a dispatched model is rebuilt the same way
+        model = build_model(args) if args.device_map else copy.deepcopy(base)
         qargs = SimpleNamespace(w_bit=wb, a_bit=16, w_group_size=args.w_group_size, w_symmetric=args.w_symmetric,
-                                w_format=args.w_format, quant_dim=0)
+                                w_format=args.w_format, quant_dim=0, fused_forward=fused)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         quantize_model(model, qargs, verbose=False)
