@@ -248,3 +248,26 @@ def test_lds_wait_lint_prefill_kernels():
     for name in names:
         i = text.index(name + ":")
         assert L.check_kernel(text[i:text.index(".Lfunc_end", i)].split("\n")) == [], name
+
+
+def test_host_abi_under_asan_ubsan():
+    """SURVEY.md §5 sanitizers: the C-ABI's host code (batch plans, argument validation, kernel and
+    split-K dispatch up to the launch) built from the library's own sources with host-side
+    AddressSanitizer + UndefinedBehaviorSanitizer (tests/asan/Makefile, host-only objects) and driven
+    by tests/asan/host_abi_check.c: every documented status, no sanitizer report (halt_on_error)."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists("/opt/rocm/bin/hipcc") or shutil.which("make") is None:
+        pytest.skip("hipcc / make not available")
+    jobs = str(min(8, os.cpu_count() or 1))
+    b = subprocess.run(["make", "-C", os.path.join(root, "tests", "asan"), "-j" + jobs], capture_output=True,
+                       text=True, timeout=900)
+    assert b.returncode == 0, b.stdout[-3000:] + b.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([os.path.join(root, "build", "asan", "host_abi_check")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "passed under ASan/UBSan" in r.stdout
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr

@@ -18,8 +18,11 @@ step() {  # step <name> <timeout> <cmd...>
   return $st
 }
 WHAT=${1:-all}
-if [[ $WHAT == all || $WHAT == *tests* ]]; then
+if [[ $WHAT == all || $WHAT == *fulltests* ]]; then
   step pytest_gpu 1000 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread
+fi
+if [[ $WHAT == *newtests* ]]; then
+  step pytest_new 900 python -u -m pytest ${NEWTESTS:-tests/test_gpu_quantize_model.py} -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread
 fi
 if [[ $WHAT == all || $WHAT == *smoke* ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
@@ -70,7 +73,8 @@ fi
 if [[ $WHAT == *dist2* ]]; then
   # rehearsal of the multi-rank bench on a 1-GPU box: 2 ranks share cuda:0 over gloo
   export IWQ_DIST_BACKEND=gloo
-  step dist2_7b 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2
+  # the driver's command form without torchrun: bench.py spawns its own ranks
+  step dist2_7b 600 python bench.py --gpus 2 --steps 5 --warmup 2 --gather
   step dist2_70b 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --model llama2-70b --steps 3 --warmup 1
   step dist2_7b_sg 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --model llama2-7b --steps 3 --warmup 1 --scatter --gather --no-shapes
   unset IWQ_DIST_BACKEND
