@@ -162,6 +162,25 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 13: return launch_variant_t<4, false, true, false>(a, st);             // default walk, plain stores
     case 14: return launch_variant_t<4, false, false, false>(a, st);            // plain loads + plain stores
     case 118: return launch_variant_t<4, false, true, true, true, false, true>(a, st);  // default walk, no arithmetic
+    // memory-stream probes on the same skeleton (no arithmetic): which walk moves the bytes fastest
+    case 119: return launch_variant_t<8, false, true, true, true, false, true>(a, st);     // 8 units in flight
+    case 120: return launch_variant_t<2, false, true, true, true, false, true>(a, st);     // 2 units in flight
+    case 121: return launch_variant_t<4, true, true, true, true, false, true>(a, st);      // + next loads prefetched
+    case 122: return launch_variant_t<4, false, true, true, true, true, true>(a, st);      // grid-stride walk
+    case 123: return launch_variant_t<4, false, true, true, true, false, true>(a, st, 4);  // 4 waves / SIMD
+    case 124: return launch_variant_t<8, false, true, true, true, false, true>(a, st, 4);  // 8 units, 4 waves / SIMD
+    case 125: return launch_variant_t<4, false, true, false, true, false, true>(a, st);    // plain stores
+    case 126: return launch_variant_t<4, false, false, true, true, false, true>(a, st);    // plain loads
+    case 127: return launch_variant_t<8, true, true, true, true, false, true>(a, st, 4);   // 8 units + prefetch, 4 waves
+    // the real kernel at lower residency (fewer concurrent streams), and more skeleton residencies
+    case 128: return launch_variant_t<4, false, true, true>(a, st, 3);                     // 3 waves / SIMD
+    case 129: return launch_variant_t<4, false, true, true>(a, st, 2);                     // 2 waves / SIMD
+    case 130: return launch_variant_t<4, false, true, true>(a, st, 5);                     // 5 waves / SIMD
+    case 131: return launch_variant_t<4, true, true, true>(a, st, 4);                      // prefetch, 4 waves / SIMD
+    case 132: return launch_variant_t<2, false, true, true>(a, st, 4);                     // 2 units, 4 waves / SIMD
+    case 133: return launch_variant_t<4, false, true, true, true, false, true>(a, st, 3);  // skeleton, 3 waves / SIMD
+    case 134: return launch_variant_t<4, false, true, true, true, false, true>(a, st, 2);  // skeleton, 2 waves / SIMD
+    case 135: return launch_variant_t<8, false, true, true, true, false, true>(a, st, 2);  // skeleton, 8 units, 2 waves
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
