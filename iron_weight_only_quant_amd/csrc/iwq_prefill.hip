@@ -1589,6 +1589,233 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32v(PrefillArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_w4a16_h2v (round 3, variants 98 / 99): b32v's per-wave work (128 rows x 64 columns, 4 x 2 tiles of
+// 32x32x16, the same hand-ordered slice stream, k order and accumulation order: bit-identical to 74)
+// on a HALF-width workgroup: 4 waves as 2 (M) x 2 (N), 256 x 128 output tile, a 2-stage LDS-DMA ring
+// of 36 KiB stages.  72 KiB of LDS and <= 256 registers per lane admit TWO workgroups per CU, so the
+// CU's 8 waves form two independent barrier domains: while one workgroup's waves wait at their
+// per-K-step barrier (or for a DMA), the other's keep the MFMA pipe busy (in 74 / b32v all 8 waves of
+// the CU share one barrier).  The ring's refill of the K-step after next is issued right after each
+// barrier and has a whole K-step to land (vmcnt(0) at the next barrier).  Per channel (scale in the
+// epilogue), as 74.
+// ---------------------------------------------------------------------------------------------
+constexpr int H2_TN = 128, H2_THR = 256, H2_NSTAGE = 2;
+constexpr int H2_CS = H2_TN * TK / 2;       // 4 KiB of codes per stage
+constexpr int H2_STAGE = XS + H2_CS;        // 36 KiB
+
+template <bool NIB>
+__global__ __launch_bounds__(H2_THR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_w4a16_h2v(PrefillArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[H2_NSTAGE * H2_STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tiles_n = a.N / H2_TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * H2_TN;
+  const int nk = a.K / TK;
+  const int64_t crow = a.K / 2;
+
+  // staging: 8 X pieces (8 rows of 128 B each) and 1 code piece (32 columns x 32 B) per wave per stage
+  const _Float16* xsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (wid * 8 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xswz(row)) << 3);
+  }
+  const int scol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + scol) * crow + (((lane & 1) ^ cswz(scol)) << 4);
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * H2_STAGE;
+    if (i < 8) glds16(xsrc[i] + kt * TK, base + (wid * 8 + i) * 1024);
+    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+  auto issue = [&](int kt, int stg) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) issue1(kt, stg, i);
+  };
+
+  h2 zz[2], zl[2], zh[2];
+  float sfl[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const _Float16 sc = gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    sfl[nt] = (float)sc;
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[4];
+  const int arow = wm * 128 + r32;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) la[s2] = lbase + (uint32_t)(arow * 128 + (((4 * h + s2) ^ xswz(arow)) << 4));
+  const int ccl = wn * 64 + r32;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + ((h ^ cswz(ccl)) << 4));  // + 1024 nt
+
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    if constexpr (NIB) {
+      const uint32_t t8 = w >> 8;
+      if (j == 0) return as_h2(and_or(w, m0_s, mg64)) - zl[nt];
+      if (j == 1) return as_h2(and_or(w, m1_s, mg54)) - zh[nt];
+      if (j == 2) return as_h2(and_or(t8, m0_s, mg64)) - zl[nt];
+      return as_h2(and_or(t8, m1_s, mg54)) - zh[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+  };
+
+  f16x acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  h8 af[4], bcur[2];
+  u32x4 wc[2];
+  h2 pn[2][4];
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+#define IWQ_MF(I) \
+  acc[(I) >> 1][(I) & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[(I) >> 1], bcur[(I) & 1], acc[(I) >> 1][(I) & 1], 0, 0, 0)
+#define IWQ_BSET()                                                                                 \
+  _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                  \
+    bcur[nt] = h8{pn[nt][0].x, pn[nt][0].y, pn[nt][1].x, pn[nt][1].y, pn[nt][2].x, pn[nt][2].y,     \
+                  pn[nt][3].x, pn[nt][3].y};
+#define IWQ_SLICE(NADDR, S1)                                                                       \
+  {                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                               \
+      if ((i & 1) == 0) IWQ_LGKM(3);                                                               \
+      IWQ_PIN();                                                                                   \
+      IWQ_MF(i);                                                                                   \
+      if (i & 1) af[i >> 1] = lds_rd<0>((NADDR) + 4096u * (uint32_t)(i >> 1));                     \
+      pn[i >> 2][i & 3] = dqp(wc[i >> 2][S1], i & 3, i >> 2);                                      \
+      IWQ_PIN();                                                                                   \
+    }                                                                                              \
+    IWQ_BSET()                                                                                     \
+  }
+
+  // prologue: stages 0 and 1 (K-step clamped to nk - 1: a re-load nobody reads)
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+  wc[0] = lds_rd_u<0>(lc);
+  wc[1] = lds_rd_u<1024>(lc);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) af[mt] = lds_rd<0>(la[0] + 4096u * (uint32_t)mt);
+  IWQ_LGKM(0);
+  landed(wc[0]);
+  landed(wc[1]);
+  IWQ_PIN();
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pn[nt][j] = dqp(wc[nt][0], j, nt);
+  IWQ_BSET()
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt & 1) * H2_STAGE);
+    IWQ_SLICE(la[1] + so, 1)
+    IWQ_SLICE(la[2] + so, 2)
+    IWQ_SLICE(la[3] + so, 3)
+    // stage kt+1 landed (nothing else in flight: 2-stage ring), every read of stage kt retired
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    const int kd = kt + 2 < nk ? kt + 2 : nk - 1;
+    const int sd = kt & 1;
+    const uint32_t sn = (uint32_t)(((kt + 1) & 1) * H2_STAGE);
+    u32x4 wq[2];
+    wq[0] = lds_rd_u<0>(lc + sn);
+    wq[1] = lds_rd_u<1024>(lc + sn);
+    const uint32_t na = la[0] + sn;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i == 2) {  // the code reads are older than the one A read issued since
+        IWQ_LGKM(1);
+        landed(wq[0]);
+        landed(wq[1]);
+      }
+      IWQ_PIN();
+      IWQ_MF(i);
+      if (i & 1) af[i >> 1] = lds_rd<0>(na + 4096u * (uint32_t)(i >> 1));
+      issue1(kd, sd, i);
+      if (i == 7) issue1(kd, sd, 8);
+      if (i == 2 || i == 3) {
+        const int q = (i - 2) * 2;
+        pn[0][q] = dqp(wq[0][0], q, 0);
+        pn[0][q + 1] = dqp(wq[0][0], q + 1, 0);
+      } else if (i >= 4) {
+        pn[1][i - 4] = dqp(wq[1][0], i - 4, 1);
+      }
+      IWQ_PIN();
+    }
+    IWQ_BSET()
+    wc[0] = wq[0];
+    wc[1] = wq[1];
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) & 1) * H2_STAGE);
+    IWQ_SLICE(la[1] + so, 1)
+    IWQ_SLICE(la[2] + so, 2)
+    IWQ_SLICE(la[3] + so, 3)
+    IWQ_LGKM(0);
+    IWQ_PIN();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) IWQ_MF(i);
+  }
+  // no LDS-DMA may still be landing when the workgroup retires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE
+#undef IWQ_BSET
+#undef IWQ_MF
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+  // epilogue (74's form): per-lane row pointer, row offsets uniform multiples of the pitch
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;
+  const bool full = m0 + TM <= a.M;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + wn * 64 + nt * 32 + r32;
+    const float b = a.bias ? (float)gp<_Float16>(a.bias)[col] : 0.0f;
+    char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + wm * 128 + 4 * h) * a.ldy + col) * 2;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = mt * 32 + (r & 3) + 8 * (r >> 2);
+        const _Float16 v = (_Float16)(opaque(acc[mt][nt][r] * sfl[nt]) + b);
+        if (full || m0 + wm * 128 + rr + 4 * h < a.M) *gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2)) = v;
+      }
+    }
+  }
+}
+
+template <bool NIB>
+hipError_t launch_h2v(const PrefillArgs& a, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / H2_TN);
+  hipLaunchKernelGGL((k_w4a16_h2v<NIB>), dim3((unsigned)blocks), dim3(H2_THR), 0, st, a);
+  return hipGetLastError();
+}
+
 template <bool NIB>
 hipError_t launch_v(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
@@ -2762,6 +2989,8 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 79: return launch_w4h<false, 2, true>(a, st);  // 2 x 2, LDS-DMA staging (3 stages)
     case 70: return launch_v<false>(a, st);             // 2 x 4 waves, hand-ordered stream
     case 71: return launch_v<true>(a, st);              // the same on NIB codes
+    case 98: return launch_h2v<false>(a, st);           // 2 x 2 waves of 128 x 64, 256 x 128 tiles, 2 WGs / CU
+    case 99: return launch_h2v<true>(a, st);            // the same on NIB codes
     case 80: return launch_w4b<false>(a, st);           // 2 x 2, weights dequantized once into LDS
     case 81: return launch_w4b<true>(a, st);            // the same on NIB codes
     default: return launch_w<false>(a, st);

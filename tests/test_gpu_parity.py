@@ -844,8 +844,9 @@ def test_w4a16_prefill_big_identity(K):
 # element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
 # The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
-B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80, 97), (47,), (48,))
-B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80), (47,))
+B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80, 97, 98), (47,),
+               (48,))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80, 98), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
 
@@ -859,7 +860,7 @@ def nib_layout(codes, N, K):
 
 
 # NIB-layout variants: same k order and accumulation order as their row-major twins
-B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45}
+B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -888,7 +889,7 @@ def test_w4a16_prefill_b32(K, M, sym, group):
             assert torch.equal(ys[v], ys[vs[0]]), (vs[0], v)
     nib = nib_layout(r.codes, N, Kd)
     for v, twin in B32_NIB.items():
-        if group != -2 and v in (67, 71, 77, 81):
+        if group != -2 and v in (67, 71, 77, 81, 99):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
