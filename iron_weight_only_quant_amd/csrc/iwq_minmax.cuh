@@ -59,6 +59,17 @@ int resident_blocks_per_cu(Kern kernel, int* cache) {
   return cache[dev];
 }
 
+// wave-uniform 64-bit values / pointers (readfirstlane of both halves)
+__device__ __forceinline__ int64_t rfl64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <typename P>
+__device__ __forceinline__ P rflp(P p) {
+  return (P)(uintptr_t)rfl64((int64_t)(uintptr_t)p);
+}
+
 __device__ __forceinline__ void flag_nan(uint32_t* nan_flag, bool any_nan) {
   // one atomic per wave at most
   uint64_t m = __ballot(any_nan);
@@ -822,6 +833,150 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
   flag_nan(nan_flag, any_nan);
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_tensor_onepass (round 3): per-tensor (-1) in ONE pass over HBM for fp16 weights that fit the
+// chip's registers.  One 512-thread workgroup per CU (2 waves per SIMD, up to 256 registers per lane:
+// two would not fit, so the grid of CU-count workgroups is co-resident -- up to ~100 MB of fp16
+// held, every Llama-2-7B shape); every thread loads its NV 16-B vectors (grid-stride,
+// coalesced) and KEEPS them in registers; the workgroup's (min, max) order keys (int16 for 16-bit
+// dtypes, packed in one dword) are published as one 8-byte granule {tag = 1, keys} by an agent-scope
+// atomic store (cdna_hip_programming.md Guideline 16 R2: the data is the flag, no fence); wave 0 of
+// every workgroup sweeps all granules (relaxed agent-scope atomic loads, bounded spin) until every
+// tag is 1, folds them, and the workgroup quantizes its registers and stores -- 4 B per element of
+// HBM traffic instead of the two-kernel pair's 6.  The granules (8 B x CU count, at the workspace's
+// start) are zeroed by a hipMemsetAsync before every launch.  A spin that gives up (a workgroup
+// not resident: another kernel holding CUs) sets bit 1 of nan_flag, so the call fails loudly.
+// ---------------------------------------------------------------------------------------------
+constexpr int OP_THR = 512;
+constexpr uint32_t OP_SPIN_LIMIT = 1u << 22;
+constexpr int OP_NT = 2;  // buffer-instruction cache bits: non-temporal (streamed once)
+
+// Workgroup b owns the contiguous vectors [b * NV * 512, (b + 1) * NV * 512) (16-B vectors of 8
+// elements); vector i of thread t is b * NV * 512 + i * 512 + t: every load / store instruction
+// covers 8 KiB contiguous per workgroup.  The loads go through a buffer descriptor over the
+// workgroup's chunk (one 32-bit per-lane offset for all NV vectors; the range check zero-fills the
+// last chunk's out-of-range loads, which the key fold masks).
+template <int DT, bool SYM, int CODES, int NV>
+__global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* out, uint8_t* codes, void* scales,
+                                                           void* zeros, int64_t nvec, unsigned long long* granules,
+                                                           int n_bits, uint32_t* nan_flag) {
+  using F = Fmt<DT>;
+  static_assert(DT == DT_F16, "one-pass per-tensor: fp16 (keys packed in one dword, packed fast path)");
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  __shared__ int32_t smn[OP_THR / 64], smx[OP_THR / 64];
+  __shared__ int32_t fin[2];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t chunk = (int64_t)NV * OP_THR;                     // vectors per workgroup
+  const int64_t v0 = (int64_t)blockIdx.x * chunk;                 // this workgroup's first vector
+  const int64_t nv_here = nvec - v0 < chunk ? nvec - v0 : chunk;  // > 0: one workgroup per non-empty chunk
+  const int nbytes = (int)(nv_here * 16);
+  const char* wb = static_cast<const char*>(rflp(static_cast<const void*>(w + v0 * 16)));
+  const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wb), 0, nbytes, 0x00020000);
+  const int voff = threadIdx.x * 16;
+  Vec8<DT> v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const u32x4v x = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, i * OP_THR * 16, OP_NT);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[i].u[j] = x[j];
+  }
+  int32_t mn = 0x7FFF, mx = -0x8000;  // int16 identities (every 16-bit order key lies in between)
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    int32_t a, b;
+    minmax8<DT, SYM>(v[i], a, b);
+    if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+      mn = min(mn, a);
+      mx = max(mx, b);
+    }
+  }
+  group_minmax<64>(mn, mx);
+  if (lane == 0) { smn[wv] = mn; smx[wv] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 1; i < OP_THR / 64; ++i) { mn = min(mn, smn[i]); mx = max(mx, smx[i]); }
+    const uint32_t keys = (uint32_t)(uint16_t)(int16_t)mn | ((uint32_t)(uint16_t)(int16_t)mx << 16);
+    __hip_atomic_store(granules + blockIdx.x, (1ull << 32) | keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wv == 0) {
+    // sweep every workgroup's granule until all carry tag 1 (relaxed agent-scope loads bypass L1)
+    const int ng = (int)gridDim.x;
+    int32_t gmn = 0x7FFF, gmx = -0x8000;
+    bool timed_out = false;
+    for (int g0 = 0; g0 < ng; g0 += 64) {
+      const int g = g0 + lane;
+      uint32_t spins = 0;
+      unsigned long long x = 0;
+      while (true) {
+        x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
+        if (__all((x >> 32) == 1ull)) break;
+        if (++spins > OP_SPIN_LIMIT) {
+          timed_out = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (g < ng && (x >> 32) == 1ull) {
+        gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
+        gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
+      }
+    }
+    group_minmax<64>(gmn, gmx);
+    if (lane == 0) {
+      fin[0] = gmn;
+      fin[1] = gmx;
+      if (timed_out && nan_flag) atomicOr(nan_flag, 2u);
+    }
+  }
+  __syncthreads();
+  const GroupParams p = params_from_keys<DT, SYM>(fin[0], fin[1], n_bits, rmax_for(n_bits, SYM));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (scales) store_param<DT>(scales, 0, p.s);
+    if (!SYM && zeros) store_param<DT>(zeros, 0, p.z);
+  }
+  // the stores are global stores: ROCm 7.2's LLVM omits the wait state a buffer_store_dwordx4 with an
+  // SGPR soffset needs before a VALU overwrites its data registers (the first dword of the stored
+  // vector was clobbered -- caught by the bit-exact tests), so the output leaves through 64-bit
+  // addresses with the range check done by hand
+  char* ob = out ? out + v0 * 16 + threadIdx.x * 16 : nullptr;
+  bool any_nan = false;
+  if (p.fast) {  // the packed fp16 path on the register-held vectors (uniform: one group)
+    const FastPk k = fast_pk<SYM>(p, n_bits);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      u32x4v o;
+      uint32_t c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t cp;
+        o[j] = quant2_fast<SYM>(v[i].u[j], p, k, cp);
+        c[j] = codes2_fast(cp, k);
+      }
+      if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+        if (ob) __builtin_nontemporal_store(o, gp<u32x4v>(static_cast<void*>(ob + (int64_t)i * OP_THR * 16)));
+        if constexpr (CODES != 0) store_codes8<CODES>(codes, (v0 + (int64_t)i * OP_THR + threadIdx.x) * 8, c);
+      }
+    }
+  } else {
+    // non-finite range / zero scale (never on real weights): the exact chain, each thread re-reading
+    // its own vectors (nothing else writes them, so this is right in place too)
+    for (int i = 0; i < NV; ++i) {
+      const int64_t u = v0 + (int64_t)i * OP_THR + threadIdx.x;
+      if (u < nvec) {
+        Vec8<DT> x, o;
+        x.template load<true>(w + u * 8 * F::BYTES);
+        uint32_t c[4];
+        any_nan |= quant8<DT, SYM>(x, p, n_bits, o, c);
+        if (out) o.template store<true>(out + u * 8 * F::BYTES);
+        if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+      }
+    }
+  }
+  flag_nan(nan_flag, any_nan);
+}
+
 template <int DT, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_seg_apply(SegArgs a) {
   using F = Fmt<DT>;
@@ -892,15 +1047,6 @@ struct BatchExArgs {
   uint32_t* nan_flag;
 };
 
-__device__ __forceinline__ int64_t rfl64(int64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-template <typename P>
-__device__ __forceinline__ P rflp(P p) {
-  return (P)(uintptr_t)rfl64((int64_t)(uintptr_t)p);
-}
 
 // largest e with entries[e].unit_begin <= u (u wave-uniform)
 __device__ __forceinline__ int32_t find_entry(const iwq_batch_entry* entries, int32_t n, int64_t u) {

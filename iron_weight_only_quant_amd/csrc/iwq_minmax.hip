@@ -370,9 +370,53 @@ void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, voi
                      zeros, nunits, ws, (int)blocks, n_bits, nan_flag);
 }
 
+// One-pass form (k_tensor_onepass, fp16): the tensor held in registers across the
+// in-launch exchange of the per-workgroup keys; NV 16-B vectors per thread, one 1024-thread
+// workgroup per CU.  Returns false (nothing launched) when the tensor does not fit (> 48 vectors per
+// thread: ~100 MB on 256 CUs).
+template <int DT, bool SYM, int CODES, int NV>
+hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nvec,
+                                    int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus) {
+  // one workgroup per NV * 512 vectors (<= the CU count: every chunk is non-empty and all are resident)
+  const int64_t chunk = (int64_t)NV * OP_THR;
+  const int64_t nblk = (nvec + chunk - 1) / chunk;
+  if (nblk < 1 || nblk > cus) return hipErrorInvalidValue;
+  const size_t gbytes = ((size_t)nblk * 8 + 15) / 16 * 16;  // the granules: zeroed before every launch
+  hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_tensor_onepass<DT, SYM, CODES, NV>), dim3((unsigned)nblk), dim3(OP_THR), 0, st,
+                     static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales, zeros,
+                     nvec, reinterpret_cast<unsigned long long*>(ws), n_bits, nan_flag);
+  return hipGetLastError();
+}
+template <int DT, bool SYM, int CODES>
+bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err) {
+  if constexpr (DT != DT_F16) {
+    return false;
+  } else {
+    const int cus = device_cu_count();
+    if (cus * 8 > (int64_t)TENSOR_PARTS_MAX * 8) return false;  // granules beyond the workspace
+    const int64_t nvec = numel / 8;
+    const int64_t per = (nvec + (int64_t)cus * OP_THR - 1) / ((int64_t)cus * OP_THR);
+    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
+    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
+    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
+    else return false;
+    return true;
+  }
+}
+
+// variants: 0 = one pass where the tensor fits the registers (fp16, n_bits <= 8), else the pair below;
+// 6 = the pair (round-2 default) forced
 template <int DT, bool SYM, int CODES>
 hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int variant) {
+  if (variant == 0) {
+    hipError_t e = hipSuccess;
+    if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e))
+      return e;
+  }
   const int64_t nunits = numel / 8;
   int64_t blocks = (int64_t)device_cu_count() * 8;
   const int64_t need = (nunits + BLOCK - 1) / BLOCK;

@@ -11,6 +11,7 @@ Produces (committed, data only):
   tests/golden/int_large.json  SHA-256 of reference outputs at Llama-2-7B shapes over oracle/synth inputs
   tests/golden/int_large_70b.json  the same at the four Llama-2-70B Linear shapes (configs[3])
                                    (`--only 70b` regenerates just this file)
+  tests/golden/int_large_pt.json   per-tensor (-1) at the 7B shapes (`--only pt`)
 
 Reference entry points exercised:
   quant_funcs.pseudo_quantize_tensor                  (quant_funcs.py:4-46)
@@ -223,7 +224,32 @@ def large70b_cases():
     return res
 
 
+def large_pt_cases():
+    """Per-tensor (-1) at the Llama-2-7B shapes on both reference entry points (round 3: the one-pass
+    per-tensor kernel holds a whole weight in registers)."""
+    res = {"generator": "oracle/synth.py (seed, shape) fp16", "cases": []}
+    for name, shp, seed in LARGE:
+        x = synth(seed, shp, "float16")
+        res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "input", "sha_input": sha(x)})
+        for bits, zp in ((4, True), (8, False)):
+            out = ref_qf(x, "float16", n_bits=bits, zero_point=zp, q_group_size=-1, per_tensor=True)
+            res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "qf_pt", "n_bits": bits,
+                                 "zero_point": zp, "sha_deq": sha(out)})
+        for bits, sym in ((4, False), (4, True), (8, False)):
+            deq, s, z, _ = ref_ql(x, "float16", w_bit=bits, w_group_size=-1, symmetric=sym)
+            res["cases"].append({"name": name, "shape": list(shp), "seed": seed, "kind": "ql", "w_bit": bits,
+                                 "symmetric": sym, "w_group_size": -1, "sha_deq": sha(deq), "sha_scales": sha(s),
+                                 "sha_zeros": None if z is None else sha(z)})
+        print("large_pt", name, flush=True)
+    return res
+
+
 if __name__ == "__main__":
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pt":
+        with open(os.path.join(HERE, "int_large_pt.json"), "w") as f:
+            json.dump(large_pt_cases(), f, indent=1)
+        print("large_pt done", flush=True)
+        sys.exit(0)
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "70b":
         with open(os.path.join(HERE, "int_large_70b.json"), "w") as f:
             json.dump(large70b_cases(), f, indent=1)
@@ -239,3 +265,6 @@ if __name__ == "__main__":
     with open(os.path.join(HERE, "int_large_70b.json"), "w") as f:
         json.dump(large70b_cases(), f, indent=1)
     print("large70b done", flush=True)
+    with open(os.path.join(HERE, "int_large_pt.json"), "w") as f:
+        json.dump(large_pt_cases(), f, indent=1)
+    print("large_pt done", flush=True)

@@ -17,6 +17,8 @@ import numpy as np
 import pytest
 import torch
 
+from oracle import iwq_oracle as O
+
 from .golden_util import GOLD, sha
 
 pytestmark = pytest.mark.gpu
@@ -198,3 +200,54 @@ def test_config3_fused_forward_m8192(K, name, group):
     yl = torch.nn.functional.linear(x, q.weight)
     assert float(((yl.float() - y.float()).abs()).max()) < 0.05, float(((yl.float() - y.float()).abs()).max())
     assert worst <= 1.0
+
+
+@pytest.mark.parametrize("name", ["q_proj", "gate_proj", "down_proj"])
+def test_per_tensor_one_pass_full_size(K, name):
+    """Per-tensor (-1) on the single-call path at the Llama-2-7B shapes: the one-pass kernel (the
+    whole weight held in registers, per-workgroup keys exchanged inside the launch) equals the
+    reference's SHA-256s (tests/golden/int_large_pt.json: pseudo_quantize_tensor(per_tensor=True)
+    and QuantLinear w_group_size=-1) and the two-kernel pair (variant 6), in place and out of place,
+    with packed codes; the exchange's timeout bit (nan_flag & 2) never fires."""
+    cases = [c for c in _cases("int_large_pt.json") if c["name"] == name]
+    inp = cases[0]
+    x = torch.empty(tuple(inp["shape"]), dtype=torch.float16, device=DEV)
+    K.fill_synthetic(x, inp["seed"])
+    assert sha(_np(x)) == inp["sha_input"]
+    for c in cases[1:]:
+        if c["kind"] == "qf_pt":
+            r = K.quantize_minmax(x, c["n_bits"], -1, not c["zero_point"], 0)
+            assert int(r.nan_flag.item()) == 0
+            assert sha(_np(r.out)) == c["sha_deq"], c
+        else:
+            r = K.quantize_minmax(x, c["w_bit"], -1, c["symmetric"], 0, want_codes=True)
+            assert int(r.nan_flag.item()) == 0
+            assert sha(_np(r.out)) == c["sha_deq"], c
+            assert sha(_np(r.scales).reshape(-1, 1)) == c["sha_scales"], c
+            if c["sha_zeros"] is not None:
+                assert sha(_np(r.zeros).reshape(-1, 1)) == c["sha_zeros"], c
+            r6 = K.quantize_minmax(x, c["w_bit"], -1, c["symmetric"], 0, want_codes=True,
+                                   flags=K.gemm_variant_flags(6))
+            assert torch.equal(r6.out.view(torch.int16), r.out.view(torch.int16))
+            assert torch.equal(r6.codes, r.codes)
+            y = x.clone()
+            ri = K.quantize_minmax(y, c["w_bit"], -1, c["symmetric"], 0, out=y)
+            assert torch.equal(y.view(torch.int16), r.out.view(torch.int16))
+            assert int(ri.nan_flag.item()) == 0
+
+
+@pytest.mark.parametrize("shape", [(1, 8), (3, 40), (48, 256), (1000, 1000), (2048, 3000)])
+@pytest.mark.parametrize("sym", [False, True])
+def test_per_tensor_one_pass_ragged(K, shape, sym):
+    """Small / ragged per-tensor sizes (one workgroup, partial chunks, a last chunk's out-of-range
+    buffer loads): equal to the oracle and to the two-kernel pair."""
+    from oracle.synth import synth as _synth
+    x_np = _synth(77 + shape[0], shape, "float16")
+    x = torch.from_numpy(x_np).to(DEV)
+    ref = O.quantlinear_int(x_np, w_bit=4, w_group_size=-1, symmetric=sym)
+    r = K.quantize_minmax(x, 4, -1, sym, 0, want_codes=shape[1] % 2 == 0)
+    assert np.array_equal(_np(r.out).view(np.uint16), ref.dequant.view(np.uint16)), shape
+    assert np.array_equal(_np(r.scales).view(np.uint16), ref.scales.reshape(-1).view(np.uint16))
+    r6 = K.quantize_minmax(x, 4, -1, sym, 0, flags=K.gemm_variant_flags(6))
+    assert torch.equal(r6.out.view(torch.int16), r.out.view(torch.int16))
+    assert int(r.nan_flag.item()) == 0
