@@ -232,6 +232,18 @@ def test_lds_wait_lint_model():
     assert len(L.check_kernel(order)) == 1
 
 
+def test_store_hazard_lint_model():
+    """The buffer-store data hazard: the instruction right after a 16-byte buffer store may not
+    write that store's data registers (ROCm 7.2 LLVM omits the wait state with an SGPR soffset)."""
+    L = _lint()
+    bad = ["buffer_store_dwordx4 v[58:61], v2, s[8:11], s2 offen nt", "v_mov_b32_e32 v58, 0"]
+    assert len(L.check_store_hazard(bad)) == 1
+    ok = ["buffer_store_dwordx4 v[58:61], v2, s[8:11], s2 offen nt", "s_nop 0", "v_mov_b32_e32 v58, 0"]
+    assert L.check_store_hazard(ok) == []
+    reads = ["buffer_store_dwordx4 v[58:61], v2, s[8:11], s2 offen", "v_add_u32_e32 v3, v58, v2"]
+    assert L.check_store_hazard(reads) == []
+
+
 def test_lds_wait_lint_prefill_kernels():
     """Every hand-ordered prefill kernel (inline-asm LDS access, hand-counted lgkmcnt) as compiled
     for gfx950: no register of an LDS read is touched before its wait retires it."""

@@ -9,7 +9,12 @@ still-pending read is reported (a use before the data landed, or an overwrite ra
 Straight-line model: branches are ignored, which is exact for these kernels' loop bodies (one basic
 block each) and conservative at block boundaries.
 
-usage: python tools/check_lds_waits.py [--asm file.s]   (exit 1 on any finding)"""
+Second check (--store-hazard, every csrc/*.hip): a buffer_store_dwordx3/x4 whose data VGPRs the very
+next instruction overwrites.  ROCm 7.2's LLVM inserts no wait state there when the store carries an
+SGPR soffset, and gfx950 then stores the overwritten value (seen as scattered garbage dwords in the
+per-tensor one-pass kernel's output before it moved to global stores).
+
+usage: python tools/check_lds_waits.py [--asm file.s] [--store-hazard]   (exit 1 on any finding)"""
 import argparse
 import os
 import re
@@ -67,9 +72,42 @@ def check_kernel(lines):
     return findings
 
 
+def check_store_hazard(lines):
+    """(line, store, next) for each >8-byte buffer store whose data registers the next instruction writes."""
+    insts = [(n, r.strip()) for n, r in enumerate(lines)
+             if r.strip() and not r.strip().startswith((";", ".")) and not r.strip().endswith(":")]
+    out = []
+    for (n, t), (_, nxt) in zip(insts, insts[1:]):
+        if not re.match(r"buffer_store_dwordx[34]\b", t):
+            continue
+        data = vregs(t.split(None, 1)[1].split(",")[0])
+        parts = nxt.split(None, 1)
+        if len(parts) == 2 and not parts[0].startswith(("s_", "buffer_store", "global_store", "ds_write")):
+            if vregs(parts[1].split(",")[0]) & data:
+                out.append((n, t, nxt))
+    return out
+
+
+def store_hazard_all():
+    bad = 0
+    with tempfile.TemporaryDirectory() as d:
+        for f in sorted(os.listdir(CSRC)):
+            if not f.endswith(".hip"):
+                continue
+            out = os.path.join(d, f + ".s")
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                            "-ffp-contract=off", "--offload-device-only", "-S", os.path.join(CSRC, f),
+                            "-I", CSRC, "-o", out], check=True, capture_output=True)
+            found = check_store_hazard(open(out).read().split("\n"))
+            bad += len(found)
+            print(f"{f}: {len(found)} store-data hazard(s)" + "".join(f"\n    line {n}: {t}  ->  {x}" for n, t, x in found[:5]))
+    return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--asm", help="existing gfx950 assembly of iwq_prefill.hip")
+    ap.add_argument("--store-hazard", action="store_true", help="also scan every csrc/*.hip for the buffer-store data hazard")
     a = ap.parse_args()
     if a.asm:
         text = open(a.asm).read()
@@ -87,6 +125,8 @@ def main():
         bad += len(f)
         print(f"{name}: {len(f)} finding(s)" + "".join(f"\n    line {n}: {t}" for n, t in f[:5]))
     print(f"{len(names)} kernels checked, {bad} finding(s)")
+    if a.store_hazard:
+        bad += store_hazard_all()
     return 1 if bad or not names else 0
 
 
