@@ -371,9 +371,9 @@ void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, voi
 }
 
 // One-pass form (k_tensor_onepass, fp16): the tensor held in registers across the
-// in-launch exchange of the per-workgroup keys; NV 16-B vectors per thread, one 1024-thread
+// in-launch exchange of the per-workgroup keys; NV 16-B vectors per thread, one 512-thread
 // workgroup per CU.  Returns false (nothing launched) when the tensor does not fit (> 48 vectors per
-// thread: ~100 MB on 256 CUs).
+// thread: ~100 MB on 256 CUs) or there is no nan_flag to report a hand-off timeout through.
 template <int DT, bool SYM, int CODES, int NV>
 hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nvec,
                                     int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus) {
@@ -395,6 +395,7 @@ bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, 
   if constexpr (DT != DT_F16) {
     return false;
   } else {
+    if (nan_flag == nullptr) return false;  // a timed-out hand-off must be reportable (bit 1)
     const int cus = device_cu_count();
     if (cus * 8 > (int64_t)TENSOR_PARTS_MAX * 8) return false;  // granules beyond the workspace
     const int64_t nvec = numel / 8;

@@ -21,10 +21,14 @@ class QuantResult:
     scales: Optional[torch.Tensor]    # [G] storage dtype
     zeros: Optional[torch.Tensor]     # [G] storage dtype (asymmetric) or None
     codes: Optional[torch.Tensor]     # packed uint8 codes (include/iwq.h layout) or None
-    nan_flag: torch.Tensor            # [1] int32 on device; nonzero if the output holds a NaN
+    nan_flag: torch.Tensor            # [1] int32 on device; bit 0: the output holds a NaN
 
     def has_nan(self) -> bool:
-        return bool(self.nan_flag.item() != 0)
+        v = int(self.nan_flag.item())
+        if v & 2:  # include/iwq.h: the per-tensor one-pass hand-off timed out, the outputs are invalid
+            raise RuntimeError("iwq: per-tensor one-pass kernel timed out waiting for its workgroups "
+                               "(not all resident); outputs invalid")
+        return v != 0
 
 
 class _FlagPool:

@@ -283,3 +283,13 @@ def test_host_abi_under_asan_ubsan():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "passed under ASan/UBSan" in r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+
+
+def test_quant_result_timeout_bit_raises():
+    """include/iwq.h nan_flag bit 1 (the per-tensor one-pass hand-off timed out) is an error, not a NaN."""
+    from iron_weight_only_quant_amd.kernels import QuantResult
+    ok = QuantResult(None, None, None, None, torch.tensor([0], dtype=torch.int32))
+    nan = QuantResult(None, None, None, None, torch.tensor([1], dtype=torch.int32))
+    assert not ok.has_nan() and nan.has_nan()
+    with pytest.raises(RuntimeError, match="timed out"):
+        QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32)).has_nan()
