@@ -321,6 +321,19 @@ int iwq_nib_codes(const void* codes, int64_t N, int64_t K, void* out, void* stre
 int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros, int n_bits, int64_t group,
                        int64_t N, int64_t K, void* out, int64_t ld_out, void* stream);
 
+/*
+ * Packed codes (layout above) -> the dequantized weight, for EVERY INT mode the quantizer writes codes
+ * for: n_bits 1..8 (symmetric: 2..8), group > 0 / IWQ_GROUP_PER_TENSOR / IWQ_GROUP_PER_CHANNEL,
+ * quant_dim 0 / 1, storage dtype F16 / BF16 / F32 (scales, zeros and out all in that dtype).
+ * out[r * ld_out + c] = RN_dtype((code - z) * s) with (s, z) of element (r, c)'s group -- bit-identical
+ * to the out_deq iwq_quantize_minmax wrote alongside those codes (quant_funcs.py:38 /
+ * quant_linear.py:947).  zeros ignored (may be NULL) when symmetric.  Load-time inverse of the packed
+ * format (the packed checkpoint, checkpoint.py); the reference has no counterpart (it keeps no codes).
+ */
+int iwq_dequant_codes(const void* codes, const void* scales, const void* zeros, int dtype, int n_bits,
+                      int64_t group, int symmetric, int quant_dim, int64_t rows, int64_t cols, void* out,
+                      int64_t ld_out, void* stream);
+
 /* Deterministic synthetic weights (oracle/synth.py bit-for-bit), written to [rows, cols] contiguous. */
 int iwq_fill_synthetic(void* out, int64_t n, int dtype, uint64_t seed, int64_t index_offset, void* stream);
 

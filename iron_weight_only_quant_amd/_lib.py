@@ -32,7 +32,7 @@ EXPORTS = (
     "iwq_selftest_division", "iwq_quantize_fp", "iwq_fp4_grid", "iwq_w4a16_gemm",
     "iwq_approx_workspace_bytes", "iwq_quantize_fp_approx", "iwq_quantize_bfp",
     "iwq_fp_build_lut", "iwq_quantize_fp_lut", "iwq_quantize_fp_approx_lut", "iwq_fp4_grid_lut",
-    "iwq_dequant_packed", "iwq_quantize_fp_batched", "iwq_tile_codes", "iwq_nib_codes",
+    "iwq_dequant_packed", "iwq_dequant_codes", "iwq_quantize_fp_batched", "iwq_tile_codes", "iwq_nib_codes",
     "iwq_w4a16_gemm_workspace_bytes", "iwq_w4a16_gemm_ws", "iwq_fp4_grid_packed", "iwq_dequant_fp_packed",
     "iwq_batch_plan_ex", "iwq_batch_workspace_bytes", "iwq_quantize_minmax_batched_ex",
 )
@@ -135,6 +135,8 @@ def load():
         lib.iwq_nib_codes.restype = i32
         lib.iwq_dequant_packed.argtypes = [vp, vp, vp, i32, i64, i64, i64, vp, i64, vp]
         lib.iwq_dequant_packed.restype = i32
+        lib.iwq_dequant_codes.argtypes = [vp, vp, vp, i32, i32, i64, i32, i32, i64, i64, vp, i64, vp]
+        lib.iwq_dequant_codes.restype = i32
         lib.iwq_selftest_division.argtypes = [vp, vp]
         lib.iwq_selftest_division.restype = i32
         _lib = lib

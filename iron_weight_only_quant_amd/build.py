@@ -7,7 +7,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
 SOURCES = ["iwq_minmax.hip", "iwq_batched.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
-           "iwq_fpunpack.hip"]
+           "iwq_fpunpack.hip", "iwq_codes.hip"]
 DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Numerics: no FMA contraction, IEEE fp32 division, denormals preserved.

@@ -513,6 +513,39 @@ def dequant_packed(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[to
     return out
 
 
+def dequant_codes(codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor], n_bits: int,
+                  group: int, symmetric: bool, quant_dim: int, rows: int, cols: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed codes of any INT mode (include/iwq.h layout) -> the dequantized [rows, cols] weight in
+    the scales' dtype, bit-identical to what quantize_minmax(..., want_codes=True) returned as `out`
+    next to those codes (iwq_dequant_codes)."""
+    L.require_device(codes)
+    dev, dt = codes.device, scales.dtype
+    if dt not in L.DTYPE_CODE:
+        raise TypeError(f"dequant_codes: unsupported parameter dtype {dt}")
+    if not 1 <= n_bits <= 8:
+        raise ValueError("dequant_codes: codes exist for 1 <= n_bits <= 8")
+    _, G = group_geometry(rows, cols, group, quant_dim)
+    if codes.dtype != torch.uint8 or not codes.is_contiguous() or codes.numel() != codes_nbytes(rows, cols, n_bits):
+        raise ValueError(f"dequant_codes: codes must be contiguous uint8 of {codes_nbytes(rows, cols, n_bits)} bytes")
+    for name, t in (("scales", scales), ("zeros", None if symmetric else zeros)):
+        if name == "zeros" and t is None and not symmetric:
+            raise ValueError("dequant_codes: asymmetric codes need zeros")
+        if t is not None and (t.device != dev or t.dtype != dt or not t.is_contiguous() or t.numel() != G):
+            raise ValueError(f"dequant_codes: {name} must be {G} contiguous {dt} values on {dev}")
+    if out is None:
+        out = torch.empty((rows, cols), dtype=dt, device=dev)
+    elif out.dtype != dt or out.device != dev or out.shape != (rows, cols) or out.stride(1) != 1:
+        raise ValueError("dequant_codes: out must be a [rows, cols] tensor of the scales' dtype, unit column stride")
+    lib = L.load()
+    with L.on_device(dev):
+        st = lib.iwq_dequant_codes(L.ptr(codes), L.ptr(scales), None if symmetric else L.ptr(zeros),
+                                   L.DTYPE_CODE[dt], int(n_bits), int(group), int(bool(symmetric)), int(quant_dim),
+                                   int(rows), int(cols), L.ptr(out), out.stride(0), L.stream_handle(dev))
+    _raise_for(st, "iwq_dequant_codes")
+    return out
+
+
 def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                  n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None,
                  tiled_codes: Optional[torch.Tensor] = None,
