@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+
 using namespace iwq;
 using iwq::seg::SegArgs;
 using iwq::seg::SEG_RUN;
@@ -43,6 +45,17 @@ int device_cu_count() {
     cached[dev] = n;
   }
   return cached[dev];
+}
+
+// Per-launch granule tag of the one-pass per-tensor kernel when the granules are not zeroed first
+// (A/B variant 8): process-wide, never 0 or 1 (1 is the memset form's tag).
+uint32_t next_onepass_tag() {
+  static std::atomic<uint32_t> counter{1};
+  uint32_t t;
+  do {
+    t = counter.fetch_add(1, std::memory_order_relaxed) + 1;
+  } while (t < 2);
+  return t;
 }
 
 // Resident 256-thread blocks per CU for a kernel (occupancy API: VGPRs/LDS; SGPRs are capped at
@@ -851,15 +864,18 @@ constexpr int OP_THR = 512;
 constexpr uint32_t OP_SPIN_LIMIT = 1u << 22;
 constexpr int OP_NT = 2;  // buffer-instruction cache bits: non-temporal (streamed once)
 
-// Workgroup b owns the contiguous vectors [b * NV * 512, (b + 1) * NV * 512) (16-B vectors of 8
-// elements); vector i of thread t is b * NV * 512 + i * 512 + t: every load / store instruction
-// covers 8 KiB contiguous per workgroup.  The loads go through a buffer descriptor over the
-// workgroup's chunk (one 32-bit per-lane offset for all NV vectors; the range check zero-fills the
-// last chunk's out-of-range loads, which the key fold masks).
+// Workgroup b owns the contiguous vectors [b * nvt * 512, (b + 1) * nvt * 512) (16-B vectors of 8
+// elements; nvt <= NV vectors per thread, chosen so the chunks spread over every CU); vector i of
+// thread t is b * nvt * 512 + i * 512 + t: every load / store instruction covers 8 KiB contiguous per
+// workgroup.  The loads go through a buffer descriptor over the workgroup's chunk (one 32-bit per-lane
+// offset for all vectors; the range check zero-fills loads beyond the chunk -- i >= nvt, or the last
+// chunk's tail -- without touching memory, and the key fold masks them).  A granule counts once its
+// tag equals this launch's `tag` (1 after the per-launch memset).
 template <int DT, bool SYM, int CODES, int NV>
 __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* out, uint8_t* codes, void* scales,
-                                                           void* zeros, int64_t nvec, unsigned long long* granules,
-                                                           int n_bits, uint32_t* nan_flag) {
+                                                           void* zeros, int64_t nvec, int nvt,
+                                                           unsigned long long* granules, uint32_t tag, int n_bits,
+                                                           uint32_t* nan_flag) {
   using F = Fmt<DT>;
   static_assert(DT == DT_F16, "one-pass per-tensor: fp16 (keys packed in one dword, packed fast path)");
   typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -867,7 +883,7 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   __shared__ int32_t fin[2];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t chunk = (int64_t)NV * OP_THR;                     // vectors per workgroup
+  const int64_t chunk = (int64_t)nvt * OP_THR;                    // vectors per workgroup
   const int64_t v0 = (int64_t)blockIdx.x * chunk;                 // this workgroup's first vector
   const int64_t nv_here = nvec - v0 < chunk ? nvec - v0 : chunk;  // > 0: one workgroup per non-empty chunk
   const int nbytes = (int)(nv_here * 16);
@@ -884,11 +900,13 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   int32_t mn = 0x7FFF, mx = -0x8000;  // int16 identities (every 16-bit order key lies in between)
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    int32_t a, b;
-    minmax8<DT, SYM>(v[i], a, b);
-    if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
-      mn = min(mn, a);
-      mx = max(mx, b);
+    if (i < nvt) {  // uniform (a branch, not a break: the loop must stay fully unrolled)
+      int32_t a, b;
+      minmax8<DT, SYM>(v[i], a, b);
+      if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+        mn = min(mn, a);
+        mx = max(mx, b);
+      }
     }
   }
   group_minmax<64>(mn, mx);
@@ -898,10 +916,12 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
 #pragma unroll
     for (int i = 1; i < OP_THR / 64; ++i) { mn = min(mn, smn[i]); mx = max(mx, smx[i]); }
     const uint32_t keys = (uint32_t)(uint16_t)(int16_t)mn | ((uint32_t)(uint16_t)(int16_t)mx << 16);
-    __hip_atomic_store(granules + blockIdx.x, (1ull << 32) | keys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(granules + blockIdx.x, ((unsigned long long)tag << 32) | keys, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   if (wv == 0) {
-    // sweep every workgroup's granule until all carry tag 1 (relaxed agent-scope loads bypass L1)
+    // sweep every workgroup's granule until all carry this launch's tag (relaxed agent-scope loads
+    // bypass L1)
     const int ng = (int)gridDim.x;
     int32_t gmn = 0x7FFF, gmx = -0x8000;
     bool timed_out = false;
@@ -910,15 +930,16 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
       uint32_t spins = 0;
       unsigned long long x = 0;
       while (true) {
-        x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
-        if (__all((x >> 32) == 1ull)) break;
+        x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : ((unsigned long long)tag << 32);
+        if (__all((uint32_t)(x >> 32) == tag)) break;
         if (++spins > OP_SPIN_LIMIT) {
           timed_out = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (g < ng && (x >> 32) == 1ull) {
+      if (g < ng && (uint32_t)(x >> 32) == tag) {
         gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
         gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
       }
@@ -946,25 +967,27 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
     const FastPk k = fast_pk<SYM>(p, n_bits);
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      u32x4v o;
-      uint32_t c[4];
+      if (i < nvt) {  // uniform
+        u32x4v o;
+        uint32_t c[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t cp;
-        o[j] = quant2_fast<SYM>(v[i].u[j], p, k, cp);
-        c[j] = codes2_fast(cp, k);
-      }
-      if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
-        if (ob) __builtin_nontemporal_store(o, gp<u32x4v>(static_cast<void*>(ob + (int64_t)i * OP_THR * 16)));
-        if constexpr (CODES != 0) store_codes8<CODES>(codes, (v0 + (int64_t)i * OP_THR + threadIdx.x) * 8, c);
+        for (int j = 0; j < 4; ++j) {
+          uint32_t cp;
+          o[j] = quant2_fast<SYM>(v[i].u[j], p, k, cp);
+          c[j] = codes2_fast(cp, k);
+        }
+        if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+          if (ob) __builtin_nontemporal_store(o, gp<u32x4v>(static_cast<void*>(ob + (int64_t)i * OP_THR * 16)));
+          if constexpr (CODES != 0) store_codes8<CODES>(codes, (v0 + (int64_t)i * OP_THR + threadIdx.x) * 8, c);
+        }
       }
     }
   } else {
     // non-finite range / zero scale (never on real weights): the exact chain, each thread re-reading
     // its own vectors (nothing else writes them, so this is right in place too)
-    for (int i = 0; i < NV; ++i) {
+    for (int i = 0; i < nvt; ++i) {
       const int64_t u = v0 + (int64_t)i * OP_THR + threadIdx.x;
-      if (u < nvec) {
+      if (u < v0 + nv_here) {
         Vec8<DT> x, o;
         x.template load<true>(w + u * 8 * F::BYTES);
         uint32_t c[4];

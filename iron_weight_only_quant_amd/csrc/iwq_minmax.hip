@@ -376,22 +376,29 @@ void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, voi
 // thread: ~100 MB on 256 CUs) or there is no nan_flag to report a hand-off timeout through.
 template <int DT, bool SYM, int CODES, int NV>
 hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nvec,
-                                    int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus) {
-  // one workgroup per NV * 512 vectors (<= the CU count: every chunk is non-empty and all are resident)
-  const int64_t chunk = (int64_t)NV * OP_THR;
+                                    int nvt, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus,
+                                    bool memset_tags) {
+  // one workgroup per nvt * 512 vectors (<= the CU count: every chunk is non-empty and all are resident)
+  const int64_t chunk = (int64_t)nvt * OP_THR;
   const int64_t nblk = (nvec + chunk - 1) / chunk;
-  if (nblk < 1 || nblk > cus) return hipErrorInvalidValue;
-  const size_t gbytes = ((size_t)nblk * 8 + 15) / 16 * 16;  // the granules: zeroed before every launch
-  hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
-  if (e != hipSuccess) return e;
+  if (nvt < 1 || nvt > NV || nblk < 1 || nblk > cus) return hipErrorInvalidValue;
+  uint32_t tag = 1;
+  if (memset_tags) {
+    const size_t gbytes = ((size_t)nblk * 8 + 15) / 16 * 16;  // the granules: zeroed before the launch
+    hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
+    if (e != hipSuccess) return e;
+  } else {
+    tag = next_onepass_tag();
+  }
   hipLaunchKernelGGL((k_tensor_onepass<DT, SYM, CODES, NV>), dim3((unsigned)nblk), dim3(OP_THR), 0, st,
                      static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales, zeros,
-                     nvec, reinterpret_cast<unsigned long long*>(ws), n_bits, nan_flag);
+                     nvec, nvt, reinterpret_cast<unsigned long long*>(ws), tag, n_bits, nan_flag);
   return hipGetLastError();
 }
 template <int DT, bool SYM, int CODES>
 bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
-                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err) {
+                           int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err,
+                           bool memset_tags, bool fixed_nv) {
   if constexpr (DT != DT_F16) {
     return false;
   } else {
@@ -400,22 +407,25 @@ bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, 
     if (cus * 8 > (int64_t)TENSOR_PARTS_MAX * 8) return false;  // granules beyond the workspace
     const int64_t nvec = numel / 8;
     const int64_t per = (nvec + (int64_t)cus * OP_THR - 1) / ((int64_t)cus * OP_THR);
-    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
-    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
-    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, ws, n_bits, nan_flag, st, cus);
+    // nvt = per spreads the chunks over every CU; fixed_nv (A/B) uses the template's NV instead
+    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags);
+    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags);
+    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags);
     else return false;
     return true;
   }
 }
 
 // variants: 0 = one pass where the tensor fits the registers (fp16, n_bits <= 8), else the pair below;
-// 6 = the pair (round-2 default) forced
+// 6 = the pair (round-2 default) forced; 7 = one pass with NV vectors per thread (the first form:
+// fewer, fuller chunks, some CUs idle); 8 = one pass with per-launch tags instead of the memset (A/B)
 template <int DT, bool SYM, int CODES>
 hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int variant) {
-  if (variant == 0) {
+  if (variant == 0 || variant == 7 || variant == 8) {
     hipError_t e = hipSuccess;
-    if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e))
+    if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e,
+                                              variant != 8, variant == 7))
       return e;
   }
   const int64_t nunits = numel / 8;
