@@ -759,10 +759,11 @@ def test_quantlinear_fused_forward_auto(K, monkeypatch):
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
 def test_per_tensor_fast_path(K, dtype):
     """group -1 (per-tensor) on a tensor big enough for many partial-key workgroups, quant_dim 0 and 1,
-    sym / asym, with codes: the two-kernel reduce + apply path vs the oracle, bit-exact."""
+    sym / asym, with codes: the default path (fp16 quant_dim 0: the one-pass kernel; else the
+    two-kernel reduce + apply) and the pair's variants vs the oracle, bit-exact."""
     x = synth(55, (1536, 2048), dtype)
     big = np.float32(-3.25)  # a single outlier decides the scale
-    x.reshape(-1)[123457] = O.f32_to_bf16_bits(big) if dtype == "bfloat16" else big
+    x.reshape(-1)[123457] = O.f32_to_bf16_bits(big).reshape(-1)[0] if dtype == "bfloat16" else big
     xd = to_dev(x, dtype)
     for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
