@@ -767,8 +767,9 @@ def test_per_tensor_fast_path(K, dtype):
     xd = to_dev(x, dtype)
     for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
-        # + per-tensor kernel-pair variants 1 (non-temporal) and 3 (apply walks backwards)
-        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4, 5)]:
+        # + pair variants 1 (non-temporal), 3 (apply walks backwards), 4 / 5 (apply unrolled), 6 (the
+        # pair forced), one-pass variants 7 (NV vectors per thread) and 8 (per-launch tags, no memset)
+        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4, 5, 6, 7, 8)]:
             r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
             assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
             assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)
