@@ -373,6 +373,20 @@ FUSED_MAX_M = 1024
 NIB_MIN_M = 256
 
 
+def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
+    """QuantLinear(fused_forward="auto"): whether the packed-code kernels beat the reference forward
+    F.linear(x, W_deq) (hipBLASLt on the resident fp16 weight) for an M-row batch on an [N, K] weight.
+    Measured COLD (each layer's weight read once per forward, as in a model; profiles/
+    r03_ab_auto_cold.jsonl, Llama-2-7B q / gate / down, 4-bit): per channel the fused kernels win at
+    every M <= 192 (1.05-2.6x), g128 at every M <= 64 (1.09-2.25x) and up to 192 on N <= K weights
+    (q / down: 1.11-1.75x; gate_proj 0.93-0.97x there); at M = 255 and above hipBLASLt wins."""
+    if M <= 64:
+        return True
+    if M <= 192:
+        return group == -2 or N <= K
+    return False
+
+
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
     g = K if group == -2 else group
     return (x.is_cuda and x.dtype == torch.float16 and 2 <= n_bits <= 4 and N % 128 == 0 and K % 128 == 0

@@ -240,15 +240,18 @@ class QuantLinear(nn.Module):
 
         With fused_forward=True (INT, 2-4 bits, quant_dim 0) the GEMM reads the packed codes instead
         (kernels.w4a16_gemm, MFMA): same weights, fp32 accumulation in a different order.
-        fused_forward="auto" takes the packed-weight kernel only where it is the faster one: decode
-        batches (M <= 16 rows: the weight-streaming GEMV, 1.8-3.6x hipBLASLt); larger M run
-        F.linear on the resident dequantized weight, like the reference."""
+        fused_forward="auto" takes the packed-weight kernels only where they are the faster ones
+        (kernels.auto_fused_preferred, measured cold): decode batches (M <= 16 rows: the
+        weight-streaming GEMV on the tile-layout codes, 1.4-2.2x hipBLASLt) and prompt-sized
+        batches up to 64 rows (192 per channel, or on N <= K weights); larger M run F.linear on the
+        resident dequantized weight, like the reference."""
         if not self.quantized:
             return F.linear(input, self.weight, self.bias)
         fused = self.fused_forward
         if fused == "auto":
-            fused = input.numel() // max(1, self.in_features) <= kernels.GEMV_MAX_M
-            if fused and self.qweight_tiled is not None and self._fused_ok(input):
+            m = input.numel() // max(1, self.in_features)
+            fused = kernels.auto_fused_preferred(m, self.out_features, self.in_features, self.w_group_size)
+            if fused and m <= kernels.GEMV_MAX_M and self.qweight_tiled is not None and self._fused_ok(input):
                 return kernels.w4a16_gemm(input, self.qweight_tiled, self.scales.view(-1),
                                           None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                           self.w_group_size, self.out_features, self.bias, tiled=True)

@@ -293,3 +293,13 @@ def test_quant_result_timeout_bit_raises():
     assert not ok.has_nan() and nan.has_nan()
     with pytest.raises(RuntimeError, match="timed out"):
         QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32)).has_nan()
+
+
+def test_auto_fused_policy():
+    """QuantLinear(fused_forward="auto")'s rule (kernels.auto_fused_preferred, profiles/
+    r03_ab_auto_cold.jsonl): fused up to 64 rows, up to 192 per channel or on N <= K, F.linear above."""
+    from iron_weight_only_quant_amd.kernels import auto_fused_preferred as P
+    assert P(1, 11008, 4096, 128) and P(64, 11008, 4096, 128)
+    assert P(128, 11008, 4096, -2) and not P(128, 11008, 4096, 128)
+    assert P(192, 4096, 11008, 128) and P(192, 4096, 4096, 128)
+    assert not P(193, 4096, 4096, -2) and not P(8192, 4096, 4096, -2)

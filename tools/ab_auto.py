@@ -1,0 +1,80 @@
+"""Where should QuantLinear(fused_forward="auto") take the packed-code kernels?  COLD A/B of the
+reference forward F.linear(x, W_deq) (hipBLASLt on the resident fp16 weight) against the fused
+forward kernels.w4a16_gemm on the packed codes (tiled codes at M <= 16, as "auto" keeps them), per
+Llama-2-7B shape, per M, per channel and g128.  Cold: each timed pass walks C distinct weight copies
+(>= 1 GB of fp16, so the 256 MB MALL holds none of them), as a model forward touches each layer's
+weight once; per-call time = pass time / C, median of rounds, arms interleaved in rotating order.
+One JSON line per (group, shape, M)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096, 11008)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="1,8,16,24,32,48,64,96,128,192,255")
+    ap.add_argument("--groups", default="-2,128")
+    ap.add_argument("--shapes", default="q_proj,gate_proj,down_proj")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--gb", type=float, default=1.2)
+    a = ap.parse_args()
+    from iron_weight_only_quant_amd import kernels
+    for group in [int(g) for g in a.groups.split(",")]:
+        for name in a.shapes.split(","):
+            N, K = SHAPES[name]
+            copies = max(4, int(a.gb * 1e9 / (N * K * 2)) + 1)
+            ws, cs, ts, ss, zs = [], [], [], [], []
+            for c in range(copies):
+                w = torch.empty(N, K, dtype=torch.float16, device="cuda")
+                kernels.fill_synthetic(w, 100 + c)
+                r = kernels.quantize_minmax(w, 4, group, False, 0, out=w, want_codes=True)
+                ws.append(w)
+                cs.append(r.codes)
+                ts.append(kernels.tile_codes(r.codes, N, K))
+                ss.append(r.scales)
+                zs.append(r.zeros)
+            for M in [int(m) for m in a.ms.split(",")]:
+                x = (torch.randn(M, K, device="cuda") * 0.5).half()
+                y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+
+                def ref():
+                    for c in range(copies):
+                        torch.nn.functional.linear(x, ws[c])
+
+                def fused():
+                    tiled = M <= kernels.GEMV_MAX_M
+                    for c in range(copies):
+                        kernels.w4a16_gemm(x, ts[c] if tiled else cs[c], ss[c], zs[c], 4, group, N, None,
+                                           tiled=tiled, out=y)
+                arms = {"hipblaslt": ref, "fused": fused}
+                for f in arms.values():
+                    f()
+                torch.cuda.synchronize()
+                times = {k: [] for k in arms}
+                keys = list(arms)
+                for rd in range(a.rounds):
+                    for k in keys[rd % 2:] + keys[:rd % 2]:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        arms[k]()
+                        e1.record()
+                        torch.cuda.synchronize()
+                        times[k].append(e0.elapsed_time(e1) * 1e3 / copies)
+                med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+                print(json.dumps({"group": group, "shape": name, "M": M, "copies": copies,
+                                  "hipblaslt_us": round(med["hipblaslt"], 2), "fused_us": round(med["fused"], 2),
+                                  "fused_speedup": round(med["hipblaslt"] / med["fused"], 3)}), flush=True)
+            del ws, cs, ts, ss, zs
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
