@@ -379,12 +379,14 @@ def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     Measured COLD (each layer's weight read once per forward, as in a model; profiles/
     r03_ab_auto_cold.jsonl, Llama-2-7B q / gate / down, 4-bit): per channel the fused kernels win at
     every M <= 192 (1.05-2.6x), g128 at every M <= 64 (1.09-2.25x) and up to 192 on N <= K weights
-    (q / down: 1.11-1.75x; gate_proj 0.93-0.97x there); at M = 255 and above hipBLASLt wins."""
+    (q / down: 1.11-1.75x; gate_proj 0.93-0.97x there); from M = 224 hipBLASLt wins on q / gate
+    (0.76-0.96x) while per-channel down_proj (K >= 2N) stays ahead up to M = 1024 (1.15-1.54x;
+    1.03x at 2048)."""
     if M <= 64:
         return True
     if M <= 192:
         return group == -2 or N <= K
-    return False
+    return M <= 1024 and group == -2 and K >= 2 * N
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:

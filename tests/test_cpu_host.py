@@ -303,3 +303,4 @@ def test_auto_fused_policy():
     assert P(128, 11008, 4096, -2) and not P(128, 11008, 4096, 128)
     assert P(192, 4096, 11008, 128) and P(192, 4096, 4096, 128)
     assert not P(193, 4096, 4096, -2) and not P(8192, 4096, 4096, -2)
+    assert P(1024, 4096, 11008, -2) and not P(1024, 4096, 11008, 128) and not P(2048, 4096, 11008, -2)
