@@ -55,6 +55,7 @@ struct FpArgs {
   int32_t lut_n8;       // table entries, rounded up to a multiple of 8
   const iwq_batch_entry* entries;  // batched form (whole model): tensor table, else null
   int32_t n_entries;
+  int32_t variant;                 // A/B variant (flags bits 16..23) where a launcher has them
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -155,6 +156,27 @@ __device__ __forceinline__ uint32_t apxd_tgt4(uint32_t x, uint32_t a, uint32_t b
   const uint32_t maxw = 0x01010101u * ((uint32_t)w8((1 << f.E) - 1) & 0xFFu);
   const uint32_t t = (gmax & mg) | (hfw & ~mg);
   return (maxw & mh) | (t & ~mh);
+}
+
+// apxd_tgt4 with fewer VALU (k_apx_double_lut V2): ">= 2 outliers" as a bit-parallel majority over
+// the four bit-6 flags ((x & a) | (b & c) | ((x | a) & (b | c)): three bitop3 + one or), "an outlier at
+// the max exponent" as one or3, and both selects as byte permutes whose selector bytes are i or i + 4
+// from the flag bit (26 instead of ~39 VALU per 4 elements); same result byte for byte.
+__device__ __forceinline__ uint32_t apxd_tgt4_v2(uint32_t x, uint32_t a, uint32_t b, uint32_t c, const FpSpec& f) {
+  const uint32_t s2 = b | c;
+  const uint32_t ge2 = (x & a) | (b & c) | ((x | a) & s2);  // bit 6 of each byte: >= 2 outliers
+  const uint32_t any = x | a | s2;                          // bit 7 of each byte: an outlier at the max
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  auto mx16 = [](uint32_t p, uint32_t q) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, p), __builtin_bit_cast(us2, q)));
+  };
+  const uint32_t ev = mx16(mx16(x & 0x000F000Fu, a & 0x000F000Fu), mx16(b & 0x000F000Fu, c & 0x000F000Fu));
+  const uint32_t od = mx16(mx16(x & 0x0F000F00u, a & 0x0F000F00u), mx16(b & 0x0F000F00u, c & 0x0F000F00u));
+  const uint32_t gmax = ev | od;
+  const uint32_t hfw = 0x01010101u * ((uint32_t)w8(f.hf) & 0xFFu);
+  const uint32_t maxw = 0x01010101u * ((uint32_t)w8((1 << f.E) - 1) & 0xFFu);
+  const uint32_t t = __builtin_amdgcn_perm(gmax, hfw, ((ge2 >> 4) & 0x04040404u) | 0x03020100u);
+  return __builtin_amdgcn_perm(maxw, t, ((any >> 5) & 0x04040404u) | 0x03020100u);
 }
 
 // decoded value (before the code's sign) of magnitude code c at target exponent tgt (table 2)
@@ -541,7 +563,10 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
 // codec on non-finite groups), one info byte per element exchanged with the 3 partners (6 lane
 // exchanges per unit: DPP / permlane swaps, lane_xor), then the quad decode and RN16(v * s) -- the reference's two passes
 // through a code buffer (and k_apx_double's scattered quad reads) in one streaming pass.
-template <int G, bool GS>
+// V: 2 = the default (info words handled in pairs + apxd_tgt4_v2: fewer VALU, same bits); A/B via
+// flags variant: 3 -> V 0, the round-2 form; 1 -> DIAGNOSTIC, V 2's predecessor + 48 extra dependent
+// VALU per unit (+11.6 % time for +17.6 % VALU: the kernel is mostly VALU-bound)
+template <int G, bool GS, int V = 0>
 __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
   static_assert(G == 32 || G == 64 || G == 128, "quad = 4 groups inside one 64-lane unit");
@@ -604,6 +629,7 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
         // otherwise); the quad exchange runs OUTSIDE the branch: partners may take the other path
         uint32_t info[8], sgn[4];  // sgn: finite groups: code-sign bits per pair; else bit 2i+1 = sign,
                                    // bit 2i = zero code of element i
+        uint32_t ip[4];            // V2: the info words of elements 2j, 2j + 1 as one dword (lo, hi)
         if (p.fast) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -614,9 +640,14 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             sgn[j] = tb & (mag + 0x7FFF7FFFu) & 0x80008000u;  // fp_encode: |t| == 0 -> code 0
             // zero code (magnitude 0, no sign: the reference masks it to 0) -> magnitude byte | 0x80,
             // a table-2 column of zeros (entry (tgt, 0) is not 0 for every tgt: int8 shift wrap)
-            const uint32_t i0 = lut[mag & 0xFFFFu], i1 = lut[mag >> 16];
-            info[2 * j] = i0 | ((i0 >> 5) & ~(sgn[j] >> 8) & 0x80u);
-            info[2 * j + 1] = i1 | ((i1 >> 5) & ~(sgn[j] >> 24) & 0x80u);
+            if constexpr (V == 2) {  // both elements at once: bit 12 of each half -> bit 7 unless signed
+              const uint32_t pr = (uint32_t)lut[mag & 0xFFFFu] | ((uint32_t)lut[mag >> 16] << 16);
+              ip[j] = pr | ((pr >> 5) & ~(sgn[j] >> 8) & 0x00800080u);
+            } else {
+              const uint32_t i0 = lut[mag & 0xFFFFu], i1 = lut[mag >> 16];
+              info[2 * j] = i0 | ((i0 >> 5) & ~(sgn[j] >> 8) & 0x80u);
+              info[2 * j + 1] = i1 | ((i1 >> 5) & ~(sgn[j] >> 24) & 0x80u);
+            }
           }
         } else {
           sgn[0] = 0;
@@ -629,16 +660,31 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             info[i] = apxd_info(code, f);
             sgn[0] |= (((code >> (f.E + f.M)) & 1u) << (2 * i + 1)) | ((code == 0u ? 1u : 0u) << (2 * i));
           }
+          if constexpr (V == 2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ip[j] = info[2 * j] | (info[2 * j + 1] << 16);
+          }
         }
         // info byte 1 (ae | zero << 4 | outlier << 6 | outlier-at-max << 7) of 4 elements per word
-        const uint32_t x0 = __builtin_amdgcn_perm(info[1], info[0], 0x0C0C0501u) |
-                            __builtin_amdgcn_perm(info[3], info[2], 0x05010C0Cu);
-        const uint32_t x1 = __builtin_amdgcn_perm(info[5], info[4], 0x0C0C0501u) |
-                            __builtin_amdgcn_perm(info[7], info[6], 0x05010C0Cu);
+        uint32_t x0, x1;
+        if constexpr (V == 2) {
+          x0 = __builtin_amdgcn_perm(ip[1], ip[0], 0x07050301u);
+          x1 = __builtin_amdgcn_perm(ip[3], ip[2], 0x07050301u);
+        } else {
+          x0 = __builtin_amdgcn_perm(info[1], info[0], 0x0C0C0501u) | __builtin_amdgcn_perm(info[3], info[2], 0x05010C0Cu);
+          x1 = __builtin_amdgcn_perm(info[5], info[4], 0x0C0C0501u) | __builtin_amdgcn_perm(info[7], info[6], 0x05010C0Cu);
+        }
         const uint32_t a0 = lane_xor<LPG>(x0), a1 = lane_xor<LPG>(x1);
         const uint32_t b0 = lane_xor<2 * LPG>(x0), b1 = lane_xor<2 * LPG>(x1);
         const uint32_t c0 = lane_xor<2 * LPG>(a0), c1 = lane_xor<2 * LPG>(a1);
-        const uint32_t tw0 = apxd_tgt4(x0, a0, b0, c0, f), tw1 = apxd_tgt4(x1, a1, b1, c1, f);
+        uint32_t tw0, tw1;
+        if constexpr (V == 2) {
+          tw0 = apxd_tgt4_v2(x0, a0, b0, c0, f);
+          tw1 = apxd_tgt4_v2(x1, a1, b1, c1, f);
+        } else {
+          tw0 = apxd_tgt4(x0, a0, b0, c0, f);
+          tw1 = apxd_tgt4(x1, a1, b1, c1, f);
+        }
         Vec8<DT_F16> o;
         bool nan8 = false;
         if (p.fast) {
@@ -647,8 +693,14 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
           for (int j = 0; j < 4; ++j) {
             const uint32_t tw = j < 2 ? tw0 : tw1;
             // table-2 index (tgt << 8) | c: byte 0 = c (| 0x80: zero code), byte 1 = this element's tgt
-            const uint32_t i0 = __builtin_amdgcn_perm(tw, info[2 * j], 0x0C0C0400u + ((uint32_t)(2 * (j & 1)) << 8));
-            const uint32_t i1 = __builtin_amdgcn_perm(tw, info[2 * j + 1], 0x0C0C0400u + ((uint32_t)(2 * (j & 1) + 1) << 8));
+            uint32_t i0, i1;
+            if constexpr (V == 2) {  // c bytes 0 / 2 of the pair word
+              i0 = __builtin_amdgcn_perm(tw, ip[j], 0x0C0C0400u + ((uint32_t)(2 * (j & 1)) << 8));
+              i1 = __builtin_amdgcn_perm(tw, ip[j], 0x0C0C0402u + ((uint32_t)(2 * (j & 1) + 1) << 8));
+            } else {
+              i0 = __builtin_amdgcn_perm(tw, info[2 * j], 0x0C0C0400u + ((uint32_t)(2 * (j & 1)) << 8));
+              i1 = __builtin_amdgcn_perm(tw, info[2 * j + 1], 0x0C0C0400u + ((uint32_t)(2 * (j & 1) + 1) << 8));
+            }
             const uint32_t vv = ((uint32_t)__builtin_bit_cast(uint16_t, t2[i0]) |
                                  ((uint32_t)__builtin_bit_cast(uint16_t, t2[i1]) << 16)) ^ sgn[j];
             o.u[j] = as_u32(as_h2(vv) * s2);  // RN16(decoded * scales): exact product, one rounding
@@ -664,6 +716,12 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             nan8 |= (y != y);
             o.set(i, F::from_f(y));
           }
+        }
+        if constexpr (V == 1) {
+          uint32_t d = o.u[0];
+#pragma unroll
+          for (int r = 0; r < 48; ++r) asm volatile("v_add_u32 %0, 1, %0" : "+v"(d));
+          if (d == 0x12345678u) o.u[1] ^= 1u;  // keeps the chain live; never true on real data
         }
         if (e0 < a.numel) {
           any_nan |= nan8;
@@ -823,10 +881,10 @@ hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int G>
-hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
-  auto kern = k_apx_double_lut<G, false>;
-  auto kern_gs = k_apx_double_lut<G, true>;
+template <int G, int V>
+hipError_t launch_apx_double_lut_v(const FpArgs& a, hipStream_t st) {
+  auto kern = k_apx_double_lut<G, false, V>;
+  auto kern_gs = k_apx_double_lut<G, true, V>;
   const size_t lds = (size_t)(a.lut_n8 + APXD_T2) * 2;
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
@@ -839,6 +897,14 @@ hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
   if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
   else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
   return hipGetLastError();
+}
+
+template <int G>
+hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
+  // default: V2 (2.6 % faster than the round-2 form, bit-identical; profiles/r03_ab_apxd.jsonl)
+  if (a.variant == 1) return launch_apx_double_lut_v<G, 1>(a, st);
+  if (a.variant == 3) return launch_apx_double_lut_v<G, 0>(a, st);
+  return launch_apx_double_lut_v<G, 2>(a, st);
 }
 
 hipError_t launch_apx_double_lut(int64_t g, const FpArgs& a, hipStream_t st) {
@@ -1111,6 +1177,7 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
     a.nan_flag = nan_flag;
     a.lut = static_cast<const uint16_t*>(lut);
     a.lut_n8 = (int32_t)((lut_bound_bits(CODEC_APXD, f) + 1 + 7) / 8 * 8);
+    a.variant = (int32_t)((flags >> 16) & 0xFFu);
     IWQ_HIP_FP(launch_apx_double_lut(group, a, static_cast<hipStream_t>(stream)));
     return IWQ_OK;
   }

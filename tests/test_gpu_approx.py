@@ -117,7 +117,7 @@ def _cases(AD):
     return out
 
 
-@pytest.mark.parametrize("flags", FLAG_SETS)
+@pytest.mark.parametrize("flags", FLAG_SETS + (3 << 16,))  # + the round-2 double-approximate kernel (A/B)
 def test_approx_golden_kernel(K, AD, flags):
     x = dev16(AD["in/apx_a"])
     n = 0
