@@ -135,6 +135,13 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
   }
 }
 
+// lane_xor through the LDS pipe (no VALU issue): ds_swizzle (xor inside 32 lanes) / ds_bpermute (32)
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor_lds(uint32_t v) {
+  if constexpr (M == 32) return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((threadIdx.x & 63) ^ 32) << 2), (int)v);
+  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);
+}
+
 // apxd_tgt on 4 elements at once: bytes of x / a / b / c are the info bytes of the quad members
 // (own, partner 1, 2, 3) of 4 elements; returns their 4 target exponents, one per byte.
 __device__ __forceinline__ uint32_t apxd_tgt4(uint32_t x, uint32_t a, uint32_t b, uint32_t c, const FpSpec& f) {
@@ -563,9 +570,10 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
 // codec on non-finite groups), one info byte per element exchanged with the 3 partners (6 lane
 // exchanges per unit: DPP / permlane swaps, lane_xor), then the quad decode and RN16(v * s) -- the reference's two passes
 // through a code buffer (and k_apx_double's scattered quad reads) in one streaming pass.
-// V: 2 = the default (info words handled in pairs + apxd_tgt4_v2: fewer VALU, same bits); A/B via
-// flags variant: 3 -> V 0, the round-2 form; 1 -> DIAGNOSTIC, V 2's predecessor + 48 extra dependent
-// VALU per unit (+11.6 % time for +17.6 % VALU: the kernel is mostly VALU-bound)
+// V: 4 = the default: info words handled in pairs, apxd_tgt4_v2, and the quad exchange through the
+// LDS pipe (ds_swizzle / ds_bpermute: no VALU issue; the kernel is VALU-bound, the LDS pipe is not);
+// A/B via flags variant: 2 -> V 2 (V 4 with the DPP / permlane exchange), 3 -> V 0 (the round-2 form),
+// 1 -> DIAGNOSTIC, V 0 + 48 extra dependent VALU per unit (+11.6 % time for +17.6 % VALU)
 template <int G, bool GS, int V = 0>
 __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
@@ -640,7 +648,7 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             sgn[j] = tb & (mag + 0x7FFF7FFFu) & 0x80008000u;  // fp_encode: |t| == 0 -> code 0
             // zero code (magnitude 0, no sign: the reference masks it to 0) -> magnitude byte | 0x80,
             // a table-2 column of zeros (entry (tgt, 0) is not 0 for every tgt: int8 shift wrap)
-            if constexpr (V == 2) {  // both elements at once: bit 12 of each half -> bit 7 unless signed
+            if constexpr (V == 2 || V == 4) {  // both elements at once: bit 12 of each half -> bit 7 unless signed
               const uint32_t pr = (uint32_t)lut[mag & 0xFFFFu] | ((uint32_t)lut[mag >> 16] << 16);
               ip[j] = pr | ((pr >> 5) & ~(sgn[j] >> 8) & 0x00800080u);
             } else {
@@ -660,25 +668,32 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             info[i] = apxd_info(code, f);
             sgn[0] |= (((code >> (f.E + f.M)) & 1u) << (2 * i + 1)) | ((code == 0u ? 1u : 0u) << (2 * i));
           }
-          if constexpr (V == 2) {
+          if constexpr (V == 2 || V == 4) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) ip[j] = info[2 * j] | (info[2 * j + 1] << 16);
           }
         }
         // info byte 1 (ae | zero << 4 | outlier << 6 | outlier-at-max << 7) of 4 elements per word
         uint32_t x0, x1;
-        if constexpr (V == 2) {
+        if constexpr (V == 2 || V == 4) {
           x0 = __builtin_amdgcn_perm(ip[1], ip[0], 0x07050301u);
           x1 = __builtin_amdgcn_perm(ip[3], ip[2], 0x07050301u);
         } else {
           x0 = __builtin_amdgcn_perm(info[1], info[0], 0x0C0C0501u) | __builtin_amdgcn_perm(info[3], info[2], 0x05010C0Cu);
           x1 = __builtin_amdgcn_perm(info[5], info[4], 0x0C0C0501u) | __builtin_amdgcn_perm(info[7], info[6], 0x05010C0Cu);
         }
-        const uint32_t a0 = lane_xor<LPG>(x0), a1 = lane_xor<LPG>(x1);
-        const uint32_t b0 = lane_xor<2 * LPG>(x0), b1 = lane_xor<2 * LPG>(x1);
-        const uint32_t c0 = lane_xor<2 * LPG>(a0), c1 = lane_xor<2 * LPG>(a1);
+        uint32_t a0, a1, b0, b1, c0, c1;
+        if constexpr (V == 4) {
+          a0 = lane_xor_lds<LPG>(x0), a1 = lane_xor_lds<LPG>(x1);
+          b0 = lane_xor_lds<2 * LPG>(x0), b1 = lane_xor_lds<2 * LPG>(x1);
+          c0 = lane_xor_lds<2 * LPG>(a0), c1 = lane_xor_lds<2 * LPG>(a1);
+        } else {
+          a0 = lane_xor<LPG>(x0), a1 = lane_xor<LPG>(x1);
+          b0 = lane_xor<2 * LPG>(x0), b1 = lane_xor<2 * LPG>(x1);
+          c0 = lane_xor<2 * LPG>(a0), c1 = lane_xor<2 * LPG>(a1);
+        }
         uint32_t tw0, tw1;
-        if constexpr (V == 2) {
+        if constexpr (V == 2 || V == 4) {
           tw0 = apxd_tgt4_v2(x0, a0, b0, c0, f);
           tw1 = apxd_tgt4_v2(x1, a1, b1, c1, f);
         } else {
@@ -694,7 +709,7 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_apx_double_lut(FpArgs a) {
             const uint32_t tw = j < 2 ? tw0 : tw1;
             // table-2 index (tgt << 8) | c: byte 0 = c (| 0x80: zero code), byte 1 = this element's tgt
             uint32_t i0, i1;
-            if constexpr (V == 2) {  // c bytes 0 / 2 of the pair word
+            if constexpr (V == 2 || V == 4) {  // c bytes 0 / 2 of the pair word
               i0 = __builtin_amdgcn_perm(tw, ip[j], 0x0C0C0400u + ((uint32_t)(2 * (j & 1)) << 8));
               i1 = __builtin_amdgcn_perm(tw, ip[j], 0x0C0C0402u + ((uint32_t)(2 * (j & 1) + 1) << 8));
             } else {
@@ -901,10 +916,11 @@ hipError_t launch_apx_double_lut_v(const FpArgs& a, hipStream_t st) {
 
 template <int G>
 hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
-  // default: V2 (2.6 % faster than the round-2 form, bit-identical; profiles/r03_ab_apxd.jsonl)
+  // default: V4 (11 % faster than the round-2 form, bit-identical; profiles/r03_ab_apxd.jsonl)
   if (a.variant == 1) return launch_apx_double_lut_v<G, 1>(a, st);
+  if (a.variant == 2) return launch_apx_double_lut_v<G, 2>(a, st);
   if (a.variant == 3) return launch_apx_double_lut_v<G, 0>(a, st);
-  return launch_apx_double_lut_v<G, 2>(a, st);
+  return launch_apx_double_lut_v<G, 4>(a, st);
 }
 
 hipError_t launch_apx_double_lut(int64_t g, const FpArgs& a, hipStream_t st) {

@@ -117,7 +117,8 @@ def _cases(AD):
     return out
 
 
-@pytest.mark.parametrize("flags", FLAG_SETS + (3 << 16,))  # + the round-2 double-approximate kernel (A/B)
+# + the double-approximate kernel's A/B forms: 2 (DPP / permlane exchange), 3 (the round-2 kernel)
+@pytest.mark.parametrize("flags", FLAG_SETS + (2 << 16, 3 << 16))
 def test_approx_golden_kernel(K, AD, flags):
     x = dev16(AD["in/apx_a"])
     n = 0

@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, ".")
 from iron_weight_only_quant_amd import kernels as K  # noqa: E402
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,3,1").split(",")]
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,2,3,1").split(",")]
 diag = {1}
 rows, cols, copies, g = 11008, 4096, 16, 128
 ws = []
