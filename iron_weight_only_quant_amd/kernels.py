@@ -376,17 +376,15 @@ NIB_MIN_M = 256
 def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     """QuantLinear(fused_forward="auto"): whether the packed-code kernels beat the reference forward
     F.linear(x, W_deq) (hipBLASLt on the resident fp16 weight) for an M-row batch on an [N, K] weight.
-    Measured COLD (each layer's weight read once per forward, as in a model; profiles/
-    r03_ab_auto_cold.jsonl, Llama-2-7B q / gate / down, 4-bit): per channel the fused kernels win at
-    every M <= 192 (1.05-2.6x), g128 at every M <= 64 (1.09-2.25x) and up to 192 on N <= K weights
-    (q / down: 1.11-1.75x; gate_proj 0.93-0.97x there); from M = 224 hipBLASLt wins on q / gate
-    (0.76-0.96x) while per-channel down_proj (K >= 2N) stays ahead up to M = 1024 (1.15-1.54x;
-    1.03x at 2048)."""
-    if M <= 64:
-        return True
-    if M <= 192:
-        return group == -2 or N <= K
-    return M <= 1024 and group == -2 and K >= 2 * N
+    Measured in DEVICE time, cold (each pass walks >= 1.2 GB of distinct weights, as a model forward
+    reads each layer once; hipGraph replay, so no host launch cost; profiles/r03_ab_auto_graph.jsonl,
+    Llama-2-7B q / gate / down, 4-bit): per channel the fused kernels win at every M <= 192
+    (1.01-3.6x) and on down-like weights (K >= 2N) up to M = 1024 (1.14-1.31x); g128 wins at every
+    M <= 32 (1.06-3.2x) and on down-like weights up to M = 512 (1.08-1.72x), but not on q_proj at
+    M = 64 (0.86x) or gate_proj at 128-192 (0.92-0.94x)."""
+    if group == -2:
+        return M <= 192 or (M <= 1024 and K >= 2 * N)
+    return M <= 32 or (M <= 512 and K >= 2 * N)
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:

@@ -241,10 +241,10 @@ class QuantLinear(nn.Module):
         With fused_forward=True (INT, 2-4 bits, quant_dim 0) the GEMM reads the packed codes instead
         (kernels.w4a16_gemm, MFMA): same weights, fp32 accumulation in a different order.
         fused_forward="auto" takes the packed-weight kernels only where they are the faster ones
-        (kernels.auto_fused_preferred, measured cold): decode batches (M <= 16 rows: the
-        weight-streaming GEMV on the tile-layout codes, 1.4-2.2x hipBLASLt) and prompt-sized
-        batches up to 64 rows (192 per channel, or on N <= K weights); larger M run F.linear on the
-        resident dequantized weight, like the reference."""
+        (kernels.auto_fused_preferred, device time, cold): decode batches (M <= 16 rows: the
+        weight-streaming GEMV on the tile-layout codes, 1.5-3.6x hipBLASLt) and prompt-sized
+        batches up to 192 rows per channel / 32 grouped (more on down-like K >= 2N weights); other
+        batches run F.linear on the resident dequantized weight, like the reference."""
         if not self.quantized:
             return F.linear(input, self.weight, self.bias)
         fused = self.fused_forward

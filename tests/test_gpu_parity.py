@@ -740,15 +740,16 @@ def test_dequant_packed_bit_exact(K, bits, group, sym):
 
 def test_quantlinear_fused_forward_auto(K, monkeypatch):
     """fused_forward="auto": the packed-weight kernels where kernels.auto_fused_preferred says they
-    are faster (tile-layout GEMV up to 16 rows, row-major codes up to 64 / 192 rows), F.linear above."""
+    are faster (tile-layout GEMV up to 16 rows, row-major codes above), F.linear where they are not."""
     from iron_weight_only_quant_amd import quant_linear as QLm
     calls = []
     real = QLm.kernels.w4a16_gemm
     monkeypatch.setattr(QLm.kernels, "w4a16_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
-    lin = torch.nn.Linear(512, 256, bias=True).half().to(DEV)
+    lin = torch.nn.Linear(512, 512, bias=True).half().to(DEV)
     q = QLm.QuantLinear.from_linear(lin, w_bit=4, w_group_size=128, symmetric=False, fused_forward="auto")
     assert q.qweight_tiled is not None and q.qweight_tiled.numel() == q.qweight.numel()
-    for shape, fused in (((1, 512), True), ((2, 8, 512), True), ((2, 24, 512), True), ((3, 64, 512), True),
+    # g128, N = K = 512 (not down-like): fused up to 32 rows (kernels.auto_fused_preferred)
+    for shape, fused in (((1, 512), True), ((2, 8, 512), True), ((2, 16, 512), True), ((3, 16, 512), False),
                          ((4, 64, 512), False)):
         calls.clear()
         x = torch.randn(*shape, device=DEV).half()

@@ -4,7 +4,8 @@ forward kernels.w4a16_gemm on the packed codes (tiled codes at M <= 16, as "auto
 Llama-2-7B shape, per M, per channel and g128.  Cold: each timed pass walks C distinct weight copies
 (>= 1 GB of fp16, so the 256 MB MALL holds none of them), as a model forward touches each layer's
 weight once; per-call time = pass time / C, median of rounds, arms interleaved in rotating order.
-One JSON line per (group, shape, M)."""
+Each pass is captured in a hipGraph and replayed, so the time is DEVICE time (--eager: eager calls,
+which at small M measure the host launch cost instead).  One JSON line per (group, shape, M)."""
 import argparse
 import json
 import os
@@ -15,7 +16,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096, 11008)}
+SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096, 11008),
+          "qkv_proj": (12288, 4096), "gate_up_proj": (22016, 4096)}  # the last two: fused-projection probes
 
 
 def main():
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--shapes", default="q_proj,gate_proj,down_proj")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--gb", type=float, default=1.2)
+    ap.add_argument("--eager", action="store_true", help="time eager calls (host launch cost included)")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels
     for group in [int(g) for g in a.groups.split(",")]:
@@ -58,6 +61,22 @@ def main():
                 for f in arms.values():
                     f()
                 torch.cuda.synchronize()
+                if not a.eager:  # device time: each pass captured once, replayed (no host launch cost)
+                    graphs = {}
+                    for k, f in arms.items():
+                        s = torch.cuda.Stream()
+                        s.wait_stream(torch.cuda.current_stream())
+                        with torch.cuda.stream(s):
+                            f()
+                        torch.cuda.current_stream().wait_stream(s)
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g):
+                            f()
+                        graphs[k] = g
+                    arms = {k: g.replay for k, g in graphs.items()}
+                    for f in arms.values():
+                        f()
+                    torch.cuda.synchronize()
                 times = {k: [] for k in arms}
                 keys = list(arms)
                 for rd in range(a.rounds):
@@ -69,7 +88,7 @@ def main():
                         torch.cuda.synchronize()
                         times[k].append(e0.elapsed_time(e1) * 1e3 / copies)
                 med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
-                print(json.dumps({"group": group, "shape": name, "M": M, "copies": copies,
+                print(json.dumps({"mode": "eager" if a.eager else "graph", "group": group, "shape": name, "M": M, "copies": copies,
                                   "hipblaslt_us": round(med["hipblaslt"], 2), "fused_us": round(med["fused"], 2),
                                   "fused_speedup": round(med["hipblaslt"] / med["fused"], 3)}), flush=True)
             del ws, cs, ts, ss, zs
