@@ -1,0 +1,77 @@
+"""Fused decode projections (fused_proj.py) on a Llama-shaped model: one packed GEMV per (q, k, v) and
+(gate, up) group at decode batch sizes, the members' own forward above; logits against the unfused
+model, launch counts, state_dict keys unchanged, unfuse restores."""
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _model(group=128):
+    from transformers import LlamaConfig, LlamaForCausalLM
+
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+    cfg = LlamaConfig(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+                      num_key_value_heads=2, vocab_size=512, max_position_embeddings=128)
+    torch.manual_seed(0)
+    m = LlamaForCausalLM(cfg).half().to(DEV).eval()
+    quantize_model(m, SimpleNamespace(w_bit=4, a_bit=16, w_group_size=group, w_symmetric=False, w_format="int",
+                                      quant_dim=0, fused_forward="auto"), verbose=False)
+    return cfg, m
+
+
+@pytest.mark.parametrize("group", [128, -2])
+def test_fused_projections_match_unfused(group, monkeypatch):
+    from iron_weight_only_quant_amd import kernels
+    from iron_weight_only_quant_amd.fused_proj import FusedProjection, fuse_projections, unfuse_projections
+    cfg, m = _model(group)
+    keys = list(m.state_dict())
+    g = torch.Generator(DEV).manual_seed(3)
+    decode = [torch.randint(0, cfg.vocab_size, (b, 1), device=DEV, generator=g) for b in (1, 4, 16)]
+    prefill = torch.randint(0, cfg.vocab_size, (2, 24), device=DEV, generator=g)
+    with torch.no_grad():
+        ref = [m(ids).logits for ids in decode + [prefill]]
+    assert fuse_projections(m) == 4  # (q, k, v) and (gate, up) in each of 2 layers
+    assert sum(isinstance(x, FusedProjection) for x in m.modules()) == 4
+    assert list(m.state_dict()) == keys  # derived buffers are not persistent
+    calls = []
+    real = kernels.w4a16_gemm
+    monkeypatch.setattr(kernels, "w4a16_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
+    with torch.no_grad():
+        for ids, r in zip(decode, ref):
+            calls.clear()
+            got = m(ids).logits
+            assert len(calls) == 2 * 4  # per layer: qkv, o, gate_up, down (was 7)
+            torch.testing.assert_close(got.float(), r.float(), rtol=2e-2, atol=2e-2)
+        got = m(prefill).logits  # M = 48 rows: every member runs its own forward, exactly as before
+        assert torch.equal(got, ref[-1])
+    unfuse_projections(m)
+    assert not any(isinstance(x, FusedProjection) for x in m.modules())
+    with torch.no_grad():
+        calls.clear()
+        assert torch.equal(m(decode[0]).logits, ref[0])
+        assert len(calls) == 7 * 2
+
+
+def test_fused_projection_cache_follows_the_input():
+    """A member called with a different tensor (or after an in-place change) recomputes."""
+    from iron_weight_only_quant_amd.fused_proj import fuse_projections
+    _, m = _model()
+    fuse_projections(m)
+    attn = m.model.layers[0].self_attn
+    x = torch.randn(1, 1, 256, device=DEV, dtype=torch.float16)
+    y = torch.randn(1, 1, 256, device=DEV, dtype=torch.float16)
+    with torch.no_grad():
+        q_x = attn.q_proj(x)
+        k_y = attn.k_proj(y)                      # not the cached input: k of y
+        k_ref = type(attn.k_proj).forward(attn.k_proj, y)
+        torch.testing.assert_close(k_y, k_ref, rtol=1e-2, atol=2e-3)
+        attn.q_proj(x)
+        x.mul_(2.0)                               # in place: the cached output is stale
+        v_x = attn.v_proj(x)
+        torch.testing.assert_close(v_x, type(attn.v_proj).forward(attn.v_proj, x), rtol=1e-2, atol=2e-3)
+        assert q_x.shape[-1] == 256 and v_x.shape[-1] == 128
