@@ -75,3 +75,24 @@ def test_fused_projection_cache_follows_the_input():
         v_x = attn.v_proj(x)
         torch.testing.assert_close(v_x, type(attn.v_proj).forward(attn.v_proj, x), rtol=1e-2, atol=2e-3)
         assert q_x.shape[-1] == 256 and v_x.shape[-1] == 128
+
+
+def test_fused_projections_on_packed_only_model(tmp_path):
+    """A packed-only model (checkpoint.load_packed(packed=True): PackedLinear, no fp16 weights) fuses
+    the same way; decode logits against the fp16-resident quantized model."""
+    from transformers import LlamaForCausalLM
+
+    from iron_weight_only_quant_amd.checkpoint import PackedLinear, load_packed, save_packed
+    from iron_weight_only_quant_amd.fused_proj import fuse_projections
+    cfg, m = _model()
+    p = tmp_path / "m.safetensors"
+    save_packed(m, p)
+    with torch.device(DEV):
+        pk = LlamaForCausalLM(cfg).half()
+    load_packed(pk, p, device=DEV, packed=True)
+    pk.eval()
+    assert isinstance(pk.model.layers[0].self_attn.q_proj, PackedLinear)
+    assert fuse_projections(pk) == 4
+    ids = torch.randint(0, cfg.vocab_size, (3, 1), device=DEV, generator=torch.Generator(DEV).manual_seed(5))
+    with torch.no_grad():
+        torch.testing.assert_close(pk(ids).logits.float(), m(ids).logits.float(), rtol=2e-2, atol=2e-2)
