@@ -123,7 +123,7 @@ __device__ __forceinline__ int apxd_tgt(uint32_t b0, uint32_t b1, uint32_t b2, u
 template <int M>
 __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
   if constexpr (M == 8) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, true);  // row_ror:8 (no v_mov 0)
   } else if constexpr (M == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
     return (threadIdx.x & 16) ? r[0] : r[1];
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(BLOCK) void k_fp_group(FpArgs a) {
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int32_t, x), CTRL, 0xF, 0xF,
-                                                               false));
+                                                               true));
 }
 // the parameters of unit k of this lane's group, held by lane k of the quad (see iter_shared_f16
 // in iwq_minmax.hip; scalars only -- never an f2 across DPP)

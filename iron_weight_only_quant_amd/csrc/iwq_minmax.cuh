@@ -142,9 +142,12 @@ __device__ __forceinline__ bool group_unit_compute(const UnitRef& r, const Vec8<
   return r.valid && any_nan;
 }
 
+// quad_perm broadcasts read inside the quad, so no source lane is out of range and bound_ctrl changes
+// nothing -- but with it set the compiler drops the v_mov 0 it otherwise emits for the `old` operand
+// (one VALU per broadcast, 4-5 per unit)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int32_t)x, CTRL, 0xF, 0xF, true);
 }
 template <int K, int CODES>
 __device__ __forceinline__ BiasedWords bcast_words_k(const BiasedWords& w) {
