@@ -378,8 +378,8 @@ def kernel_sources_sha():
     trusted while it carries the same hash."""
     import hashlib
     h = hashlib.sha256()
-    for rel in ("iron_weight_only_quant_amd/csrc/iwq_minmax.hip", "iron_weight_only_quant_amd/csrc/iwq_common.cuh",
-                "include/iwq.h"):
+    for rel in ("iron_weight_only_quant_amd/csrc/iwq_minmax.hip", "iron_weight_only_quant_amd/csrc/iwq_minmax.cuh",
+                "iron_weight_only_quant_amd/csrc/iwq_common.cuh", "include/iwq.h"):
         with open(os.path.join(ROOT, rel), "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]

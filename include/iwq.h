@@ -93,8 +93,10 @@ int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant
  *   nan_flag   device uint32, OR-ed with 1 if any dequantized value is NaN; nullable.  Also OR-ed
  *              with 2 if the per-tensor one-pass kernel's in-launch hand-off between workgroups timed
  *              out (its workgroups were not all resident -- another kernel held CUs): the outputs are
- *              then invalid; the caller must fail (kernels.QuantResult.has_nan raises).  Without a
- *              nan_flag the per-tensor path takes the two-kernel form, which cannot time out.
+ *              then invalid.  Out of place the input is untouched and the caller re-runs the call with
+ *              IWQ_FLAG_VARIANT(6) (the two-kernel form, which cannot time out) into the same outputs
+ *              (kernels.QuantResult.has_nan does); in place it must fail.  Without a nan_flag the
+ *              per-tensor path takes the two-kernel form.
  *   symmetric  0 -> zero_point=True path (:16-22), 1 -> absmax path (:23-29)
  */
 int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int n_bits,

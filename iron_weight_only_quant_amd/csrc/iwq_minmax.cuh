@@ -878,7 +878,7 @@ template <int DT, bool SYM, int CODES, int NV>
 __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* out, uint8_t* codes, void* scales,
                                                            void* zeros, int64_t nvec, int nvt,
                                                            unsigned long long* granules, uint32_t tag, int n_bits,
-                                                           uint32_t* nan_flag) {
+                                                           uint32_t* nan_flag, uint32_t spin_limit) {
   using F = Fmt<DT>;
   static_assert(DT == DT_F16, "one-pass per-tensor: fp16 (keys packed in one dword, packed fast path)");
   typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
         x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                    : ((unsigned long long)tag << 32);
         if (__all((uint32_t)(x >> 32) == tag)) break;
-        if (++spins > OP_SPIN_LIMIT) {
+        if (++spins > spin_limit) {
           timed_out = true;
           break;
         }

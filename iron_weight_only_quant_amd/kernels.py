@@ -6,13 +6,17 @@ reference raises (quant_funcs.py:11/15/40, quant_linear.py:897/906).
 """
 import ctypes
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import torch
 
 from . import _lib as L
 
 FAST_GROUPS = (8, 16, 32, 64, 128, 256, 512)
+
+
+# iwq_minmax.hip per-tensor variant 6: the reduce + apply pair, which cannot time out
+_TENSOR_PAIR = 6 << 16
 
 
 @dataclass
@@ -22,10 +26,20 @@ class QuantResult:
     zeros: Optional[torch.Tensor]     # [G] storage dtype (asymmetric) or None
     codes: Optional[torch.Tensor]     # packed uint8 codes (include/iwq.h layout) or None
     nan_flag: torch.Tensor            # [1] int32 on device; bit 0: the output holds a NaN
+    retry: Optional[Callable[[], torch.Tensor]] = None  # re-run on the pair into the same outputs
+    retried: bool = False             # has_nan() found a timed-out hand-off and re-ran the call
 
     def has_nan(self) -> bool:
         v = int(self.nan_flag.item())
-        if v & 2:  # include/iwq.h: the per-tensor one-pass hand-off timed out, the outputs are invalid
+        if v & 2 and self.retry is not None:
+            # include/iwq.h: the per-tensor one-pass hand-off timed out (its workgroups were not all
+            # resident, e.g. another stream's kernel held CUs).  Out of place the input is untouched,
+            # so the same call on the two-kernel form rewrites every output; its flag replaces this one.
+            self.nan_flag = self.retry()
+            self.retry = None
+            self.retried = True
+            v = int(self.nan_flag.item())
+        if v & 2:  # in place: the input may already be partly overwritten
             raise RuntimeError("iwq: per-tensor one-pass kernel timed out waiting for its workgroups "
                                "(not all resident); outputs invalid")
         return v != 0
@@ -136,11 +150,24 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
     # the specialised kernels need no workspace; the C-ABI checks for one before launching anything,
     # so only the per-tensor and universal paths pay for the allocation (and a second call)
     st = call(None, 0)
+    retry = None
     if st == L.IWQ_ERR_WORKSPACE:
         wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
-        st = call(torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev), wsb)
+        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        st = call(ws, wsb)
+        if group == -1 and (out is None or out.data_ptr() != w.data_ptr()):
+            def retry():  # the one-pass hand-off timed out (QuantResult.has_nan): same call on the pair
+                flag2 = torch.zeros(1, dtype=torch.int32, device=dev)
+                with L.on_device(dev):
+                    st2 = lib.iwq_quantize_minmax(
+                        L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group),
+                        int(bool(symmetric)), int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols),
+                        L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(flag2),
+                        (int(flags) & ~(0xFF << 16)) | _TENSOR_PAIR, L.stream_handle(dev))
+                _raise_for(st2, "iwq_quantize_minmax")
+                return flag2
     _raise_for(st, "iwq_quantize_minmax")
-    return QuantResult(out, scales, zeros, codes, nan_flag)
+    return QuantResult(out, scales, zeros, codes, nan_flag, retry)
 
 
 class _LutCache:

@@ -785,6 +785,26 @@ def test_per_tensor_fast_path(K, dtype):
     assert r.has_nan()
 
 
+def test_per_tensor_onepass_timeout_retry(K):
+    """A one-pass hand-off that times out (test-only variant 9: the granule sweep gives up at once,
+    as it would with workgroups held off the CUs by another stream) sets nan_flag bit 1; out of place
+    has_nan() re-runs the call on the two-kernel form into the same outputs (bit-exact vs the oracle),
+    in place (input possibly overwritten) it raises."""
+    x = synth(56, (1536, 2048), "float16")
+    exp = O.quantlinear_int(x, 4, -1, False, 0, "float16")
+    r = K.quantize_minmax(to_dev(x, "float16"), 4, -1, False, 0, want_codes=True, flags=K.gemm_variant_flags(9))
+    assert not r.has_nan()
+    assert r.retried
+    assert bits_equal(to_np(r.out), exp.dequant)
+    assert bits_equal(to_np(r.scales), exp.scales.reshape(-1))
+    assert bits_equal(to_np(r.zeros), exp.zeros.reshape(-1))
+    assert np.array_equal(r.codes.cpu().numpy().reshape(-1), O.pack_codes(exp.codes, 4).reshape(-1))
+    xi = to_dev(x, "float16")
+    r = K.quantize_minmax(xi, 4, -1, False, 0, out=xi, flags=K.gemm_variant_flags(9))
+    with pytest.raises(RuntimeError, match="timed out"):
+        r.has_nan()
+
+
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
 def test_quant_dim1_register_kernel(K, dtype):
     """quant_dim 1 with groups of 32/64/128/256 rows (the register-resident column kernel; cols not a
