@@ -589,20 +589,24 @@ def all_ranks_sum(x, ws_n):
 
 
 def weak_secondary(args, ws_n, rank):
-    """7B at N > 1: every rank quantizes a full 7B (weak scaling), timed like the headline."""
+    """7B at N > 1: every rank quantizes a full 7B (weak scaling), timed like the headline.  With
+    shapes: the cold single-tensor calls per Llama shape on the same full copy, every rank running its
+    own calls at once (per_shape: max over ranks, aggregate = N x one GPU's calls) -- the north star's
+    per-shape GB/s at N GPUs.  Every rank holds every shape, so the per-shape collectives line up."""
     from iron_weight_only_quant_amd import kernels
-    weights, _, _ = make_weights(args.model, rank, ws_n, weak=True)
+    weights, names, _ = make_weights(args.model, rank, ws_n, weak=True)
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
     stream = torch.cuda.current_stream()
     clock_ramp(plan, 0.2)
     kernel_ms, ms = timed_steps(plan, args, ws_n, stream)
     total = all_ranks_sum(plan.numel, ws_n)
+    shapes = None if args.no_shapes else per_shape(plan, names, ws_n, args)
     del plan, weights
     torch.cuda.empty_cache()
     return {"scaling": "weak", "value": round(total * 2 / (ms / 1e3) / 1e9, 2), "ms_per_step": round(ms, 4),
             "kernel_ms_rank0": round(kernel_ms, 4), "fp16_weights_total": total,
             "workload": f"every rank quantizes all {len(make_shapes(args.model))} Linear weights of "
-                        f"{MODEL_NAME[args.model]}"}
+                        f"{MODEL_NAME[args.model]}"}, shapes
 
 
 def make_shapes(model):
@@ -669,7 +673,7 @@ def main():
         del plan
         weights = None
         torch.cuda.empty_cache()
-        weak_rec = weak_secondary(args, ws_n, rank)
+        weak_rec, shapes_rec = weak_secondary(args, ws_n, rank)
 
     cpu = None
     if rank == 0 and ws_n == 1 and not args.no_cpu_baseline:
@@ -703,6 +707,9 @@ def main():
                                                  if ceiling else None),
                          "other_placement": other},
             "shapes": shapes_rec,
+            "shapes_scaling": (None if shapes_rec is None else "single GPU" if ws_n == 1 else
+                               f"weak: each of {ws_n} ranks runs its own cold calls at once; weights_GBps = "
+                               "all ranks' input bytes / max-over-ranks time"),
             "weak": weak_rec,
             "cpu_baseline": cpu,
             "ppl_delta": None,
