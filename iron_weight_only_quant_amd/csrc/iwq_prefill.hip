@@ -805,7 +805,11 @@ __device__ __forceinline__ uint32_t lds_rd_d(uint32_t addr) {
 // applies s per weight (RN16((q - z) s), the reference's fp16 weight; no epilogue scale).
 // SPLIT: one K range of a split-K launch (k_w4a16_b32e's SPLIT: tile / range from blockIdx, the raw
 // accumulators to the workspace in b32e's 2 x 4 wave layout, so k_splitk_reduce is shared).
-template <bool NIB, bool GROUPED = false, bool SPLIT = false, int EPI = 0>
+// PG (grouped only): the parameters change once per group, not per K-step -- a K-step stages, reads
+// and converts them only when it starts a group (or is the range's first); the others keep the
+// registers (one DMA piece, two LDS reads and the set_params VALU fewer per wave on every K-step
+// that does not start a group: half of them at g = 128).  The vmcnt counts follow the pieces issued.
+template <bool NIB, bool GROUPED = false, bool SPLIT = false, int EPI = 0, bool PG = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
   constexpr int PER_STAGE = GROUPED ? 6 : 5;
@@ -846,19 +850,29 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
     psrc = arr + (int64_t)(n0 + (wid & 3) * 64 + lane) * a.gpr;
   }
+  // does K-step k of this range carry its group's parameters (wave-uniform)?
+  auto hp = [&](int k) -> bool {
+    if constexpr (!GROUPED) return false;
+    else if constexpr (!PG) return true;
+    else return k == 0 || ((kbase + k) * TK) % a.group == 0;
+  };
   auto issue = [&](int kt, int stg) {
     uint8_t* base = smem + stg * STAGE;
 #pragma unroll
     for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
+    if constexpr (GROUPED) {
+      if (hp(kt)) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
+    }
   };
   // one DMA piece (i < 4: X rows, 4: codes, 5: parameters) of K-step kt into stage stg
   auto issue1 = [&](int kt, int stg, int i) {
     uint8_t* base = smem + stg * STAGE;
     if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     else if (i == 4) glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    else if constexpr (GROUPED) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
+    else if constexpr (GROUPED) {
+      if (hp(kt)) glds2(psrc + ((kbase + kt) * TK) / a.group, base + XS + CS + wid * 256);
+    }
   };
 
   // this lane's column and its parameters (per channel: once; grouped: per K-step, set_params)
@@ -957,7 +971,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
   // prologue: stages 0, 1, 2 (K-steps clamped to nk - 1: re-loads of stages nobody reads again)
   issue(0, 0);
   issue(nk > 1 ? 1 : 0, 1);
-  if constexpr (GROUPED) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if (hp(nk > 1 ? 1 : 0)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   issue(nk > 2 ? 2 : nk - 1, 2);
@@ -984,10 +998,10 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     IWQ_SLICE(la[1] + so, wc[1], true)
     IWQ_SLICE(la[2] + so, wc[2], true)
     IWQ_SLICE(la[3] + so, wc[3], true)
-    // stage kt+1 landed (this wave's part: only stage kt+2's 5 pieces may still fly; near the end
-    // those are re-loads of the last K-step into a stage nobody reads again, so the count is
-    // constant), every read of stage kt retired
-    if constexpr (GROUPED) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    // stage kt+1 landed (this wave's part: only stage kt+2's 5 pieces -- 6 with the parameters -- may
+    // still fly; near the end those are re-loads of the last K-step into a stage nobody reads again),
+    // every read of stage kt retired
+    if (hp(kt + 2 < nk ? kt + 2 : nk - 1)) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     IWQ_PIN();
@@ -995,9 +1009,12 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     const int sd = kt % NSTAGE;
     const uint32_t sn = (uint32_t)(((kt + 1) % NSTAGE) * STAGE);
     u32x4 wn = lds_rd_u<0>(lc + sn);
+    const bool newp = hp(kt + 1);
     if constexpr (GROUPED) {  // older than the 4 A reads below: retired by the same lgkmcnt(4)
-      psv = lds_rd_d<0>(lp + sn);
-      pzv = lds_rd_d<TN * 4>(lp + sn);
+      if (newp) {
+        psv = lds_rd_d<0>(lp + sn);
+        pzv = lds_rd_d<TN * 4>(lp + sn);
+      }
     }
     // slice 3 of this stage; rolling reads of the next stage's slice 0; the refill of stage kt
     // spread one DMA piece per MFMA gap (each costs the issuing wave ~60-185 cycles: back to back
@@ -1012,7 +1029,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b32w(PrefillArgs a) {
     IWQ_PIN(); IWQ_MF(3); IWQ_RD_A(3, na); issue1(kd, sd, 3); IWQ_PIN();
     IWQ_LGKM(4);
     landed(wn);
-    params_landed();
+    if (newp) params_landed();
     IWQ_PIN(); IWQ_MF(4); IWQ_RD_A(4, na); issue1(kd, sd, 4); p0 = dqp(wn[0], t8, 0); if (NIB) t8 = wn[0] >> 8; IWQ_PIN();
     IWQ_PIN(); IWQ_MF(5); IWQ_RD_A(5, na); if (GROUPED) issue1(kd, sd, 5); p1 = dqp(wn[0], t8, 1); IWQ_PIN();
     IWQ_PIN(); IWQ_MF(6); IWQ_RD_A(6, na); p2 = dqp(wn[0], t8, 2); IWQ_PIN();
@@ -1823,10 +1840,10 @@ hipError_t launch_v(const PrefillArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool NIB, bool GROUPED = false>
+template <bool NIB, bool GROUPED = false, bool PG = false>
 hipError_t launch_w(const PrefillArgs& a, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
-  hipLaunchKernelGGL((k_w4a16_b32w<NIB, GROUPED>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
+  hipLaunchKernelGGL((k_w4a16_b32w<NIB, GROUPED, false, 0, PG>), dim3((unsigned)blocks), dim3(THR), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2943,6 +2960,7 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
       case 69: return launch_e<true, false, 2, false, true, true>(a, st);
       case 74: return launch_w<false, true>(a, st);  // 1 x 8 waves, hand-ordered stream
       case 75: return launch_w<true, true>(a, st);   // the same on NIB codes
+      case 79: return launch_w<false, true, true>(a, st);  // 74 with the parameters staged once per group
       default: return launch_w<false, true>(a, st);  // 74: +7-8 % over 45 (r02_ab_gemm_b32w_grouped.jsonl)
     }
   }
