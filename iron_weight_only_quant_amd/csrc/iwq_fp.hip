@@ -481,16 +481,13 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
     Vec8<DT_F16> o;
     bool nan8 = false;
     uint32_t c[8];
+    uint32_t cp[4];  // table path: the codes of elements 2j, 2j+1 in the 16-bit halves of cp[j]
     if (table) {  // finite group (grid: S > 0): table path, no NaN possible
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         uint32_t q;
         o.u[j] = fp_pair_lut<CODEC, SYM>(vk.u[j], p, bound2, lut, CODES ? &q : nullptr);
-        if constexpr (CODES != 0) {
-          const uint32_t cc = codes_of_values(q, a.f, rebias);
-          c[2 * j] = cc & 0xFFFFu;
-          c[2 * j + 1] = cc >> 16;
-        }
+        if constexpr (CODES != 0) cp[j] = codes_of_values(q, a.f, rebias);
       }
     } else {
 #pragma unroll
@@ -503,7 +500,12 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
     if (e0 < tnumel) {
       any_nan |= nan8;
       if (tout) o.store(tout + e0 * F::BYTES);
-      if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
+      if constexpr (CODES != 0) {
+        // table path: the pairs' halves straight into bytes / nibbles (two v_perm for bytes, the INT
+        // packing) instead of splitting them into eight words first (~14 VALU per unit)
+        if (table) store_codes8<CODES>(a.codes, e0, cp);
+        else store_fp_codes8<CODES>(a.codes, e0, c);
+      }
       if ((lane % LPG) == 0) {
         if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
         if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);

@@ -56,7 +56,12 @@ def main():
     ap.add_argument("--reps", type=int, default=2, help="passes over the copies per graph")
     ap.add_argument("--copies", type=int, default=16)
     ap.add_argument("--only", default="", help="comma list of path names to run")
+    ap.add_argument("--lib", default="", help="A/B: load this libiwq.so build instead of the tree's")
+    ap.add_argument("--tag", default="", help="A/B: label added to every line")
     a = ap.parse_args()
+    if a.lib:
+        from iron_weight_only_quant_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     from iron_weight_only_quant_amd import kernels as K
     R, C = a.rows, a.cols
     n = R * C
@@ -134,7 +139,7 @@ def main():
         fn()
         torch.cuda.synchronize()
         t = timed(fn, a.reps) / len(ws)
-        print(json.dumps({"path": name, "shape": [R, C], "copies": len(ws), "ms": round(t * 1e3, 4),
+        print(json.dumps({**({"tag": a.tag} if a.tag else {}), "path": name, "shape": [R, C], "copies": len(ws), "ms": round(t * 1e3, 4),
                           "weights_GBps": round(2 * n / t / 1e9, 1), "algo_bytes": int(algo),
                           "achieved_GBps": round(algo / t / 1e9, 1), "frac_of_8TBps": round(algo / t / PEAK, 3)}),
               flush=True)
