@@ -126,6 +126,29 @@ def test_no_cpu_fallback():
         QuantLinear.from_linear(torch.nn.Linear(128, 4).half(), w_bit=4, w_group_size=128)
 
 
+def test_quant_result_timeout_retry_logic():
+    """QuantResult.has_nan on nan_flag bit 1 (a timed-out per-tensor hand-off, include/iwq.h): with a
+    retry (out of place) it re-runs once and reports the new flag; without one (in place) it raises."""
+    from iron_weight_only_quant_amd.kernels import QuantResult
+    calls = []
+
+    def retry(v):
+        calls.append(v)
+        return torch.tensor([v], dtype=torch.int32)
+    r = QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32), lambda: retry(0))
+    assert not r.has_nan() and r.retried and calls == [0]
+    assert not r.has_nan() and calls == [0]  # the retry runs once
+    r = QuantResult(None, None, None, None, torch.tensor([3], dtype=torch.int32), lambda: retry(1))
+    assert r.has_nan() and r.retried  # the re-run's own NaN bit
+    r = QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32), lambda: retry(2))
+    with pytest.raises(RuntimeError, match="timed out"):
+        r.has_nan()  # the re-run timed out too
+    r = QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32))
+    with pytest.raises(RuntimeError, match="timed out"):
+        r.has_nan()
+    assert not QuantResult(None, None, None, None, torch.tensor([0], dtype=torch.int32)).has_nan()
+
+
 def test_geometry_errors_mirror_reference():
     from iron_weight_only_quant_amd.kernels import group_geometry
     assert group_geometry(4096, 11008, 128, 0) == (128, 4096 * 86)
