@@ -390,10 +390,9 @@ def gemm_variant_flags(v: int) -> int:
 
 GEMV_MAX_M = 16  # iwq_w4a16_gemm takes the weight-streaming decode kernel up to this many rows
 # w4a16_linear keeps the fused kernels (decode GEMV, the mid-M weight-streaming kernel below 256
-# rows, the split-K prefill kernel from 256) up to this many rows; above, dequantize-once + hipBLASLt
-# is faster (profiles/r02_ab_gemm_splitk_auto.jsonl vs the dequant pass of r02_gemm_sweep.jsonl:
-# at M = 1024 fused / dequant+hipBLASLt = 1.10 q_proj, 0.96 gate_proj, 0.84 down_proj)
-FUSED_MAX_M = 1024
+# rows, the split-K prefill kernel from 256) up to packed_fused_preferred's row count, at most this;
+# above, dequantize-once + hipBLASLt
+FUSED_MAX_M = 2048
 # from this many rows the prefill kernel can read NIB-layout codes (nib_codes; iwq_w4a16_gemm with
 # IWQ_FLAG_NIB_CODES): 74's NIB twin (variant 75), +0.5-1.2 % per channel at M = 8192 over the
 # current 74 (+4.5-5 % over the round-2 first 74; profiles/r02_ab_gemm_nib_product.jsonl)
@@ -412,6 +411,21 @@ def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     if group == -2:
         return M <= 192 or (M <= 1024 and K >= 2 * N)
     return M <= 32 or (M <= 512 and K >= 2 * N)
+
+
+def packed_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
+    """kernels.w4a16_linear (packed-only weights, PackedLinear): whether the fused kernels beat
+    dequant-once (iwq_dequant_packed) + F.linear for an M-row batch on an [N, K] weight.  Measured
+    cold in device time (tools/ab_auto.py --packed: each pass walks >= 1.2 GB of distinct codes,
+    hipGraph replay; profiles/r03_ab_packed_graph.jsonl, Llama-2-7B q / gate / down, 4-bit): per
+    channel every shape wins up to M = 1024 (q 0.99x there, gate 1.21x, down 1.38x) and down-like
+    weights (K >= 2N) up to 2048 (1.15x); g128 q / gate up to 768 (1.03 / 1.00x; q 0.93x at 1024),
+    down up to 1024 (1.18x; 0.99x at 1536).  (Round 2 stopped every shape at 1024 from MALL-warm
+    single-weight timings.)"""
+    down = K >= 2 * N
+    if group == -2:
+        return M <= (FUSED_MAX_M if down else 1024)
+    return M <= (1024 if down else 768)
 
 
 def w4a16_gemm_supported(x: torch.Tensor, N: int, K: int, n_bits: int, group: int) -> bool:
@@ -593,14 +607,14 @@ def w4a16_linear(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zer
                  nib_codes: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Forward on packed-only weights, fastest path per batch size: the weight-streaming GEMV for
     decode batches (M <= GEMV_MAX_M; on `tiled_codes` = tile_codes(codes) when given), the mid-M
-    weight-streaming kernel and the split-K prefill kernel up to FUSED_MAX_M rows, dequant-once +
-    hipBLASLt (F.linear) above,
+    weight-streaming kernel and the split-K prefill kernel up to packed_fused_preferred's rows
+    (1024 / 2048 per channel, 768 / 1024 g128), dequant-once + hipBLASLt (F.linear) above,
     where the library GEMM on a freshly dequantized weight beats the fused kernels.
     nib_codes: the same codes in the NIB layout (nib_codes(codes)), read by the prefill kernel at
     M >= NIB_MIN_M."""
     K = x.shape[-1]
     M = x.numel() // K
-    if M <= FUSED_MAX_M and w4a16_gemm_supported(x, N, K, n_bits, group):
+    if packed_fused_preferred(M, N, K, group) and w4a16_gemm_supported(x, N, K, n_bits, group):
         if tiled_codes is not None and M <= GEMV_MAX_M:
             return w4a16_gemm(x, tiled_codes, scales, zeros, n_bits, group, N, bias, tiled=True)
         if nib_codes is not None and M >= NIB_MIN_M and nib_supported(x, N, K, n_bits, group):

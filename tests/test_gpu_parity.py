@@ -967,7 +967,7 @@ def test_w4a16_nib_default(K, M, group):
     assert bool(((y1.float() - ref).abs() <= tol).all())
     with pytest.raises(ValueError):
         K.w4a16_gemm(x[:255], nib, r.scales, r.zeros, 4, group, N, b, nib=True)
-    if M <= K.FUSED_MAX_M:  # above, w4a16_linear dequantizes once and calls hipBLASLt
+    if K.packed_fused_preferred(M, N, Kd, group):  # else w4a16_linear dequantizes once for hipBLASLt
         yl = K.w4a16_linear(x, r.codes, r.scales, r.zeros, 4, group, N, b, nib_codes=nib)
         assert torch.equal(yl, y0)
 

@@ -5,7 +5,9 @@ Llama-2-7B shape, per M, per channel and g128.  Cold: each timed pass walks C di
 (>= 1 GB of fp16, so the 256 MB MALL holds none of them), as a model forward touches each layer's
 weight once; per-call time = pass time / C, median of rounds, arms interleaved in rotating order.
 Each pass is captured in a hipGraph and replayed, so the time is DEVICE time (--eager: eager calls,
-which at small M measure the host launch cost instead).  One JSON line per (group, shape, M)."""
+which at small M measure the host launch cost instead).  One JSON line per (group, shape, M).
+--packed: the packed-only forward instead (PackedLinear / kernels.w4a16_linear, no fp16 weight held):
+the fused kernels against dequant-once (iwq_dequant_packed) + F.linear, cold over >= --gb of CODES."""
 import argparse
 import json
 import os
@@ -28,18 +30,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--gb", type=float, default=1.2)
     ap.add_argument("--eager", action="store_true", help="time eager calls (host launch cost included)")
+    ap.add_argument("--packed", action="store_true", help="fused vs dequant-once + F.linear (packed-only weights)")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels
     for group in [int(g) for g in a.groups.split(",")]:
         for name in a.shapes.split(","):
             N, K = SHAPES[name]
-            copies = max(4, int(a.gb * 1e9 / (N * K * 2)) + 1)
+            copies = max(4, int(a.gb * 1e9 / (N * K * (0.5 if a.packed else 2))) + 1)
             ws, cs, ts, ss, zs = [], [], [], [], []
             for c in range(copies):
                 w = torch.empty(N, K, dtype=torch.float16, device="cuda")
                 kernels.fill_synthetic(w, 100 + c)
                 r = kernels.quantize_minmax(w, 4, group, False, 0, out=w, want_codes=True)
-                ws.append(w)
+                ws.append(None if a.packed else w)
                 cs.append(r.codes)
                 ts.append(kernels.tile_codes(r.codes, N, K))
                 ss.append(r.scales)
@@ -50,7 +53,10 @@ def main():
 
                 def ref():
                     for c in range(copies):
-                        torch.nn.functional.linear(x, ws[c])
+                        if a.packed:  # kernels.w4a16_linear above FUSED_MAX_M
+                            torch.nn.functional.linear(x, kernels.dequant_packed(cs[c], ss[c], zs[c], 4, group, N, K))
+                        else:
+                            torch.nn.functional.linear(x, ws[c])
 
                 def fused():
                     tiled = M <= kernels.GEMV_MAX_M
@@ -88,7 +94,7 @@ def main():
                         torch.cuda.synchronize()
                         times[k].append(e0.elapsed_time(e1) * 1e3 / copies)
                 med = {k: sorted(v)[len(v) // 2] for k, v in times.items()}
-                print(json.dumps({"mode": "eager" if a.eager else "graph", "group": group, "shape": name, "M": M, "copies": copies,
+                print(json.dumps({"mode": ("packed-" if a.packed else "") + ("eager" if a.eager else "graph"), "group": group, "shape": name, "M": M, "copies": copies,
                                   "hipblaslt_us": round(med["hipblaslt"], 2), "fused_us": round(med["fused"], 2),
                                   "fused_speedup": round(med["hipblaslt"] / med["fused"], 3)}), flush=True)
             del ws, cs, ts, ss, zs
