@@ -74,6 +74,9 @@ def parse():
                     help="untimed clock ramp before the copy-ceiling probe and the W warmup steps")
     ap.add_argument("--no-shapes", action="store_true",
                     help="skip the cold single-tensor calls per Llama shape (4096x4096, 11008x4096, 4096x11008)")
+    ap.add_argument("--no-sections", action="store_true",
+                    help="skip the configs[2] fused-forward, configs[4] format and configs[3] 70B sections")
+    ap.add_argument("--no-70b", action="store_true", help="skip the configs[3] Llama-2-70B section")
     return ap.parse_args()
 
 
@@ -289,7 +292,7 @@ def host_cpus():
     return usable, {"os_cpu_count": n_os, "affinity": n_aff, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
-def cpu_baseline(weights, bits, group, symmetric, budget_s):
+def cpu_baseline(weights, bits, group, symmetric, budget_s, model_name):
     """Reference CPU arithmetic on whole tensors of the same workload until the budget is spent, on
     every host CPU this job may use (torch intra-op threads = usable CPUs, recorded)."""
     from oracle.torch_ref import minmax_fake_quant_cpu
@@ -312,7 +315,7 @@ def cpu_baseline(weights, bits, group, symmetric, budget_s):
         torch.set_num_threads(prev)
     return {"value": round(done_bytes / spent / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "host": info,
-            "sample": f"{n} of the Llama-2-7B weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
+            "sample": f"{n} of this rank's {model_name} weight tensors ({done_bytes / 1e9:.2f} GB fp16) through "
                       f"oracle/torch_ref.py (reference quant_funcs.py:16-38 op sequence, torch CPU, "
                       f"{threads} threads on {info['cpu_model']}), {spent:.1f} s"}
 
@@ -341,7 +344,8 @@ def time_gather(plan, names, all_shapes, args, ws_n):
 def dry_run(args, ws_n, rank):
     """--dry-run: the multi-rank plumbing without a GPU (CPU tests): every rank builds zero-filled
     packed results of its bin's sizes, the rooted gather moves them to rank 0, and rank 0 prints the
-    bytes that crossed (each non-root bin exactly once) next to the plan's totals."""
+    bench record (per-rank roofline from stand-in kernel times, the CPU baseline) with the bytes that
+    crossed (each non-root bin exactly once) next to the plan's totals."""
     from iron_weight_only_quant_amd import shard
     shapes = shard.model_linear_shapes(args.model)
     bins = shard.plan_shards(shapes, ws_n)
@@ -350,7 +354,7 @@ def dry_run(args, ws_n, rank):
     names, codes, scales, zeros = [], [], [], []
     for i in mine:
         name, (r, c) = shapes[i]
-        G = r * c // args.group
+        G = shard.n_groups(r, c, args.group)
         names.append(name)
         codes.append(torch.zeros(r * (c // 2) if args.bits <= 4 else r * c, dtype=torch.uint8))
         scales.append(torch.zeros(G, dtype=torch.float16))
@@ -366,11 +370,27 @@ def dry_run(args, ws_n, rank):
         dist.all_reduce(t)
         sent, recv = int(t[0]), int(t[1])
         got = len(out) if out is not None else 0
+    # the record's multi-rank plumbing with stand-in timings (no GPU): per-rank statistics gathered
+    # over gloo, the roofline over ranks, the CPU baseline on rank 0 (a small CPU sample)
+    kernel_ms = 1.0 + 0.25 * rank  # stand-in: rank r "took" 1 + r/4 ms
+    numel = sum(shapes[i][1][0] * shapes[i][1][1] for i in mine)
+    alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
+    per_rank = gather_per_rank([kernel_ms, alg], ws_n)
+    roof = roofline_record(per_rank, "k_group<f16,128,asym,batched>", None, "dry run: no PMC")
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle.synth import synth
+        sample = [torch.from_numpy(synth(900 + i, (256, 1024), "float16")) for i in range(4)]
+        cpu = cpu_baseline(sample, args.bits, args.group, args.symmetric, 0.2, MODEL_NAME[args.model] + " (stand-in)")
+    total = all_ranks_sum(numel, ws_n)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "world": ws_n, "model": args.model, "tensors": len(shapes),
-                          "tensors_at_rank0": got,
-                          "plan_packed_bytes_per_rank": [sum(nb(shapes[i][1]) for i in b) for b in bins],
-                          "gather_sent_bytes": sent, "gather_recv_bytes": recv}), flush=True)
+        rec = build_record(args, ws_n, 0, args.weak, shapes, total, None, roof, {
+            "dry_run": True, "world": ws_n, "model": args.model, "tensors": len(shapes),
+            "tensors_at_rank0": got,
+            "plan_packed_bytes_per_rank": [sum(nb(shapes[i][1]) for i in b) for b in bins],
+            "gather_sent_bytes": sent, "gather_recv_bytes": recv, "cpu_baseline": cpu})
+        rec["note"] = "dry run over gloo on the CPU: stand-in timings, no GPU"
+        print(json.dumps(rec), flush=True)
 
 
 def kernel_sources_sha():
@@ -614,6 +634,253 @@ def make_shapes(model):
     return shard.model_linear_shapes(model)
 
 
+# ---------------------------------------------------------------------------------------------
+# Per-rank statistics and the JSON record (shared by the GPU run and the --dry-run rehearsal)
+# ---------------------------------------------------------------------------------------------
+def gather_per_rank(vals, ws_n):
+    """[[v0, v1, ...] of rank 0, of rank 1, ...]: every rank's float statistics, on every rank."""
+    if ws_n == 1:
+        return [list(vals)]
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=coll_device())
+    out = [torch.zeros_like(t) for _ in range(ws_n)]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu()] for o in out]
+
+
+def roofline_record(per_rank, kernel_name, traffic, traffic_src, ceiling=None, other=None):
+    """HBM roofline of the headline kernel over all ranks.  per_rank = [kernel_ms, alg_bytes] per rank
+    (HIP-event time of its launch on its stream; its algorithmic bytes per launch).  `achieved` is
+    per GPU: the mean algorithmic bytes per rank over the SLOWEST rank's kernel time (what the
+    max-over-ranks step time sees); `per_rank` gives each rank's own rate and fraction."""
+    kmax = max(k for k, _ in per_rank)
+    mean_bytes = sum(b for _, b in per_rank) / len(per_rank)
+    achieved = mean_bytes / (kmax / 1e3) / 1e9 if kmax > 0 else None
+    rec = {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+           "traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_name,
+           "kernel_ms": round(kmax, 4), "kernel_ms_basis": "max over ranks" if len(per_rank) > 1 else "rank 0",
+           "alg_bytes_per_launch": int(round(mean_bytes)) if len(per_rank) > 1 else int(per_rank[0][1]),
+           "per_rank": [{"rank": r, "kernel_ms": round(k, 4), "alg_bytes": int(b),
+                         "frac": (round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k > 0 else None)}
+                        for r, (k, b) in enumerate(per_rank)]}
+    if ceiling is not None:
+        rec["ceiling"] = ceiling
+        rec["kernel_over_ceiling"] = round(achieved / ceiling["GBps"], 4) if achieved else None
+    if other is not None:
+        rec["other_placement"] = other
+    return rec
+
+
+# ---------------------------------------------------------------------------------------------
+# Extra sections of the default run: BASELINE configs[2] (fused forward), configs[4] (FP formats),
+# configs[3] (Llama-2-70B) -- bounded, after the headline's timed region
+# ---------------------------------------------------------------------------------------------
+MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md chip table; never the sparse figure)
+FF_SHAPES = (("q_proj", 4096, 4096), ("gate_proj", 11008, 4096), ("down_proj", 4096, 11008))
+
+
+def _interleaved_ms(arms, reps=5, rounds=7):
+    """Median ms per call of each arm: every round times each arm once (reps calls back to back, HIP
+    events on the current stream -- the stream every arm launches on), arms in rotating order
+    (cdna_hip_programming.md §5.4 rule 24)."""
+    st = torch.cuda.current_stream()
+    for f in arms.values():
+        f()
+    torch.cuda.synchronize()
+    keys = list(arms)
+    times = {k: [] for k in keys}
+    for rd in range(rounds):
+        for k in keys[rd % len(keys):] + keys[:rd % len(keys)]:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                arms[k]()
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1) / reps)
+    return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
+
+
+def _graph_ms(calls, rounds=5):
+    """Median device ms per call of `calls` captured in ONE hipGraph and replayed (no host launch cost
+    in the time; the calls rotate over distinct resident buffers, so they run cold)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for c in calls:
+            c()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for c in calls:
+            c()
+    g.replay()
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    out = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        g.replay()
+        e1.record(st)
+        torch.cuda.synchronize()
+        out.append(e0.elapsed_time(e1) / len(calls))
+    del g
+    return sorted(out)[len(out) // 2]
+
+
+def fused_forward_section(rot_bytes=1 << 30):
+    """BASELINE configs[2]: Llama-2-7B INT4 per channel (and g=128) QuantLinear forward on the packed
+    codes (kernels.w4a16_gemm: MFMA dequant->GEMM) against the reference forward F.linear(x, W_deq)
+    (hipBLASLt on the resident fp16 weight, quant_linear.py:960-972) timed in the same run.
+    M = 8192 (the PPL batch 4 x 2048, main.py:117-128): interleaved, MFMA-bound -> TF/s and fraction
+    of the dense fp16 MFMA peak.  M = 1 (decode): cold (each call reads a different resident copy,
+    >= 1 GiB per replay, hipGraph) -> packed-weight GB/s and fraction of 8 TB/s.  `auto` = which path
+    QuantLinear(fused_forward="auto") takes at that M (kernels.auto_fused_preferred)."""
+    from iron_weight_only_quant_amd import kernels as K
+    F = torch.nn.functional
+    out = []
+    gen = torch.Generator(device="cuda").manual_seed(1234)
+    for name, N, Kd in FF_SHAPES:
+        w = torch.empty(N, Kd, dtype=torch.float16, device="cuda")
+        K.fill_synthetic(w, 7)
+        for group in (-2, 128):
+            r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+            gname = "per-channel" if group == -2 else f"g{group}"
+            M = 8192
+            x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
+            y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+            t = _interleaved_ms({"fused": lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y),
+                                 "F.linear": lambda: F.linear(x, r.out)})
+            tf = 2.0 * M * N * Kd / (t["fused"] / 1e3) / 1e12
+            out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "mfma",
+                        "fused_ms": round(t["fused"], 4), "F_linear_ms": round(t["F.linear"], 4),
+                        "fused_TFLOPs": round(tf, 1), "frac_of_mfma_peak": round(tf / MFMA_PEAK_TFLOPS, 4),
+                        "F_linear_TFLOPs": round(2.0 * M * N * Kd / (t["F.linear"] / 1e3) / 1e12, 1),
+                        "fused_vs_F_linear": round(t["F.linear"] / t["fused"], 3),
+                        "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
+            del x, y
+            # decode: M = 1, cold, codes in the decode tile layout (what QuantLinear "auto" keeps)
+            M = 1
+            x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
+            y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+            tiled = K.tile_codes(r.codes, N, Kd)
+            cb = r.codes.numel()
+            copies = [tiled] + [tiled.clone() for _ in range(int(rot_bytes // cb))]
+            wbytes = cb + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0)
+            t_f = _graph_ms([(lambda c=c: K.w4a16_gemm(x, c, r.scales, r.zeros, 4, group, N, tiled=True, out=y))
+                             for c in copies])
+            refs = [r.out] + [r.out.clone() for _ in range(int(rot_bytes // (N * Kd * 2)))]
+            t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs])
+            gbs = wbytes / (t_f / 1e3) / 1e9
+            out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "hbm",
+                        "fused_ms": round(t_f, 5), "F_linear_ms": round(t_r, 5),
+                        "packed_weight_GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                        "fused_vs_F_linear": round(t_r / t_f, 3), "cold_copies": len(copies),
+                        "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
+            del x, y, tiled, copies, refs, r
+        del w
+        torch.cuda.empty_cache()
+    return {"config": "BASELINE configs[2]: Llama-2-7B INT4 fused dequant+GEMM QuantLinear forward (packed codes) "
+                      "vs F.linear on the dequantized fp16 weight, same run",
+            "kernels": "M=8192: k_w4a16_b32w (iwq_prefill.hip); M=1: k_w4a16_gemv(_ct) on tile-layout codes",
+            "mfma_peak_TFLOPs": MFMA_PEAK_TFLOPS, "rows": out}
+
+
+def formats_section(rows=11008, cols=4096, copies=16):
+    """BASELINE configs[4]: FP8 E4M3 and FP4 (E2M1 codec, and the fp4_quantize_cpu.py E2M1 grid)
+    weight formats as pack (fake-quant + codes) / unpack (codes -> fp16) kernels on a Llama-2-7B
+    gate_proj weight, cold (the calls rotate over `copies` distinct resident weights, hipGraph)."""
+    from iron_weight_only_quant_amd import kernels as K
+    n, g = rows * cols, 128
+    G = n // g
+    ws = []
+    for c in range(copies):
+        t = torch.empty(rows, cols, dtype=torch.float16, device="cuda")
+        K.fill_synthetic(t, 100 + c)
+        ws.append(t)
+    outs = [torch.empty_like(t) for t in ws]
+    paths = []
+    for fname, e, m, sym in (("fp8_e4m3_g128_sym", 4, 3, True), ("fp8_e4m3_g128_asym", 4, 3, False),
+                             ("fp4_e2m1_g128_asym", 2, 1, False)):
+        cb = n if 1 + e + m > 4 else n // 2
+        par = 2 * G * (1 if sym else 2)
+        packs = [K.quantize_fp(w, e, m, g, sym, 0, out=o, want_codes=True) for w, o in zip(ws, outs)]
+        paths.append((fname + "_pack", [(lambda w=w, o=o, e=e, m=m, sym=sym:
+                                         K.quantize_fp(w, e, m, g, sym, 0, out=o, want_codes=True))
+                                        for w, o in zip(ws, outs)], 4 * n + cb + par))
+        paths.append((fname + "_unpack", [(lambda p=p, o=o, e=e, m=m:
+                                           K.dequant_fp_packed(p.codes, p.scales, p.zeros, e, m, g, rows, cols, out=o))
+                                          for p, o in zip(packs, outs)], 2 * n + cb + par))
+    grids = [K.fp4_grid(w, g, want_codes=True) for w in ws]
+    paths.append(("e2m1_grid_g128_pack", [(lambda w=w: K.fp4_grid(w, g, want_codes=True)) for w in ws],
+                  4 * n + n // 2 + 2 * G))
+    paths.append(("e2m1_grid_g128_unpack", [(lambda p=p, o=o: K.dequant_fp_packed(p.codes, p.scales, None, 2, 1, g,
+                                                                                  rows, cols, out=o))
+                                            for p, o in zip(grids, outs)], 2 * n + n // 2 + 2 * G))
+    res = []
+    for name, calls, alg in paths:
+        t = _graph_ms(calls) / 1e3
+        res.append({"path": name, "us": round(t * 1e6, 2), "alg_bytes": int(alg),
+                    "achieved_GBps": round(alg / t / 1e9, 1), "frac_of_hbm_peak": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)})
+    del ws, outs, grids
+    torch.cuda.empty_cache()
+    return {"config": f"BASELINE configs[4]: FP8 / FP4 weight formats, pack (fake-quant + codes) and unpack "
+                      f"(codes -> fp16) on [{rows}, {cols}] fp16, cold over {copies} resident copies",
+            "kernels": "pack: k_fp_group_lut / fp4 grid (iwq_fp.hip); unpack: iwq_fpunpack.hip", "rows": res}
+
+
+def model70b_section(args, ws_n, rank, steps=5, warmup=2):
+    """BASELINE configs[3]: Llama-2-70B INT4 g=128, all 560 Linear weights (137 GB fp16) bin-packed
+    over the ranks, quantized IN PLACE (QuantLinear semantics; one GPU holds the whole model) with one
+    batched launch per rank per step.  value = 70B fp16 bytes / max-over-ranks step time."""
+    from iron_weight_only_quant_amd import kernels
+    weights, _, shapes = make_weights("llama2-70b", rank, ws_n)
+    plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric, outs=weights)
+    stream = torch.cuda.current_stream()
+    a = argparse.Namespace(warmup=warmup, steps=steps, variant=0)
+    kernel_ms, ms = timed_steps(plan, a, ws_n, stream)
+    numel = plan.numel
+    alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
+    per_rank = gather_per_rank([kernel_ms, alg], ws_n)
+    total = all_ranks_sum(numel, ws_n)
+    del plan, weights
+    torch.cuda.empty_cache()
+    return {"config": f"BASELINE configs[3]: Llama-2-70B {len(shapes)} Linear weights bin-packed over {ws_n} GPU(s), "
+                      f"INT{args.bits} g={args.group} {'sym' if args.symmetric else 'asym'}, in place",
+            "value": round(total * 2 / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
+            "steps": steps, "warmup": warmup, "fp16_weights_total": total, "scaling": "strong",
+            "roofline": roofline_record(per_rank, "k_group<f16,128,asym,batched> in place", None,
+                                        "no PMC record for this workload")}
+
+
+def build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, roofline, extra):
+    placement = "in-place" if args.inplace else "out-of-place"
+    if weak:
+        workload = f"{MODEL_NAME[args.model]} all {len(all_shapes)} Linear weights on every GPU "
+    else:
+        workload = f"{MODEL_NAME[args.model]} {len(all_shapes)} Linear weights bin-packed over {ws_n} GPU(s) "
+    value = total_numel * 2 / (ms_per_step / 1e3) / 1e9 if ms_per_step else None
+    rec = {
+        "metric": METRIC, "value": None if value is None else round(value, 2), "unit": "GB/s", "n_gpus": n_dev,
+        "ranks": ws_n, "n_devices": n_dev, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None if ms_per_step is None else round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "fp16",
+        "data": "synthetic",
+        "config": {"workload": workload + f"({total_numel} fp16 weights in all), INT{args.bits} g={args.group} "
+                               f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
+                               f"{placement} dequant + scales/zeros, one batched launch per rank per step",
+                   "model": args.model, "bits": args.bits, "group": args.group,
+                   "parallelism": f"layer-shard x{ws_n} (no collective)"},
+        "roofline": roofline,
+    }
+    rec.update(extra)
+    if n_dev < ws_n:
+        rec["note"] = f"{ws_n} ranks shared {n_dev} GPU(s) (gloo rehearsal): one GPU's bandwidth, not a scaling point"
+    return rec
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -664,9 +931,13 @@ def main():
     alg_bytes = numel * 2 + numel * 2 + groups * 2 * (1 if args.symmetric else 2)  # read w, write deq, s(,z)
     if args.gather:
         alg_bytes += numel // 2 if args.bits <= 4 else numel  # packed codes written too
-    value = total_numel * 2 / (ms_per_step / 1e3) / 1e9
-    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
-    traffic, traffic_src = committed_traffic(args.traffic_file, numel, args.bits, args.group)
+    per_rank = gather_per_rank([kernel_ms, alg_bytes], ws_n)
+    if ws_n == 1:
+        traffic, traffic_src = committed_traffic(args.traffic_file, numel, args.bits, args.group)
+    else:
+        traffic, traffic_src = None, ("the committed PMC record is the 1-GPU workload's; at N > 1 every rank runs "
+                                      "a different bin (profiles/traffic.json: +0.07 % over algorithmic at N = 1)")
+    roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched>", traffic, traffic_src, ceiling, other)
 
     weak_rec = None
     if ws_n > 1 and not weak and args.model == "llama2-7b" and not args.no_weak and not args.scatter:
@@ -674,38 +945,28 @@ def main():
         weights = None
         torch.cuda.empty_cache()
         weak_rec, shapes_rec = weak_secondary(args, ws_n, rank)
+        weights, _, _ = make_weights(args.model, rank, ws_n) if (rank == 0 and not args.no_cpu_baseline) else (None, 0, 0)
 
     cpu = None
-    if rank == 0 and ws_n == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(weights, args.bits, args.group, args.symmetric, args.cpu_seconds)
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(weights, args.bits, args.group, args.symmetric, args.cpu_seconds, MODEL_NAME[args.model])
+    plan = weights = None
+    torch.cuda.empty_cache()
 
     ppl = None
     if rank == 0 and ws_n == 1 and not args.no_ppl:
         ppl = ppl_plumbing(args.bits, args.group, args.symmetric)
 
+    # BASELINE configs[2] / [4] (one GPU: the driver's N = 1 run) and configs[3] (every N)
+    fused = formats = m70 = None
+    if ws_n == 1 and not args.no_sections:
+        fused = fused_forward_section()
+        formats = formats_section()
+    if args.model == "llama2-7b" and not args.no_sections and not args.no_70b:
+        m70 = model70b_section(args, ws_n, rank)
+
     if rank == 0:
-        placement = "in-place" if args.inplace else "out-of-place"
-        if weak:
-            workload = f"{MODEL_NAME[args.model]} all {len(all_shapes)} Linear weights on every GPU "
-        else:
-            workload = f"{MODEL_NAME[args.model]} {len(all_shapes)} Linear weights bin-packed over {ws_n} GPU(s) "
-        rec = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": n_dev, "ranks": ws_n,
-            "n_devices": n_dev, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": workload + f"({total_numel} fp16 weights in all), INT{args.bits} g={args.group} "
-                                   f"{'sym' if args.symmetric else 'asym'} pseudo_quantize_tensor, "
-                                   f"{placement} dequant + scales/zeros, one batched launch per rank per step",
-                       "model": args.model, "bits": args.bits, "group": args.group,
-                       "parallelism": f"layer-shard x{ws_n} (no collective)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_group<f16,128,asym,batched>", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes, "ceiling": ceiling,
-                         "kernel_over_ceiling": (round(alg_bytes / (kernel_ms / 1e3) / 1e9 / ceiling["GBps"], 4)
-                                                 if ceiling else None),
-                         "other_placement": other},
+        rec = build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, roofline, {
             "shapes": shapes_rec,
             "shapes_scaling": (None if shapes_rec is None else "single GPU" if ws_n == 1 else
                                f"weak: each of {ws_n} ranks runs its own cold calls at once; weights_GBps = "
@@ -716,9 +977,10 @@ def main():
             "ppl_plumbing": ppl,
             "gather_ms": gather_ms, "gather_bytes_to_rank0": gather_bytes,
             "scatter_ms": scatter_ms,
-        }
-        if n_dev < ws_n:
-            rec["note"] = f"{ws_n} ranks shared {n_dev} GPU(s) (gloo rehearsal): one GPU's bandwidth, not a scaling point"
+            "fused_forward": fused,
+            "formats": formats,
+            "llama2_70b": m70,
+        })
         print(json.dumps(rec), flush=True)
     if ws_n > 1:
         import torch.distributed as dist

@@ -91,12 +91,15 @@ int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant
  *   out_scales [G] storage dtype; nullable
  *   out_zeros  [G] storage dtype; ignored when symmetric; nullable
  *   nan_flag   device uint32, OR-ed with 1 if any dequantized value is NaN; nullable.  Also OR-ed
- *              with 2 if the per-tensor one-pass kernel's in-launch hand-off between workgroups timed
- *              out (its workgroups were not all resident -- another kernel held CUs): the outputs are
- *              then invalid.  Out of place the input is untouched and the caller re-runs the call with
- *              IWQ_FLAG_VARIANT(6) (the two-kernel form, which cannot time out) into the same outputs
- *              (kernels.QuantResult.has_nan does); in place it must fail.  Without a nan_flag the
- *              per-tensor path takes the two-kernel form.
+ *              with 2 if the per-tensor one-pass kernel's in-launch hand-off between workgroups was
+ *              ABORTED (its workgroups were not all resident -- another kernel held CUs): the launch
+ *              then wrote NOTHING (no output, code or parameter byte; a consensus word decides one
+ *              outcome for every workgroup before any store), so the input is untouched, in place
+ *              too, and the caller re-runs the call with IWQ_FLAG_VARIANT(6) (the two-kernel form,
+ *              which cannot time out) into the same outputs (kernels.QuantResult.has_nan does).
+ *              OR-ed with 4 if the outputs are invalid (a workgroup could not rejoin a launch that
+ *              went ahead; not reachable while stores become visible): the call must fail.  Without a
+ *              nan_flag the per-tensor path takes the two-kernel form.
  *   symmetric  0 -> zero_point=True path (:16-22), 1 -> absmax path (:23-29)
  */
 int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int n_bits,

@@ -58,7 +58,15 @@ class PackedLinear(nn.Module):
         self.register_buffer("scales", scales.reshape(-1, 1).contiguous())
         self.register_buffer("zeros", None if self.symmetric else zeros.reshape(-1, 1).contiguous())
         self.bias = nn.Parameter(bias, requires_grad=False) if bias is not None else None
-        self._tiled = None
+        # the decode tile layout of qweight: a derived cache, so a non-persistent buffer (module.to()
+        # moves it, state_dict keys stay qweight / scales / zeros / bias) dropped on every state-dict
+        # load (the new codes are copied into qweight; a stale tile copy would serve M <= 16 batches)
+        self.register_buffer("_tiled", None, persistent=False)
+        self.register_load_state_dict_post_hook(PackedLinear._drop_tiles_after_load)
+
+    @staticmethod
+    def _drop_tiles_after_load(module, incompatible_keys):
+        module._buffers["_tiled"] = None
 
     @classmethod
     def from_quant_linear(cls, q):
@@ -86,7 +94,7 @@ class PackedLinear(nn.Module):
             m = x.numel() // self.in_features
             if (self._tiled is None and m <= kernels.GEMV_MAX_M and self.out_features % 16 == 0
                     and self.in_features % 128 == 0):
-                self._tiled = kernels.tile_codes(self.qweight, self.out_features, self.in_features)
+                self._buffers["_tiled"] = kernels.tile_codes(self.qweight, self.out_features, self.in_features)
             return kernels.w4a16_linear(x, self.qweight, self.scales.view(-1),
                                         None if self.zeros is None else self.zeros.view(-1), self.w_bit,
                                         self.w_group_size, self.out_features,

@@ -47,17 +47,6 @@ int device_cu_count() {
   return cached[dev];
 }
 
-// Per-launch granule tag of the one-pass per-tensor kernel when the granules are not zeroed first
-// (A/B variant 8): process-wide, never 0 or 1 (1 is the memset form's tag).
-uint32_t next_onepass_tag() {
-  static std::atomic<uint32_t> counter{1};
-  uint32_t t;
-  do {
-    t = counter.fetch_add(1, std::memory_order_relaxed) + 1;
-  } while (t < 2);
-  return t;
-}
-
 // Resident 256-thread blocks per CU for a kernel (occupancy API: VGPRs/LDS; SGPRs are capped at
 // 80 on the persistent kernels so the API answer is exact).  Cached per instantiation & device.
 template <typename Kern>
@@ -860,12 +849,23 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
 // every workgroup sweeps all granules (relaxed agent-scope atomic loads, bounded spin) until every
 // tag is 1, folds them, and the workgroup quantizes its registers and stores -- 4 B per element of
 // HBM traffic instead of the two-kernel pair's 6.  The granules (8 B x CU count, at the workspace's
-// start) are zeroed by a hipMemsetAsync before every launch.  A spin that gives up (a workgroup
-// not resident: another kernel holding CUs) sets bit 1 of nan_flag, so the call fails loudly.
+// start) and the CONSENSUS word after them are zeroed by a hipMemsetAsync before every launch.
+//
+// Fail-safe hand-off (round 4): the hand-off needs every workgroup resident at once; when another
+// kernel holds CUs a sweep can give up.  Every workgroup stores NOTHING until the launch has agreed
+// on one outcome, decided by the first compare-and-swap on the consensus word:
+//   * a sweep that saw every granule CASes 0 -> GO; a sweep that gave up CASes 0 -> ABORT;
+//   * a workgroup stores (output, codes, parameters) only if the word reads GO;
+//   * a workgroup that gave up but finds GO sweeps again: the GO-er saw every granule, so all of
+//     them are published and this sweep ends (bounded; a second give-up -- not reachable while
+//     stores become visible -- sets nan_flag bit 2: outputs invalid).
+// On ABORT no byte of any output is written and nan_flag bit 1 is set, so the host can re-run the
+// same call on the two-kernel pair, IN PLACE too: the input is untouched.
 // ---------------------------------------------------------------------------------------------
 constexpr int OP_THR = 512;
 constexpr uint32_t OP_SPIN_LIMIT = 1u << 22;
 constexpr int OP_NT = 2;  // buffer-instruction cache bits: non-temporal (streamed once)
+constexpr unsigned long long OP_GO = 1, OP_ABORT = 2;
 
 // Workgroup b owns the contiguous vectors [b * nvt * 512, (b + 1) * nvt * 512) (16-B vectors of 8
 // elements; nvt <= NV vectors per thread, chosen so the chunks spread over every CU); vector i of
@@ -873,17 +873,18 @@ constexpr int OP_NT = 2;  // buffer-instruction cache bits: non-temporal (stream
 // workgroup.  The loads go through a buffer descriptor over the workgroup's chunk (one 32-bit per-lane
 // offset for all vectors; the range check zero-fills loads beyond the chunk -- i >= nvt, or the last
 // chunk's tail -- without touching memory, and the key fold masks them).  A granule counts once its
-// tag equals this launch's `tag` (1 after the per-launch memset).
+// tag equals 1 (granules[gridDim.x] is the consensus word; all zeroed by the per-launch memset).
 template <int DT, bool SYM, int CODES, int NV>
 __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* out, uint8_t* codes, void* scales,
                                                            void* zeros, int64_t nvec, int nvt,
-                                                           unsigned long long* granules, uint32_t tag, int n_bits,
+                                                           unsigned long long* granules, int n_bits,
                                                            uint32_t* nan_flag, uint32_t spin_limit) {
+  constexpr uint32_t tag = 1;
   using F = Fmt<DT>;
   static_assert(DT == DT_F16, "one-pass per-tensor: fp16 (keys packed in one dword, packed fast path)");
   typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
   __shared__ int32_t smn[OP_THR / 64], smx[OP_THR / 64];
-  __shared__ int32_t fin[2];
+  __shared__ int32_t fin[3];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t chunk = (int64_t)nvt * OP_THR;                    // vectors per workgroup
@@ -923,38 +924,65 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
                        __HIP_MEMORY_SCOPE_AGENT);
   }
   if (wv == 0) {
-    // sweep every workgroup's granule until all carry this launch's tag (relaxed agent-scope loads
-    // bypass L1)
+    // sweep every workgroup's granule until all carry the tag (relaxed agent-scope loads bypass L1)
     const int ng = (int)gridDim.x;
-    int32_t gmn = 0x7FFF, gmx = -0x8000;
-    bool timed_out = false;
-    for (int g0 = 0; g0 < ng; g0 += 64) {
-      const int g = g0 + lane;
-      uint32_t spins = 0;
-      unsigned long long x = 0;
-      while (true) {
-        x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : ((unsigned long long)tag << 32);
-        if (__all((uint32_t)(x >> 32) == tag)) break;
-        if (++spins > spin_limit) {
-          timed_out = true;
-          break;
+    int32_t gmn, gmx;
+    auto sweep = [&](uint32_t limit) -> bool {  // true: gave up before seeing every granule
+      gmn = 0x7FFF;
+      gmx = -0x8000;
+      bool gave_up = false;
+      for (int g0 = 0; g0 < ng; g0 += 64) {
+        const int g = g0 + lane;
+        uint32_t spins = 0;
+        unsigned long long x = 0;
+        while (true) {
+          x = g < ng ? __hip_atomic_load(granules + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : ((unsigned long long)tag << 32);
+          if (__all((uint32_t)(x >> 32) == tag)) break;
+          if (++spins > limit) {
+            gave_up = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (g < ng && (uint32_t)(x >> 32) == tag) {
+          gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
+          gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
+        }
       }
-      if (g < ng && (uint32_t)(x >> 32) == tag) {
-        gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
-        gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
+      return gave_up;
+    };
+    // spin_limit 0 (test-only variant 9): every workgroup gives up, so the launch ABORTs
+    bool timed_out = sweep(spin_limit) || spin_limit == 0;
+    // one outcome for the whole launch: the first CAS on the consensus word decides
+    unsigned long long decided = 0;
+    if (lane == 0) {
+      unsigned long long expect = 0;
+      const unsigned long long want = timed_out ? OP_ABORT : OP_GO;
+      decided = __hip_atomic_compare_exchange_strong(granules + ng, &expect, want, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    ? want
+                    : expect;
+    }
+    decided = (unsigned long long)__shfl((long long)decided, 0);
+    bool go = decided == OP_GO;
+    if (go && timed_out) {
+      // another workgroup saw every granule: they are all published, so this sweep completes
+      if (sweep(OP_SPIN_LIMIT * 4)) {
+        go = false;
+        if (lane == 0 && nan_flag) atomicOr(nan_flag, 4u);
       }
     }
     group_minmax<64>(gmn, gmx);
     if (lane == 0) {
       fin[0] = gmn;
       fin[1] = gmx;
-      if (timed_out && nan_flag) atomicOr(nan_flag, 2u);
+      fin[2] = go ? 1 : 0;
+      if (!go && decided == OP_ABORT && nan_flag) atomicOr(nan_flag, 2u);
     }
   }
   __syncthreads();
+  if (fin[2] == 0) return;  // ABORT: no output byte is written (the input is untouched)
   const GroupParams p = params_from_keys<DT, SYM>(fin[0], fin[1], n_bits, rmax_for(n_bits, SYM));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (scales) store_param<DT>(scales, 0, p.s);

@@ -377,40 +377,36 @@ void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, voi
 template <int DT, bool SYM, int CODES, int NV>
 hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nvec,
                                     int nvt, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus,
-                                    bool memset_tags, uint32_t spin_limit) {
+                                    uint32_t spin_limit) {
   // one workgroup per nvt * 512 vectors (<= the CU count: every chunk is non-empty and all are resident)
   const int64_t chunk = (int64_t)nvt * OP_THR;
   const int64_t nblk = (nvec + chunk - 1) / chunk;
   if (nvt < 1 || nvt > NV || nblk < 1 || nblk > cus) return hipErrorInvalidValue;
-  uint32_t tag = 1;
-  if (memset_tags) {
-    const size_t gbytes = ((size_t)nblk * 8 + 15) / 16 * 16;  // the granules: zeroed before the launch
-    hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
-    if (e != hipSuccess) return e;
-  } else {
-    tag = next_onepass_tag();
-  }
+  // the granules and the consensus word after them: zeroed before the launch
+  const size_t gbytes = ((size_t)(nblk + 1) * 8 + 15) / 16 * 16;
+  hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_tensor_onepass<DT, SYM, CODES, NV>), dim3((unsigned)nblk), dim3(OP_THR), 0, st,
                      static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales, zeros,
-                     nvec, nvt, reinterpret_cast<unsigned long long*>(ws), tag, n_bits, nan_flag, spin_limit);
+                     nvec, nvt, reinterpret_cast<unsigned long long*>(ws), n_bits, nan_flag, spin_limit);
   return hipGetLastError();
 }
 template <int DT, bool SYM, int CODES>
 bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err,
-                           bool memset_tags, bool fixed_nv, uint32_t spin_limit) {
+                           bool fixed_nv, uint32_t spin_limit) {
   if constexpr (DT != DT_F16) {
     return false;
   } else {
-    if (nan_flag == nullptr) return false;  // a timed-out hand-off must be reportable (bit 1)
+    if (nan_flag == nullptr) return false;  // an aborted hand-off must be reportable (bit 1)
     const int cus = device_cu_count();
-    if (cus * 8 > (int64_t)TENSOR_PARTS_MAX * 8) return false;  // granules beyond the workspace
+    if ((int64_t)cus + 1 > (int64_t)TENSOR_PARTS_MAX) return false;  // granules beyond the workspace
     const int64_t nvec = numel / 8;
     const int64_t per = (nvec + (int64_t)cus * OP_THR - 1) / ((int64_t)cus * OP_THR);
     // nvt = per spreads the chunks over every CU; fixed_nv (A/B) uses the template's NV instead
-    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags, spin_limit);
-    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags, spin_limit);
-    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, memset_tags, spin_limit);
+    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
     else return false;
     return true;
   }
@@ -418,16 +414,16 @@ bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, 
 
 // variants: 0 = one pass where the tensor fits the registers (fp16, n_bits <= 8), else the pair below;
 // 6 = the pair (round-2 default) forced; 7 = one pass with NV vectors per thread (the first form:
-// fewer, fuller chunks, some CUs idle); 8 = one pass with per-launch tags instead of the memset (A/B);
-// 9 = TEST ONLY: one pass whose hand-off gives up at once (spin limit 0), so the timeout report
-// (nan_flag bit 1) and the host's retry on the pair can be exercised
+// fewer, fuller chunks, some CUs idle);
+// 9 = TEST ONLY: one pass whose every sweep gives up at once (spin limit 0), so the launch ABORTs:
+// nothing is written, nan_flag bit 1 is set, and the host's retry on the pair can be exercised
 template <int DT, bool SYM, int CODES>
 hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int variant) {
-  if (variant == 0 || variant == 7 || variant == 8 || variant == 9) {
+  if (variant == 0 || variant == 7 || variant == 9) {
     hipError_t e = hipSuccess;
     if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e,
-                                              variant != 8, variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT))
+                                              variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT))
       return e;
   }
   const int64_t nunits = numel / 8;

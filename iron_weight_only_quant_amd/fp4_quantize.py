@@ -1,9 +1,9 @@
 """Drop-in for the reference's fp4_quantize_cpu.py (`quantize_fp16_to_fp4_e1m2`, :47-72) on the GPU.
 
-Same signature, grouping and errors; like the reference it returns the GROUPED view
-([-1, group_size], or [1, numel] per tensor) of the fake-quantized fp16 values, and
-`return_scales=True` (accepted but ignored by the reference) additionally returns the per-group
-scales S = absmax / 6."""
+Same signature, grouping, errors and return value: the GROUPED view ([-1, group_size], or [1, numel]
+per tensor) of the fake-quantized fp16 values.  `return_scales` is accepted and ignored, as in the
+reference (fp4_quantize_cpu.py:47, :72); the per-group scales S = absmax / 6 (and the E2M1 codes) are
+available from kernels.fp4_grid(w, group_size, per_tensor, want_codes=...)."""
 import torch
 
 from . import kernels
@@ -24,6 +24,4 @@ def quantize_fp16_to_fp4_e1m2(tensor, group_size=128, per_tensor=False, return_s
         out = out.reshape(-1, group_size)
     if per_tensor:
         out = out.reshape(1, -1)
-    if return_scales:
-        return out, res.scales.view(-1, 1)
     return out

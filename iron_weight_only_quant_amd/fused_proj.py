@@ -21,6 +21,12 @@ input and keeps it; the other members called with the SAME tensor object (same s
 take their column slice of it.  Any other input, or a batch above the decode GEMV's rows, makes a
 member run its own module's forward -- so a caller that does not follow the q, k, v order still gets
 exact per-layer results.
+
+Staleness: the concatenated copies are derived from the members' codes / scales / zeros / bias.
+Every new input first compares the members' current tensors (object and in-place version) with the
+ones the copies were built from; after a load_state_dict (QuantLinear drops its codes, PackedLinear
+copies new ones in place) or a re-quantization the group is rebuilt from the members' new state, or
+-- if a member can no longer take part -- retired, and every member runs its own forward.
 """
 import torch
 import torch.nn as nn
@@ -51,11 +57,33 @@ def _packed_view(m):
     return codes, sc, zr, bias, m.w_bit, m.w_group_size, bool(m.symmetric)
 
 
+def _version(t):
+    try:
+        return t._version
+    except RuntimeError:  # inference-mode tensors keep no version counter
+        return -1
+
+
+def _member_state(m):
+    """Identity of the member tensors the fused copies are built from: (object, in-place version)."""
+    ts = (m._buffers.get("qweight"), m._buffers.get("scales"), m._buffers.get("zeros"), m._parameters.get("bias"))
+    return tuple(None if t is None else (id(t), _version(t), t.data_ptr()) for t in ts)
+
+
 class FusedProjection(nn.Module):
     """Row-concatenated packed codes (decode tile layout) + parameters of sibling projections."""
 
     def __init__(self, members):
         super().__init__()
+        # the members are not submodules of this one (they stay where the model holds them)
+        self.__dict__["_members"] = list(members)
+        self._dead = False
+        self._build()
+        self._key = None
+        self._out = None
+
+    def _build(self):
+        members = self._members
         views = [_packed_view(m) for m in members]
         if any(v is None for v in views):
             raise ValueError("FusedProjection: every member must be an INT 2-4 bit quant_dim-0 fp16 layer with codes")
@@ -79,23 +107,35 @@ class FusedProjection(nn.Module):
             bias = torch.cat([v[3] if v[3] is not None else torch.zeros(n, dtype=torch.float16, device=codes.device)
                               for v, n in zip(views, self.sizes)])
         self.register_buffer("bias", bias, persistent=False)
-        self._key = None
-        self._out = None
+        self._state = [_member_state(m) for m in members]
+
+    def _refresh(self):
+        """Rebuild from the members' current state if it changed since the copies were made; False
+        (and retired for good) if a member can no longer take part."""
+        if self._dead:
+            return False
+        if [_member_state(m) for m in self._members] == self._state:
+            return True
+        try:
+            self._build()
+            return True
+        except ValueError:
+            self._dead = True
+            self.qweight_tiled = self.scales = self.zeros = self.bias = None
+            return False
 
     def usable(self, x):
-        return (x.dtype == torch.float16 and x.shape[-1] == self.in_features
+        return (not self._dead and x.dtype == torch.float16 and x.shape[-1] == self.in_features
                 and x.numel() // self.in_features <= kernels.GEMV_MAX_M
                 and kernels.w4a16_gemm_supported(x, self.out_features, self.in_features, self.w_bit,
                                                  self.w_group_size))
 
     def output_for(self, x):
         """The concatenated [.., sum N] output for x, computed once per (tensor, storage version)."""
-        try:
-            ver = x._version
-        except RuntimeError:  # inference-mode tensors keep no version counter
-            ver = -1
-        key = (id(x), ver, x.data_ptr())
+        key = (id(x), _version(x), x.data_ptr())
         if self._key != key or self._out is None:
+            if not self._refresh():
+                return None
             self._out = kernels.w4a16_gemm(x, self.qweight_tiled, self.scales, self.zeros, self.w_bit,
                                            self.w_group_size, self.out_features, self.bias, tiled=True)
             self._key = key
@@ -116,10 +156,12 @@ def _member_forward(member, fused, index):
 
     def forward(x):
         if fused.usable(x):
-            y = fused.output_for(x)[..., lo:hi]
-            if last:
-                fused.release()  # the last member: drop the cached output
-            return y
+            full = fused.output_for(x)
+            if full is not None:  # None: the group was retired (a member changed; see _refresh)
+                y = full[..., lo:hi]
+                if last:
+                    fused.release()  # the last member: drop the cached output
+                return y
         return own(x)
     return forward
 

@@ -30,19 +30,25 @@ class QuantResult:
     retried: bool = False             # has_nan() found a timed-out hand-off and re-ran the call
 
     def has_nan(self) -> bool:
+        v = self.settle()
+        return v != 0
+
+    def settle(self) -> int:
+        """Resolve an aborted per-tensor one-pass hand-off (include/iwq.h, nan_flag bit 1): the launch
+        wrote nothing -- its workgroups were not all resident, e.g. another stream's kernel held CUs
+        -- so the input is untouched, out of place and in place alike, and the same call on the
+        two-kernel form rewrites every output; its flag replaces this one.  Returns the final flag
+        word (one device sync); raises if the outputs are invalid (bit 2)."""
         v = int(self.nan_flag.item())
         if v & 2 and self.retry is not None:
-            # include/iwq.h: the per-tensor one-pass hand-off timed out (its workgroups were not all
-            # resident, e.g. another stream's kernel held CUs).  Out of place the input is untouched,
-            # so the same call on the two-kernel form rewrites every output; its flag replaces this one.
             self.nan_flag = self.retry()
             self.retry = None
             self.retried = True
             v = int(self.nan_flag.item())
-        if v & 2:  # in place: the input may already be partly overwritten
-            raise RuntimeError("iwq: per-tensor one-pass kernel timed out waiting for its workgroups "
-                               "(not all resident); outputs invalid")
-        return v != 0
+        if v & 6:
+            raise RuntimeError("iwq: per-tensor one-pass kernel could not complete its in-launch hand-off "
+                               "(workgroups not all resident); outputs invalid")
+        return v
 
 
 class _FlagPool:
@@ -155,8 +161,8 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
         wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         st = call(ws, wsb)
-        if group == -1 and (out is None or out.data_ptr() != w.data_ptr()):
-            def retry():  # the one-pass hand-off timed out (QuantResult.has_nan): same call on the pair
+        if group == -1 and w.dtype == torch.float16 and quant_dim == 0:  # where the one-pass kernel runs
+            def retry():  # the one-pass hand-off aborted (QuantResult.settle): same call on the pair
                 flag2 = torch.zeros(1, dtype=torch.int32, device=dev)
                 with L.on_device(dev):
                     st2 = lib.iwq_quantize_minmax(

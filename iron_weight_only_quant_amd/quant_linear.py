@@ -139,6 +139,10 @@ class QuantLinear(nn.Module):
             res = kernels.quantize_minmax(w, self.w_bit, self.w_group_size, bool(self.symmetric), self.quant_dim,
                                           out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None,
                                           want_codes=self.keep_codes and self.w_bit <= 8)
+            if res.retry is not None:
+                # per-tensor one-pass kernel: an aborted in-launch hand-off (another kernel holding
+                # CUs) wrote nothing; re-run on the two-kernel form (the reference never fails here)
+                res.settle()
             if res.out is not w:
                 w.copy_(res.out)
             self._set_int_result(res.scales, res.zeros, res.codes)

@@ -100,11 +100,26 @@ def _flatten(res: ShardResult) -> torch.Tensor:
     return torch.cat([p.to(parts[0].device) for p in parts])
 
 
+def n_groups(rows: int, cols: int, group: int) -> int:
+    """Parameter count G of one [rows, cols] weight (quant_dim 0, the sharded path's layout):
+    group > 0 -> rows*cols/group, -1 (per-tensor) -> 1, -2 (per-channel) -> rows
+    (quant_linear.py:896-906; kernels.group_geometry without the torch dependency)."""
+    if group > 0:
+        if cols % group:
+            raise ValueError(f"group {group} does not divide {cols} columns")
+        return rows * cols // group
+    if group == -1:
+        return 1
+    if group == -2:
+        return rows
+    raise ValueError("Invalid w_group_size")
+
+
 def packed_nbytes(shape: Tuple[int, int], n_bits: int, group: int, symmetric: bool, esz: int = 2) -> int:
     """Bytes of one weight's packed result in the gather layout: codes, scales[, zeros]."""
     rows, cols = shape
     ncode = rows * (cols // 2) if n_bits <= 4 else rows * cols
-    G = rows * cols // group
+    G = n_groups(rows, cols, group)
     return ncode + G * esz * (1 if symmetric else 2)
 
 
@@ -132,6 +147,12 @@ def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bi
     if staged:
         flat = flat.cpu()
     dev = flat.device
+    # point-to-point peers are GLOBAL ranks, also inside a sub-group
+    peer = (lambda r: r) if pg is None else (lambda r: dist.get_global_rank(pg, r))
+    if any(sz == 0 for sz in sizes[1:]):
+        # a rank with an empty bin posts no operation; batch_isend_irecv must not be the group's
+        # first collective then (RCCL/NCCL: every rank joins the first one)
+        dist.barrier(group=pg)
     outs = [None] * world
     if rank == 0:
         outs[0] = flat
@@ -139,9 +160,9 @@ def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bi
         for r in range(1, world):
             outs[r] = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
             if sizes[r]:
-                ops.append(dist.P2POp(dist.irecv, outs[r], r, group=pg))
+                ops.append(dist.P2POp(dist.irecv, outs[r], peer(r), group=pg))
     else:
-        ops = [dist.P2POp(dist.isend, flat, 0, group=pg)] if sizes[rank] else []
+        ops = [dist.P2POp(dist.isend, flat, peer(0), group=pg)] if sizes[rank] else []
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -157,7 +178,7 @@ def gather_to_rank0(res: ShardResult, shapes: Dict[str, Tuple[int, int]], all_bi
         for name in sorted(all_bins_names[r]):
             rows, cols = shapes[name]
             ncode = rows * (cols // 2) if n_bits <= 4 else rows * cols
-            G = rows * cols // group
+            G = n_groups(rows, cols, group)
             codes = data[off: off + ncode].clone()
             off += ncode
             scales = data[off: off + G * esz].clone().view(dtype)
@@ -198,12 +219,13 @@ def scatter_from_rank0(send_flats: Optional[List[torch.Tensor]], recv_flat: Opti
     staged = dist.get_backend(pg) == "gloo" and any(
         t is not None and t.is_cuda for t in ([recv_flat] + list(send_flats or [])))
     host = (lambda t: t.cpu()) if staged else (lambda t: t)
+    peer = (lambda r: r) if pg is None else (lambda r: dist.get_global_rank(pg, r))  # global ranks
     if rank == 0:
-        ops = [dist.P2POp(dist.isend, host(send_flats[r]), r, group=pg) for r in range(1, world)]
+        ops = [dist.P2POp(dist.isend, host(send_flats[r]), peer(r), group=pg) for r in range(1, world)]
         rbuf = None
     else:
         rbuf = torch.empty(recv_flat.shape, dtype=recv_flat.dtype) if staged else recv_flat
-        ops = [dist.P2POp(dist.irecv, rbuf, 0, group=pg)]
+        ops = [dist.P2POp(dist.irecv, rbuf, peer(0), group=pg)]
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()

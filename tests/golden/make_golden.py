@@ -12,6 +12,8 @@ Produces (committed, data only):
   tests/golden/int_large_70b.json  the same at the four Llama-2-70B Linear shapes (configs[3])
                                    (`--only 70b` regenerates just this file)
   tests/golden/int_large_pt.json   per-tensor (-1) at the 7B shapes (`--only pt`)
+  tests/golden/int_batched.json    quantize_model's batched group modes on a 4-tensor set, fp16 and
+                                   bf16, SHA-256 of every layer's outputs (`--only batched`)
 
 Reference entry points exercised:
   quant_funcs.pseudo_quantize_tensor                  (quant_funcs.py:4-46)
@@ -244,7 +246,49 @@ def large_pt_cases():
     return res
 
 
+# quantize_model's batched launches in every non-headline group mode (per-channel, per-tensor,
+# quant_dim 1, long and non-power-of-two groups) on multi-tensor sets, fp16 AND bf16 (round 4:
+# the batched bf16 modes were compared with the per-layer path only)
+BATCHED_SPECS = {"a": (384, 3072), "b": (256, 1536), "c": (128, 2304), "d": (512, 1536)}
+BATCHED_MODES = ((-2, 0), (-1, 0), (128, 1), (-2, 1), (64, 1), (768, 0), (96, 0))
+BATCHED_BITS = ((4, False), (8, False), (3, True))
+
+
+def batched_inputs(dtype):
+    """{name: [out, in] array}: oracle/synth inputs (seeds 300..), row 3 of "b" constant 0.5."""
+    out = {}
+    for i, (n, shp) in enumerate(sorted(BATCHED_SPECS.items())):
+        x = synth(300 + i, shp, dtype)
+        if n == "b":  # a constant row (range 0 -> clamp 1e-5); bf16 arrays hold the bit patterns
+            x[3] = {"bfloat16": np.uint16(0x3F00), "float16": np.float16(0.5)}[dtype]
+        out[n] = x
+    return out
+
+
+def batched_cases():
+    res = {"generator": "oracle/synth.py (300 + sorted index, shape), row 3 of 'b' = 0.5", "specs": BATCHED_SPECS,
+           "cases": []}
+    for dtype in ("float16", "bfloat16"):
+        ins = batched_inputs(dtype)
+        for n, x in ins.items():
+            res["cases"].append({"dtype": dtype, "name": n, "kind": "input", "sha_input": sha(x)})
+        for g, qd in BATCHED_MODES:
+            for bits, sym in BATCHED_BITS:
+                for n, x in ins.items():
+                    deq, s, z, _ = ref_ql(x, dtype, w_bit=bits, w_group_size=g, symmetric=sym, quant_dim=qd)
+                    res["cases"].append({"dtype": dtype, "name": n, "kind": "ql", "w_bit": bits, "symmetric": sym,
+                                         "w_group_size": g, "quant_dim": qd, "sha_deq": sha(deq),
+                                         "sha_scales": sha(s), "sha_zeros": None if z is None else sha(z)})
+        print("batched", dtype, flush=True)
+    return res
+
+
 if __name__ == "__main__":
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "batched":
+        with open(os.path.join(HERE, "int_batched.json"), "w") as f:
+            json.dump(batched_cases(), f, indent=1)
+        print("batched done", flush=True)
+        sys.exit(0)
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pt":
         with open(os.path.join(HERE, "int_large_pt.json"), "w") as f:
             json.dump(large_pt_cases(), f, indent=1)

@@ -127,8 +127,9 @@ def test_no_cpu_fallback():
 
 
 def test_quant_result_timeout_retry_logic():
-    """QuantResult.has_nan on nan_flag bit 1 (a timed-out per-tensor hand-off, include/iwq.h): with a
-    retry (out of place) it re-runs once and reports the new flag; without one (in place) it raises."""
+    """QuantResult.has_nan on nan_flag bit 1 (an aborted per-tensor hand-off that wrote nothing,
+    include/iwq.h): with a retry it re-runs once and reports the new flag; without one, or with bit 2
+    (outputs invalid), it raises."""
     from iron_weight_only_quant_amd.kernels import QuantResult
     calls = []
 
@@ -141,11 +142,14 @@ def test_quant_result_timeout_retry_logic():
     r = QuantResult(None, None, None, None, torch.tensor([3], dtype=torch.int32), lambda: retry(1))
     assert r.has_nan() and r.retried  # the re-run's own NaN bit
     r = QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32), lambda: retry(2))
-    with pytest.raises(RuntimeError, match="timed out"):
-        r.has_nan()  # the re-run timed out too
+    with pytest.raises(RuntimeError, match="hand-off"):
+        r.has_nan()  # the re-run aborted too
     r = QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32))
-    with pytest.raises(RuntimeError, match="timed out"):
+    with pytest.raises(RuntimeError, match="hand-off"):
         r.has_nan()
+    r = QuantResult(None, None, None, None, torch.tensor([4], dtype=torch.int32), lambda: retry(0))
+    with pytest.raises(RuntimeError, match="invalid"):
+        r.has_nan()  # a launch that went ahead without one workgroup: no retry can help
     assert not QuantResult(None, None, None, None, torch.tensor([0], dtype=torch.int32)).has_nan()
 
 
@@ -309,12 +313,12 @@ def test_host_abi_under_asan_ubsan():
 
 
 def test_quant_result_timeout_bit_raises():
-    """include/iwq.h nan_flag bit 1 (the per-tensor one-pass hand-off timed out) is an error, not a NaN."""
+    """include/iwq.h nan_flag bit 1 (the per-tensor one-pass hand-off aborted) is an error, not a NaN."""
     from iron_weight_only_quant_amd.kernels import QuantResult
     ok = QuantResult(None, None, None, None, torch.tensor([0], dtype=torch.int32))
     nan = QuantResult(None, None, None, None, torch.tensor([1], dtype=torch.int32))
     assert not ok.has_nan() and nan.has_nan()
-    with pytest.raises(RuntimeError, match="timed out"):
+    with pytest.raises(RuntimeError, match="hand-off"):
         QuantResult(None, None, None, None, torch.tensor([2], dtype=torch.int32)).has_nan()
 
 

@@ -1,7 +1,7 @@
 """Multi-process (gloo, world_size 2, CPU) tests of the layer-sharded path: shard planning, every
-weight owned exactly once, and the single all_gather of packed results reproduces the
-single-process result bit-exactly.  The GPU quantizer is replaced by the oracle here (CPU box);
-on MI355X the same code runs the batched kernel and RCCL."""
+weight owned exactly once, the rooted gather (and the scatter) of packed results reproduces the
+single-process result bit-exactly, and bench.py's multi-rank record.  The GPU quantizer is replaced
+by the oracle here (CPU box); on MI355X the same code runs the batched kernel and RCCL."""
 import os
 import socket
 
@@ -63,6 +63,58 @@ def _worker(rank, world, port, out_q, sym):
             out_q.put({k: (v[0].numpy(), v[1].numpy(), None if v[2] is None else v[2].numpy()) for k, v in got.items()})
     finally:
         dist.destroy_process_group()
+
+
+def _subgroup_worker(rank, world, port, out_q, group):
+    """World 3; the gather runs inside the sub-group of global ranks {1, 2} (its root is global rank
+    1): point-to-point peers must be translated to global ranks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pg = dist.new_group([1, 2])
+        if rank in (1, 2):
+            from oracle.synth import synth
+            shapes = _small_model()
+            bins = shard.plan_shards(shapes, 2)
+            me = rank - 1
+            mine = {shapes[i][0]: torch.from_numpy(synth(700 + i, shapes[i][1], "float16")) for i in bins[me]}
+            res = shard.quantize_shard(mine, 4, group, False, quantize_fn=_oracle_quantize_fn(4, group, False))
+            got = shard.gather_to_rank0(res, dict(shapes), [[shapes[i][0] for i in b] for b in bins], 4, group,
+                                        False, pg=pg)
+            if me == 0:
+                out_q.put({k: (v[0].numpy(), v[1].numpy(), v[2].numpy()) for k, v in got.items()})
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("group", [128, -2])
+def test_gloo_subgroup_gather_uses_global_peers(group):
+    """gather_to_rank0 inside a sub-group that does not start at global rank 0, and with
+    per-channel parameters (G = rows, not rows * cols / group)."""
+    from oracle import iwq_oracle as O
+    from oracle.synth import synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, 3, port, q, group)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shapes = _small_model()
+    assert set(got) == {n for n, _ in shapes}
+    for i, (n, shp) in enumerate(shapes):
+        r = O.quantlinear_int(synth(700 + i, shp, "float16"), w_bit=4, w_group_size=group, symmetric=False)
+        codes, scales, zeros = got[n]
+        assert np.array_equal(codes, O.pack_codes(r.codes, 4).reshape(-1))
+        assert np.array_equal(scales.view(np.uint16), r.scales.reshape(-1).view(np.uint16))
+        assert np.array_equal(zeros.view(np.uint16), r.zeros.reshape(-1).view(np.uint16))
+    assert shard.packed_nbytes((64, 256), 4, -2, False) == 64 * 128 + 64 * 4
+    assert shard.packed_nbytes((64, 256), 4, -1, True) == 64 * 128 + 2
 
 
 def _free_port():
@@ -169,6 +221,15 @@ def test_bench_gpus2_spawns_ranks_and_rooted_gather_moves_each_byte_once():
     shapes = shard.model_linear_shapes("opt-125m")
     assert sum(per_rank) == sum(shard.packed_nbytes(s, 4, 128, False) for _, s in shapes)
     assert rec["gather_sent_bytes"] == per_rank[1] == rec["gather_recv_bytes"]
+    # the N = 2 record is complete for the driver's scaling runs: ranks, devices, the roofline over
+    # ranks (slowest rank's kernel time, every rank's fraction) and the CPU baseline on rank 0
+    assert rec["ranks"] == 2 and "n_devices" in rec
+    roof = rec["roofline"]
+    assert roof["kernel_ms"] == 1.25 and roof["kernel_ms_basis"] == "max over ranks"
+    assert [p["rank"] for p in roof["per_rank"]] == [0, 1]
+    assert roof["per_rank"][0]["kernel_ms"] == 1.0 and roof["frac"] > 0
+    cpu = rec["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port" and "OPT-125M" in cpu["sample"]
 
 
 def test_bench_world_size_must_match_gpus():

@@ -529,6 +529,9 @@ def test_fp4_grid_golden(K, FPD, flags):
             out = quantize_fp16_to_fp4_e1m2(x, group_size=g, per_tensor=pt)
             assert tuple(out.shape) == exp.shape
             assert bits_equal(to_np(out), exp, nan_equal=True)
+            # the reference ignores return_scales (fp4_quantize_cpu.py:47, :72): the same tensor back
+            out2 = quantize_fp16_to_fp4_e1m2(x, group_size=g, per_tensor=pt, return_scales=True)
+            assert isinstance(out2, torch.Tensor) and bits_equal(to_np(out2), exp, nan_equal=True)
 
 
 def test_fp_large_sha(K, FPD):
@@ -771,8 +774,8 @@ def test_per_tensor_fast_path(K, dtype):
     for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
         # + pair variants 1 (non-temporal), 3 (apply walks backwards), 4 / 5 (apply unrolled), 6 (the
-        # pair forced), one-pass variants 7 (NV vectors per thread) and 8 (per-launch tags, no memset)
-        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4, 5, 6, 7, 8)]:
+        # pair forced), one-pass variant 7 (NV vectors per thread)
+        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4, 5, 6, 7)]:
             r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
             assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
             assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)
@@ -786,23 +789,49 @@ def test_per_tensor_fast_path(K, dtype):
 
 
 def test_per_tensor_onepass_timeout_retry(K):
-    """A one-pass hand-off that times out (test-only variant 9: the granule sweep gives up at once,
-    as it would with workgroups held off the CUs by another stream) sets nan_flag bit 1; out of place
-    has_nan() re-runs the call on the two-kernel form into the same outputs (bit-exact vs the oracle),
-    in place (input possibly overwritten) it raises."""
+    """A one-pass hand-off that gives up (test-only variant 9: every granule sweep gives up at once,
+    as it would with workgroups held off the CUs by another stream) ABORTS the launch through the
+    consensus word: nan_flag bit 1, and NOT ONE output byte written.  has_nan() then re-runs the call
+    on the two-kernel form into the same outputs -- out of place and IN PLACE (the input is untouched)
+    -- bit-exact vs the oracle.  QuantLinear(w_group_size=-1) settles the same way."""
     x = synth(56, (1536, 2048), "float16")
     exp = O.quantlinear_int(x, 4, -1, False, 0, "float16")
+    # out of place
     r = K.quantize_minmax(to_dev(x, "float16"), 4, -1, False, 0, want_codes=True, flags=K.gemm_variant_flags(9))
+    assert int(r.nan_flag.item()) & 2
     assert not r.has_nan()
     assert r.retried
     assert bits_equal(to_np(r.out), exp.dequant)
     assert bits_equal(to_np(r.scales), exp.scales.reshape(-1))
     assert bits_equal(to_np(r.zeros), exp.zeros.reshape(-1))
     assert np.array_equal(r.codes.cpu().numpy().reshape(-1), O.pack_codes(exp.codes, 4).reshape(-1))
+    # in place: the aborted launch leaves the weight (and the poisoned outputs) untouched
     xi = to_dev(x, "float16")
-    r = K.quantize_minmax(xi, 4, -1, False, 0, out=xi, flags=K.gemm_variant_flags(9))
-    with pytest.raises(RuntimeError, match="timed out"):
-        r.has_nan()
+    r = K.quantize_minmax(xi, 4, -1, False, 0, out=xi, want_codes=True, flags=K.gemm_variant_flags(9))
+    r.scales.fill_(7.0)
+    r.codes.fill_(0xAB)
+    torch.cuda.synchronize()
+    flag = int(r.nan_flag.item())
+    assert flag & 2 and not flag & 4, flag
+    assert bits_equal(to_np(xi), x), "aborted one-pass launch wrote into the weight"
+    assert bool((r.codes == 0xAB).all()) and bool((r.scales == 7.0).all())
+    assert not r.has_nan()
+    assert r.retried
+    assert bits_equal(to_np(xi), exp.dequant)
+    assert bits_equal(to_np(r.scales), exp.scales.reshape(-1))
+    assert np.array_equal(r.codes.cpu().numpy().reshape(-1), O.pack_codes(exp.codes, 4).reshape(-1))
+    # QuantLinear's in-place per-tensor branch takes the retry too
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    lin = torch.nn.Linear(2048, 1536, bias=False).half().cuda()
+    lin.weight.data.copy_(to_dev(x, "float16"))
+    orig = K.quantize_minmax
+    K.quantize_minmax = lambda *a, **kw: orig(*a, **{**kw, "flags": K.gemm_variant_flags(9)})
+    try:
+        q = QuantLinear.from_linear(lin, w_bit=4, w_group_size=-1, symmetric=False)
+    finally:
+        K.quantize_minmax = orig
+    assert bits_equal(to_np(q.weight.data), exp.dequant)
+    assert bits_equal(to_np(q.scales.view(-1)), exp.scales.reshape(-1))
 
 
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])

@@ -106,3 +106,63 @@ def test_quantize_model_batched_all_group_modes(mode, bits, sym, dtype):
                                     quant_dim=qd)
             assert bits_equal(a.weight.data.cpu().numpy(), ref.dequant), n
             assert bits_equal(a.scales.cpu().numpy(), ref.scales), n
+
+
+_BATCHED = None
+
+
+def _batched_golden():
+    global _BATCHED
+    if _BATCHED is None:
+        import json
+        import os
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "int_batched.json")) as f:
+            _BATCHED = json.load(f)
+    return _BATCHED
+
+
+@pytest.mark.parametrize("mode", [(-2, 0), (-1, 0), (128, 1), (-2, 1), (64, 1), (768, 0), (96, 0)])
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_quantize_model_batched_vs_reference_fixtures(mode, dtype):
+    """quantize_model's batched launch(es) in every non-headline group mode, fp16 AND bf16, against
+    the REFERENCE's own QuantLinear.from_linear outputs on the same inputs (tests/golden/
+    int_batched.json, made by make_golden.py --only batched: SHA-256 of every layer's weight, scales
+    and zeros) -- not only against the per-layer path."""
+    import hashlib
+
+    from oracle.synth import synth
+    from iron_weight_only_quant_amd.quant_wrapper import quantize_model
+    gold = _batched_golden()
+    group, qd = mode
+    td = {"float16": torch.float16, "bfloat16": torch.bfloat16}[dtype]
+    specs, originals = {}, {}
+    for i, (n, (o, k)) in enumerate(sorted(gold["specs"].items())):
+        x = synth(300 + i, (o, k), dtype)
+        if n == "b":
+            x[3] = {"bfloat16": np.uint16(0x3F00), "float16": np.float16(0.5)}[dtype]
+        sha_in = [c["sha_input"] for c in gold["cases"] if c["kind"] == "input" and c["dtype"] == dtype
+                  and c["name"] == n][0]
+        assert hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest() == sha_in, n
+        t = torch.from_numpy(x.view(np.int16)).view(torch.bfloat16) if dtype == "bfloat16" else torch.from_numpy(x)
+        specs[n] = (o, k, False)
+        originals[n] = t
+
+    def h(t):
+        t = t.detach().contiguous().cpu()
+        if t.dtype == torch.bfloat16:
+            t = t.view(torch.int16)
+        return hashlib.sha256(t.numpy().tobytes()).hexdigest()
+    for bits, sym in ((4, False), (8, False), (3, True)):
+        m = _model(specs, originals, td)
+        quantize_model(m, _args(w_bit=bits, w_group_size=group, w_symmetric=sym, quant_dim=qd), batched=True,
+                       verbose=False)
+        for n in specs:
+            ref = [c for c in gold["cases"] if c["kind"] == "ql" and c["dtype"] == dtype and c["name"] == n
+                   and c["w_bit"] == bits and c["symmetric"] == sym and c["w_group_size"] == group
+                   and c["quant_dim"] == qd][0]
+            q = getattr(m, n)
+            assert h(q.weight.data) == ref["sha_deq"], (n, bits, sym)
+            assert h(q.scales) == ref["sha_scales"], (n, bits, sym)
+            assert (q.zeros is None) == (ref["sha_zeros"] is None)
+            if q.zeros is not None:
+                assert h(q.zeros) == ref["sha_zeros"], (n, bits, sym)
