@@ -7,8 +7,9 @@ CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
 SOURCES = ["iwq_minmax.hip", "iwq_batched.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
-           "iwq_fpunpack.hip", "iwq_codes.hip"]
-DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h"]
+           "iwq_fpunpack.hip", "iwq_codes.hip", "iwq_prefill16.hip", "iwq_fpdt.hip"]
+DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h",
+                  "iwq_fp_tables_dt.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # Numerics: no FMA contraction, IEEE fp32 division, denormals preserved.
 # --offload-compress: the gfx950 code objects are stored compressed in the .so (35 -> ~9 MiB; the HIP

@@ -24,6 +24,15 @@ using iwq::seg::SegArgs;
 using iwq::seg::SEG_RUN;
 using iwq::seg::seg_locate;
 
+namespace iwq {
+// iwq_fpdt.hip: the same entry points on bf16 / fp32 weights
+int64_t fp_dt_workspace_bytes(int64_t rows, int64_t cols, int64_t G, bool double_approx);
+int run_fp_dt(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
+              int mant_bits, int64_t group, int symmetric, int quant_dim, void* out, int64_t ld_out, void* codes_out,
+              void* scales, void* zeros, void* ws, int64_t ws_bytes, uint32_t* nan_flag, void* stream, int hs,
+              int hf, int tp);
+}  // namespace iwq
+
 namespace {
 
 #define IWQ_HIP_FP(call)                \
@@ -1006,6 +1015,12 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
            int mant_bits, int64_t group, int symmetric, int quant_dim, void* out, int64_t ld_out, void* codes_out,
            void* scales, void* zeros, void* ws, int64_t ws_bytes, uint32_t* nan_flag, unsigned flags,
            void* stream, int hs = 0, int hf = 0, int tp = 0, const void* lut = nullptr) {
+  if (dtype == IWQ_BF16 || dtype == IWQ_F32) {  // iwq_fpdt.hip (the E2M1 grid is fp16-only, as its reference)
+    if (codec != CODEC_FP && codec != CODEC_APX) return IWQ_ERR_DTYPE;
+    return iwq::run_fp_dt(codec == CODEC_APX ? 1 : 0, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group,
+                          symmetric, quant_dim, out, ld_out, codes_out, scales, zeros, ws, ws_bytes, nan_flag, stream,
+                          hs, hf, tp);
+  }
   if (dtype != IWQ_F16) return IWQ_ERR_DTYPE;
   if (!w) return IWQ_ERR_ARG;
   if (rows <= 0 || cols <= 0 || ld_w < cols || (out && ld_out < cols)) return IWQ_ERR_SHAPE;
@@ -1156,7 +1171,10 @@ int64_t iwq_approx_workspace_bytes(int64_t rows, int64_t cols, int exp_bits, int
   if (rows <= 0 || cols <= 0 || group <= 0) return 0;
   const int64_t G = rows * cols / group;
   (void)quant_dim;
-  return round256(8 * G) + (double_approx ? apx_codes_bytes(rows, cols, exp_bits, mant_bits) : 0);
+  // (covers bf16 / fp32 weights too: iwq_fpdt.hip keeps byte codes and fp32 scales for the quads)
+  const int64_t f16 = round256(8 * G) + (double_approx ? apx_codes_bytes(rows, cols, exp_bits, mant_bits) : 0);
+  const int64_t dt = iwq::fp_dt_workspace_bytes(rows, cols, G, double_approx != 0);
+  return f16 > dt ? f16 : dt;
 }
 
 int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_t ld_w, int dtype, int exp_bits,
@@ -1166,6 +1184,10 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
                                uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
   if (group <= 0) return IWQ_ERR_GROUP_MODE;  // approximate needs w_group_size > 0 (ValueError)
   if (!out_deq || !out_scales) return IWQ_ERR_ARG;
+  if (double_approx && (dtype == IWQ_BF16 || dtype == IWQ_F32))  // iwq_fpdt.hip
+    return iwq::run_fp_dt(2, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
+                          nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, stream, hi_align_start,
+                          hi_align_exp_field, tail_pad_bits);
   if (!double_approx)
     return run_fp(CODEC_APX, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
                   nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, flags, stream, hi_align_start,

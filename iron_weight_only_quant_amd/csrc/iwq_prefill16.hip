@@ -1,0 +1,385 @@
+// iwq_prefill16.hip — the prefill (large M) fused dequant -> GEMM of iwq_prefill.hip's 74
+// (k_w4a16_b32w) on the 16x16x32 f16 MFMA instead of 32x32x16.
+//
+// Replaces QuantLinear.forward = F.linear(x, W_deq, b) (quant_linear.py:960-972) for weights held
+// packed (include/iwq.h layout), per channel: y = RN16(s * sum_k x (q - z) + b).
+//
+// Why a second MFMA shape: both shapes do the same FLOP per cycle, but under load the chip holds a
+// higher clock on the 16x16x32 loop (MI355X_MICROARCH.md 'DVFS give-back' item 7: ~1.12-1.15x the
+// FLOP/s on random data with every operand re-read from LDS; hipBLASLt's own kernel for these
+// shapes is MT256x256x64_MI16x16).  74's structure is kept: 256 x 256 tile per 512-thread workgroup,
+// 8 waves as 1 (M) x 8 (N) so each weight is dequantized once per workgroup; a wave owns 256 rows x
+// 32 columns = 16 x 2 tiles of 16x16; K-steps of 64 staged by LDS-DMA into a ring; one raw
+// s_barrier per K-step placed early (its wait covers only reads that are already in registers).
+//
+// k order: MFMA slice s (0, 1) of a K-step gives lane group g = lane >> 4 the logical
+// k = 16 g + 8 s + [0, 8) -- the same permutation on both operands -- so a lane's codes for the whole
+// K-step are 8 contiguous bytes of its column (one ds_read_b64 per 16-column tile) and its A fragment
+// of slice s is one 16-B piece of its X row.
+// LDS images (the DMA writes lane-linearly; swizzles are applied to the per-lane SOURCE address):
+//   X rows of 128 B, 16-B chunk c of row r at c ^ h(r), h(r) = ((r >> 1) & 1) | (((r >> 3) & 1) * 6):
+//     a ds_read_b128 lane group reads 16 rows, 8 of them at chunk c and 8 at chunk c ^ 2 (lanes
+//     0-3 / 12-15 vs 4-11 of a 16-row tile), and h makes the 16 (row, chunk) slots distinct.
+//   codes: columns of 32 B, 16-B chunk c of column n at c ^ ((n >> 3) & 1) (74's image); the b64
+//     read of unit g (bytes 8 g .. 8 g + 7) hits 32 distinct dword pairs per 32 lanes.
+// STAGGER (4-slot ring, 160 KiB): waves 4-7 run half a K-step (16 MFMA pairs) behind waves 0-3 --
+// their barrier sits between pairs 7 and 8 of slice 0, the others' between pairs 7 and 8 of slice 1
+// -- so the two waves sharing a SIMD do not reach their DMA issue, code reads and barrier together
+// (MI355X_MICROARCH.md 'Two waves per SIMD' item 9).  A slot is then refilled one barrier later
+// (after every wave has left it), hence the fourth slot.
+#include "iwq_common.cuh"
+#include "iwq_prefill.h"
+
+namespace iwq {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int TM = 256, TN = 256, TK = 64, THR = 512;
+constexpr int XS = TM * TK * 2;  // X bytes per stage (32 KiB)
+constexpr int CS = TN * TK / 2;  // code bytes per stage (8 KiB)
+constexpr int STAGE = XS + CS;
+
+__device__ __forceinline__ int xh(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) * 6); }
+__device__ __forceinline__ int cswz(int n) { return (n >> 3) & 1; }
+
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
+  return r;
+}
+
+__device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
+  const int64_t xcd = bid % 8, i = bid / 8;
+  const int64_t q = nblocks / 8, r = nblocks % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+}
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int OFF>
+__device__ __forceinline__ h8 lds_rd(uint32_t addr) {
+  h8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ u32x2 lds_rd2(uint32_t addr) {
+  u32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+// re-defines v after its wait (see iwq_prefill.hip: keeps post-wait uses below the wait)
+template <class T>
+__device__ __forceinline__ void landed(T& v) {
+  asm volatile("" : "+v"(v));
+}
+
+#define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
+
+// NIB: codes in the NIB layout (iwq_nib_codes: nibble p of a code dword holds k offset
+// (0, 2, 4, 6, 1, 3, 5, 7)[p]) -- 9 instead of 12 VALU per 8 weights, the same (q - z) values, so
+// the same bits as the row-major form
+// LAG (A/B): the staggered waves' barrier sits 16 MFMA pairs (half a K-step) or 8 pairs before the
+// others'; PRIO (A/B): static s_setprio 1 for waves 4-7 (1) or 0-3 (2) (cdna_hip_programming.md T5)
+template <bool STAGGER, bool NIB = false, int LAG = 16, int PRIO = 0>
+__global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
+  static_assert(LAG == 16 || LAG == 8, "barrier between pairs 7/8 or after pair 15 of slice 0");
+  constexpr int NST = STAGGER ? 4 : 3;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NST * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool late = STAGGER && wid >= 4;  // wave-uniform: waves 4-7 run half a K-step behind
+  const int r16 = lane & 15, g = lane >> 4;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int64_t crow = a.K / 2;
+  const int nk = a.K / TK;
+
+  // DMA sources: X rows (wid * 4 + i) * 8 + lane / 8, 16-B chunk lane % 8 from chunk (lane % 8) ^ h;
+  // codes: column wid * 32 + lane / 2, chunk lane % 2 from chunk (lane % 2) ^ cswz
+  const _Float16* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wid * 4 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3);
+  }
+  const int ccol = wid * 32 + (lane >> 1);
+  const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * STAGE;
+    if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
+    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+  };
+  auto issue = [&](int kt, int stg) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) issue1(kt, stg, i);
+  };
+
+  // this lane's two columns (16-column tiles 0, 1 of the wave) and their parameters
+  const int col0 = n0 + wid * 32 + r16;
+  float sfl[2];
+  h2 zz[2], zl[2], zh[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = col0 + 16 * nt;
+    sfl[nt] = (float)gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  // LDS byte addresses: A fragment (stage st, slice s, tile mt) = la[s] + st * STAGE + 2048 mt;
+  // codes of tile nt = lc + st * STAGE + 512 nt
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
+  const int ccl = wid * 32 + r16;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+
+  // weight pair j (k offsets 2j, 2j + 1) of code dword w, tile nt: (q - z) exactly (3 VALU; NIB:
+  // 2, plus one shift per dword for pairs 2 and 3)
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    if constexpr (NIB) {
+      const uint32_t t = j >= 2 ? w >> 8 : w;
+      return (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+  };
+  auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
+
+  f4 acc[16][2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 af[8];
+  h8 b0, b1;    // B fragments of the running slice (tiles 0, 1)
+  u32x2 wc0, wc1;  // the running K-step's code dwords (tile 0, 1): .x slice 0, .y slice 1
+
+#define IWQ_RD(MT, ADDR) af[(MT) & 7] = lds_rd<((MT) & 15) * 2048>(ADDR)
+#define IWQ_MF2(MT)                                                                        \
+  acc[MT][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], b0, acc[MT][0], 0, 0, 0); \
+  acc[MT][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], b1, acc[MT][1], 0, 0, 0)
+  // pair MT of a slice: its two MFMAs, then the rolling read 8 pairs ahead (READ), VALU work (DQ)
+#define IWQ_PAIR(MT, WAIT, READ, DQ) \
+  {                                  \
+    if (WAIT) IWQ_LGKM(7);           \
+    IWQ_PIN();                       \
+    IWQ_MF2(MT);                     \
+    READ;                            \
+    DQ;                              \
+    IWQ_PIN();                       \
+  }
+
+  // slice 0 of a K-step (stage offset SO): rolling reads of frags 8..15 of slice 0 and 0..7 of
+  // slice 1; slice 1's B fragments (the same code dwords' .y) dequantized on the way, one weight pair
+  // per MFMA pair; MID runs between pairs 7 and 8, END after pair 15 (the staggered waves' barrier)
+#define IWQ_SLICE0(SO, MID, END)                                                          \
+  {                                                                                       \
+    const uint32_t a0 = la[0] + (SO), a1 = la[1] + (SO);                                  \
+    h2 p[8];                                                                              \
+    IWQ_PAIR(0, true, IWQ_RD(8, a0), p[0] = dqp(wc0.y, 0, 0));                            \
+    IWQ_PAIR(1, true, IWQ_RD(9, a0), p[1] = dqp(wc0.y, 1, 0));                            \
+    IWQ_PAIR(2, true, IWQ_RD(10, a0), p[2] = dqp(wc0.y, 2, 0));                           \
+    IWQ_PAIR(3, true, IWQ_RD(11, a0), p[3] = dqp(wc0.y, 3, 0));                           \
+    IWQ_PAIR(4, true, IWQ_RD(12, a0), p[4] = dqp(wc1.y, 0, 1));                           \
+    IWQ_PAIR(5, true, IWQ_RD(13, a0), p[5] = dqp(wc1.y, 1, 1));                           \
+    IWQ_PAIR(6, true, IWQ_RD(14, a0), p[6] = dqp(wc1.y, 2, 1));                           \
+    IWQ_PAIR(7, true, IWQ_RD(15, a0), p[7] = dqp(wc1.y, 3, 1));                           \
+    MID;                                                                                  \
+    IWQ_PAIR(8, true, IWQ_RD(0, a1), );                                                   \
+    IWQ_PAIR(9, true, IWQ_RD(1, a1), );                                                   \
+    IWQ_PAIR(10, true, IWQ_RD(2, a1), );                                                  \
+    IWQ_PAIR(11, true, IWQ_RD(3, a1), );                                                  \
+    IWQ_PAIR(12, true, IWQ_RD(4, a1), );                                                  \
+    IWQ_PAIR(13, true, IWQ_RD(5, a1), );                                                  \
+    IWQ_PAIR(14, true, IWQ_RD(6, a1), );                                                  \
+    IWQ_PAIR(15, true, IWQ_RD(7, a1), );                                                  \
+    END;                                                                                  \
+    b0 = frag(p);                                                                         \
+    b1 = frag(p + 4);                                                                     \
+  }
+
+  // prologue: stages 0 .. NST-1 (K-steps clamped to nk - 1: re-loads nobody reads again)
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  issue(nk > 2 ? 2 : nk - 1, 2);  // (STAGGER: slot 3 receives K-step 3 after the first barrier)
+  IWQ_PIN();
+  wc0 = lds_rd2<0>(lc);
+  wc1 = lds_rd2<512>(lc);
+  IWQ_RD(0, la[0]); IWQ_RD(1, la[0]); IWQ_RD(2, la[0]); IWQ_RD(3, la[0]);
+  IWQ_RD(4, la[0]); IWQ_RD(5, la[0]); IWQ_RD(6, la[0]); IWQ_RD(7, la[0]);
+  IWQ_LGKM(0);
+  landed(wc0);
+  landed(wc1);
+  IWQ_PIN();
+  {
+    h2 p[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[j] = dqp(wc0.x, j, 0);
+      p[4 + j] = dqp(wc1.x, j, 1);
+    }
+    b0 = frag(p);
+    b1 = frag(p + 4);
+  }
+
+  // vmcnt at a barrier (both rings): this wave's pieces of the stage being published have landed;
+  // the next K-step's 5 pieces (issued after the previous barrier) may still fly
+  constexpr int VM_AHEAD = 5;
+  if constexpr (PRIO == 1) {
+    if (late) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (PRIO == 2) {
+    if (STAGGER && !late) __builtin_amdgcn_s_setprio(1);
+  }
+  // the last K-step is peeled (a branch in the body made the compiler keep two register images)
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NST) * STAGE);
+    const uint32_t sn = (uint32_t)(((kt + 1) % NST) * STAGE);
+    // the slot refilled in this K-step and the K-step it receives (clamped: re-loads nobody reads)
+    const int sd = STAGGER ? (kt + NST - 1) % NST : kt % NST;
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
+    // waves 4-7 (STAGGER): their barrier between pairs 7 and 8 of slice 0, 16 MFMA pairs before the
+    // others' -- stage kt + 1 published; the slot a DMA may refill before the next barrier holds
+    // stage kt - 1, whose reads this wave retired in K-step kt - 1
+    IWQ_SLICE0(so, if (LAG == 16 && late) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+      __builtin_amdgcn_s_barrier();
+    }, if (LAG == 8 && late) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+      __builtin_amdgcn_s_barrier();
+    })
+    // slice 1: pairs 0..7 read frags 8..15 of slice 1; pairs 8..15 read the next K-step's slice-0
+    // frags 0..7 (after the barrier that publishes it), its codes, and issue this K-step's refill
+    const uint32_t a1 = la[1] + so;
+    IWQ_PAIR(0, true, IWQ_RD(8, a1), );
+    IWQ_PAIR(1, true, IWQ_RD(9, a1), );
+    IWQ_PAIR(2, true, IWQ_RD(10, a1), );
+    IWQ_PAIR(3, true, IWQ_RD(11, a1), );
+    IWQ_PAIR(4, true, IWQ_RD(12, a1), );
+    IWQ_PAIR(5, true, IWQ_RD(13, a1), );
+    IWQ_PAIR(6, true, IWQ_RD(14, a1), );
+    IWQ_PAIR(7, true, IWQ_RD(15, a1), );
+    if (!late) {
+      // waves 0-3 (all waves without STAGGER): stage kt + 1 landed (this wave's part), and -- 3-slot
+      // ring -- every read of stage kt retired (its slot is refilled right after)
+      if constexpr (STAGGER) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(VM_AHEAD) : "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (STAGGER) IWQ_LGKM(0);  // frags 8..15 of slice 1 in registers
+    IWQ_PIN();
+    // codes of stage kt + 1 (oldest of what follows), then the rolling reads of its slice 0
+    u32x2 wn0 = lds_rd2<0>(lc + sn);
+    u32x2 wn1 = lds_rd2<512>(lc + sn);
+    const uint32_t na = la[0] + sn;
+    IWQ_PAIR(8, false, IWQ_RD(0, na), issue1(kd, sd, 0));
+    IWQ_PAIR(9, false, IWQ_RD(1, na), issue1(kd, sd, 1));
+    IWQ_PAIR(10, false, IWQ_RD(2, na), issue1(kd, sd, 2));
+    IWQ_PAIR(11, false, IWQ_RD(3, na), issue1(kd, sd, 3));
+    IWQ_LGKM(4);  // the code reads (older than the 4 A reads above) landed
+    landed(wn0);
+    landed(wn1);
+    h2 p[8];
+    IWQ_PAIR(12, false, IWQ_RD(4, na), issue1(kd, sd, 4); p[0] = dqp(wn0.x, 0, 0); p[1] = dqp(wn0.x, 1, 0));
+    IWQ_PAIR(13, false, IWQ_RD(5, na), p[2] = dqp(wn0.x, 2, 0); p[3] = dqp(wn0.x, 3, 0));
+    IWQ_PAIR(14, false, IWQ_RD(6, na), p[4] = dqp(wn1.x, 0, 1); p[5] = dqp(wn1.x, 1, 1));
+    IWQ_PAIR(15, false, IWQ_RD(7, na), p[6] = dqp(wn1.x, 2, 1); p[7] = dqp(wn1.x, 3, 1));
+    b0 = frag(p);
+    b1 = frag(p + 4);
+    wc0 = wn0;
+    wc1 = wn1;
+  }
+  {
+    // the last K-step: no next stage, no barrier
+    const uint32_t so = (uint32_t)(((nk - 1) % NST) * STAGE);
+    IWQ_SLICE0(so, , )
+    const uint32_t a1 = la[1] + so;
+    IWQ_PAIR(0, true, IWQ_RD(8, a1), );
+    IWQ_PAIR(1, true, IWQ_RD(9, a1), );
+    IWQ_PAIR(2, true, IWQ_RD(10, a1), );
+    IWQ_PAIR(3, true, IWQ_RD(11, a1), );
+    IWQ_PAIR(4, true, IWQ_RD(12, a1), );
+    IWQ_PAIR(5, true, IWQ_RD(13, a1), );
+    IWQ_PAIR(6, true, IWQ_RD(14, a1), );
+    IWQ_PAIR(7, true, IWQ_RD(15, a1), );
+    IWQ_LGKM(0);
+    IWQ_PIN();
+    IWQ_MF2(8); IWQ_MF2(9); IWQ_MF2(10); IWQ_MF2(11);
+    IWQ_MF2(12); IWQ_MF2(13); IWQ_MF2(14); IWQ_MF2(15);
+  }
+  // no LDS-DMA may still be landing when the workgroup retires (the CU's next workgroup owns the LDS)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_SLICE0
+#undef IWQ_PAIR
+#undef IWQ_MF2
+#undef IWQ_RD
+
+  // epilogue: lane holds rows 16 mt + 4 g + r of columns col0, col0 + 16
+  const float bc0 = a.bias ? (float)gp<_Float16>(a.bias)[col0] : 0.0f;
+  const float bc1 = a.bias ? (float)gp<_Float16>(a.bias)[col0 + 16] : 0.0f;
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;  // row pitch, bytes
+  char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * g) * a.ldy + col0) * 2;
+  const bool full = m0 + TM <= a.M;
+#pragma unroll
+  for (int mt = 0; mt < 16; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = mt * 16 + r;
+      if (full || m0 + rr + 4 * g < a.M) {
+        auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
+        p[0] = (_Float16)(opaque(acc[mt][0][r] * sfl[0]) + bc0);
+        p[16] = (_Float16)(opaque(acc[mt][1][r] * sfl[1]) + bc1);
+      }
+    }
+}
+#undef IWQ_LGKM
+#undef IWQ_PIN
+
+}  // namespace
+
+// 16x16x32 forms of 74 (per channel): variants 150 (3-slot ring), 151 (4-slot ring, waves 4-7
+// staggered half a K-step: the per-channel default since round 4), 152 / 153 the same on NIB codes
+bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr) {
+  return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && gpr == 1;
+}
+
+hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
+  const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
+  const dim3 grid((unsigned)blocks), blk(THR);
+  switch (variant) {
+    case 150: hipLaunchKernelGGL((k_w4a16_b16w<false>), grid, blk, 0, st, a); break;
+    case 152: hipLaunchKernelGGL((k_w4a16_b16w<false, true>), grid, blk, 0, st, a); break;
+    case 153: hipLaunchKernelGGL((k_w4a16_b16w<true, true>), grid, blk, 0, st, a); break;
+    case 154: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 8>), grid, blk, 0, st, a); break;    // A/B
+    case 155: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 1>), grid, blk, 0, st, a); break;
+    case 156: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 2>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace iwq

@@ -214,13 +214,15 @@ def fp_code_nbytes(rows, cols, exp_bits, mant_bits):
 def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symmetric: bool, quant_dim: int = 0,
                 out: Optional[torch.Tensor] = None, want_codes: bool = False, flags: int = 0,
                 use_lut: bool = True) -> QuantResult:
-    """FP4/FP6/FP8 fake quantization of an fp16 2-D weight (QuantLinear FP branches) on the GPU.
-    use_lut: decode through the per-format LDS table (same bits; False = bit-level ALU codec)."""
+    """FP4/FP6/FP8 fake quantization of a 2-D weight (QuantLinear FP branches) on the GPU.
+    fp16 weights: the LDS-table kernels (use_lut; False = bit-level ALU codec, same bits).  bf16 / fp32
+    weights (round 4, iwq_fpdt.hip): every op in the weight's dtype like the reference; scales / zeros
+    come back fp16, as the reference's .half() buffers (quant_linear.py:760-766)."""
     L.require_device(w)
     if w.dim() != 2:
         raise AssertionError("weight must be 2-D")
-    if w.dtype != torch.float16:
-        raise TypeError("FP weight formats are implemented for fp16 weights")
+    if w.dtype not in L.DTYPE_CODE:
+        raise TypeError(f"unsupported dtype {w.dtype}")
     lib = L.load()
     if w.stride(1) != 1 or w.stride(0) < w.shape[1]:
         w = w.contiguous()
@@ -229,16 +231,17 @@ def quantize_fp(w: torch.Tensor, exp_bits: int, mant_bits: int, group: int, symm
     dev = w.device
     if out is None:
         out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
-    scales = torch.empty(G, dtype=w.dtype, device=dev)
-    zeros = None if symmetric else torch.empty(G, dtype=w.dtype, device=dev)
+    scales = torch.empty(G, dtype=torch.float16, device=dev)
+    zeros = None if symmetric else torch.empty(G, dtype=torch.float16, device=dev)
     codes = torch.empty(fp_code_nbytes(rows, cols, exp_bits, mant_bits), dtype=torch.uint8, device=dev) \
         if want_codes else None
     nan_flag = _flags.take(dev)
-    lut = _luts.get(dev, L.IWQ_CODEC_FP, exp_bits, mant_bits) if use_lut else None
+    f16 = w.dtype == torch.float16
+    lut = _luts.get(dev, L.IWQ_CODEC_FP, exp_bits, mant_bits) if (use_lut and f16) else None
 
     def call(ws, wsb):
         with L.on_device(dev):
-            return lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
+            return lib.iwq_quantize_fp_lut(L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(exp_bits),
                                            int(mant_bits), int(group), int(bool(symmetric)), int(quant_dim),
                                            L.ptr(out), out.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                            L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), L.stream_handle(dev),
@@ -260,8 +263,8 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     L.require_device(w)
     if w.dim() != 2:
         raise AssertionError("weight must be 2-D")
-    if w.dtype != torch.float16:
-        raise TypeError("approximate FP formats are implemented for fp16 weights")
+    if w.dtype not in L.DTYPE_CODE:
+        raise TypeError(f"unsupported dtype {w.dtype}")
     if group <= 0:
         raise ValueError("approximate 仅支持分组量化，w_group_size 必须 > 0")
     lib = L.load()
@@ -274,15 +277,16 @@ def quantize_fp_approx(w: torch.Tensor, exp_bits: int, mant_bits: int, group: in
     dev = w.device
     if out is None:
         out = torch.empty((rows, cols), dtype=w.dtype, device=dev)
-    scales = torch.empty(G, dtype=w.dtype, device=dev)
+    scales = torch.empty(G, dtype=torch.float16, device=dev)  # the reference's .half() buffer (:606)
     nan_flag = _flags.take(dev)
     wsb = int(lib.iwq_approx_workspace_bytes(rows, cols, int(exp_bits), int(mant_bits), int(group), int(quant_dim),
                                              int(bool(double_approx))))
     ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
     lut = (_luts.get(dev, L.IWQ_CODEC_APX_DOUBLE if double_approx else L.IWQ_CODEC_APX, exp_bits, mant_bits,
-                     hi_align_start, hi_align_exp_field, tail_pad_bits) if use_lut else None)
+                     hi_align_start, hi_align_exp_field, tail_pad_bits) if (use_lut and w.dtype == torch.float16)
+           else None)
     with L.on_device(dev):
-        st = lib.iwq_quantize_fp_approx_lut(L.ptr(w), rows, cols, w.stride(0), L.IWQ_F16, int(exp_bits),
+        st = lib.iwq_quantize_fp_approx_lut(L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(exp_bits),
                                             int(mant_bits), int(group), int(quant_dim), int(hi_align_start),
                                             int(hi_align_exp_field), int(tail_pad_bits), int(bool(double_approx)),
                                             L.ptr(out), out.stride(0), L.ptr(scales), L.ptr(ws), ws.numel(),

@@ -898,9 +898,10 @@ def test_w4a16_prefill_big_identity(K):
 # element (exact) or in the epilogue (factored), on 32x32x16 or 16x16x32; grouped: one set per shape.
 # The wave layout (60-62: 4 x 2 waves / static priority; 63-64: four waves of 128 x 128) changes
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
+# 150 / 151: 74 on the 16x16x32 MFMA (iwq_prefill16.hip; per channel only -- grouped falls back to 74)
 B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80, 97, 98), (47,),
-               (48,))
-B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80, 98), (47,))
+               (48,), (150, 151, 154, 155, 156))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80, 98, 150, 151, 154, 155, 156), (47,))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
 
@@ -914,7 +915,7 @@ def nib_layout(codes, N, K):
 
 
 # NIB-layout variants: same k order and accumulation order as their row-major twins
-B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45}
+B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45, 152: 150, 153: 151}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -946,7 +947,7 @@ def test_w4a16_prefill_b32(K, M, sym, group):
         if group != -2 and v in (67, 71, 77, 81, 99):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
-        assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)
+        assert torch.equal(y, ys[twin if group == -2 else 45]), (v, twin)  # grouped 152/153: 75 = 45
 
 
 def test_nib_codes_layout(K):
@@ -991,6 +992,9 @@ def test_w4a16_nib_default(K, M, group):
     y74 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(74))
     y75 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(75))
     assert torch.equal(y74, y75)
+    y151 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(151))
+    y153 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(153))
+    assert torch.equal(y151, y153)
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     assert bool(((y1.float() - ref).abs() <= tol).all())
@@ -1188,13 +1192,17 @@ def test_w4a16_prefill_short_k(K, Kd):
     for v in (70, 74, 76, 78, 79, 80):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y45), v
-    for v in (110, 112, 130, 132):  # short-tile splits: 1-3 K-steps per range
+    for v in (110, 112, 130, 132, 150, 151):  # short-tile splits: 1-3 K-steps per range; 16x16x32 forms
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert bool(((y.float() - ref).abs() <= tol).all()), v
     nib = nib_layout(r.codes, N, Kd)
     for v in (71, 75, 77, 81):
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y45), v
+    y150 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(150))
+    for v, cd in ((151, r.codes), (152, nib), (153, nib)):  # the 16x16x32 forms: one set of bits
+        y = K.w4a16_gemm(x, cd, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y150), v
 
 
 MID_VARIANTS = (50, 51, 52, 53, 54, 55)  # k_w4a16_mid: (MT row tiles, CT column tiles) shapes

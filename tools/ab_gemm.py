@@ -27,7 +27,7 @@ def nib_layout(codes, N, K):
     return out.reshape(N, K // 2).contiguous()
 
 
-NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99)
+NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99, 152, 153)
 
 
 def main():

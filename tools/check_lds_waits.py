@@ -1,4 +1,5 @@
-"""ISA lint for the hand-ordered prefill kernels (iwq_prefill.hip: k_w4a16_b32w / b32v / b32s / w4h / w4b).
+"""ISA lint for the hand-ordered prefill kernels (iwq_prefill.hip: k_w4a16_b32w / b32v / b32s / w4h / w4b;
+iwq_prefill16.hip: k_w4a16_b16w).
 
 Those kernels issue their LDS reads and writes as inline asm and count the lgkmcnt waits by hand,
 which the compiler cannot see: a register an asm ds_read fills is only valid once a wait has retired
@@ -6,8 +7,10 @@ that read.  This tool compiles iwq_prefill.hip for gfx950 to assembly (the build
 every such kernel in program order, modelling the LDS queue: ds_read_b128 / ds_write_b128 enter it,
 `s_waitcnt lgkmcnt(n)` retires all but the n newest.  Any instruction that touches a VGPR of a
 still-pending read is reported (a use before the data landed, or an overwrite racing it).
-Straight-line model: branches are ignored, which is exact for these kernels' loop bodies (one basic
-block each) and conservative at block boundaries.
+Control flow: the kernel is cut into basic blocks (labels, s_branch / s_cbranch_*), and the queue at
+a block's entry is the merge of its predecessors' exit queues aligned from the newest entry (what
+`lgkmcnt(n)` keeps), iterated to a fixed point -- exact for straight-line loop bodies and for the
+wave-uniform branches around the staggered barriers of k_w4a16_b16w.
 
 Second check (--store-hazard, every csrc/*.hip): a buffer_store_dwordx3/x4 whose data VGPRs the very
 next instruction overwrites.  ROCm 7.2's LLVM inserts no wait state there when the store carries an
@@ -24,12 +27,13 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "iron_weight_only_quant_amd", "csrc")
-KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v)\w*):", re.M)
+KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v|b16w)\w*):", re.M)
+SOURCES = ("iwq_prefill.hip", "iwq_prefill16.hip")
 
 
-def compile_asm(out):
+def compile_asm(out, src="iwq_prefill.hip"):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-           "--offload-device-only", "-S", os.path.join(CSRC, "iwq_prefill.hip"), "-I", CSRC, "-o", out]
+           "--offload-device-only", "-S", os.path.join(CSRC, src), "-I", CSRC, "-o", out]
     subprocess.run(cmd, check=True, capture_output=True)
 
 
@@ -41,35 +45,92 @@ def vregs(text):
     return regs
 
 
+def _step(pending, t, n, findings):
+    """One instruction: updated queue; appends (n, t) to findings on a hazard."""
+    op = t.split()[0]
+    if op == "s_waitcnt" and "lgkmcnt" in t:
+        keep = int(re.search(r"lgkmcnt\((\d+)\)", t).group(1))
+        return pending[len(pending) - keep:] if keep else []
+    if op.startswith("ds_read"):
+        dst = t.split(None, 1)[1].split(",")[0]
+        if any(p[1] & vregs(t.split(",", 1)[1]) for p in pending):
+            findings.append((n, t))
+        return pending + [("r", vregs(dst))]
+    if op.startswith("ds_write"):
+        if any(p[0] == "r" and p[1] & vregs(t) for p in pending):
+            findings.append((n, t))
+        return pending + [("w", set())]
+    used = vregs(t)
+    if any(p[0] == "r" and p[1] & used for p in pending):
+        findings.append((n, t))
+    return pending
+
+
+def _merge(a, b):
+    """Queues aligned from the newest entry; an entry is a read if either is, registers united."""
+    if a is None:
+        return b
+    la, lb = len(a), len(b)
+    out = []
+    for i in range(max(la, lb), 0, -1):
+        ea = a[la - i] if i <= la else None
+        eb = b[lb - i] if i <= lb else None
+        if ea is None or eb is None:
+            out.append(ea or eb)
+        else:
+            out.append(("r" if "r" in (ea[0], eb[0]) else "w", ea[1] | eb[1]))
+    return out
+
+
 def check_kernel(lines):
-    pending = []  # (kind, vgpr set) in issue order
-    findings = []
+    # basic blocks: (first line, [(n, instruction)], successor labels, falls through)
+    blocks, cur, label_of = [], None, {}
     for n, raw in enumerate(lines):
         t = raw.strip()
-        if not t or t.startswith((";", ".")) or t.endswith(":"):
+        if not t or t.startswith(";") or (t.startswith(".") and not t.endswith(":")):
             continue
+        if t.endswith(":"):
+            if cur is not None:
+                blocks.append(cur)
+            cur = {"label": t[:-1], "ins": [], "succ": [], "fall": True}
+            label_of[t[:-1]] = len(blocks)
+            continue
+        if cur is None:
+            cur = {"label": None, "ins": [], "succ": [], "fall": True}
+        cur["ins"].append((n, t))
         op = t.split()[0]
-        if op == "s_waitcnt" and "lgkmcnt" in t:
-            keep = int(re.search(r"lgkmcnt\((\d+)\)", t).group(1))
-            pending = pending[len(pending) - keep:] if keep else []
-            continue
-        if op.startswith("ds_read"):
-            dst = t.split(None, 1)[1].split(",")[0]
-            hit = [p for p in pending if p[1] & vregs(t.split(",", 1)[1])]
-            if hit:
-                findings.append((n, t))
-            pending.append(("r", vregs(dst)))
-            continue
-        if op.startswith("ds_write"):
-            hit = [p for p in pending if p[0] == "r" and p[1] & vregs(t)]
-            if hit:
-                findings.append((n, t))
-            pending.append(("w", set()))
-            continue
-        used = vregs(t)
-        if any(p[0] == "r" and p[1] & used for p in pending):
-            findings.append((n, t))
-    return findings
+        if op == "s_branch" or op.startswith("s_cbranch") or op == "s_endpgm":
+            if op != "s_endpgm":
+                cur["succ"].append(t.split()[-1])
+            cur["fall"] = op.startswith("s_cbranch")
+            blocks.append(cur)
+            cur = {"label": None, "ins": [], "succ": [], "fall": True}
+    if cur is not None:
+        blocks.append(cur)
+    index = {b["label"]: i for i, b in enumerate(blocks) if b["label"]}
+    succs = []
+    for i, b in enumerate(blocks):
+        s = [index[x] for x in b["succ"] if x in index]
+        if b["fall"] and i + 1 < len(blocks):
+            s.append(i + 1)
+        succs.append(s)
+    entry = [None] * len(blocks)
+    entry[0] = []
+    work = [0]
+    findings = set()
+    while work:
+        i = work.pop()
+        q = entry[i]
+        f = []
+        for n, t in blocks[i]["ins"]:
+            q = _step(q, t, n, f)
+        findings.update(f)
+        for j in succs[i]:
+            m = _merge(entry[j], q)
+            if m != entry[j]:
+                entry[j] = m
+                work.append(j)
+    return sorted(findings)
 
 
 def check_store_hazard(lines):
@@ -112,10 +173,12 @@ def main():
     if a.asm:
         text = open(a.asm).read()
     else:
+        text = ""
         with tempfile.TemporaryDirectory() as d:
-            out = os.path.join(d, "iwq_prefill.s")
-            compile_asm(out)
-            text = open(out).read()
+            for src in SOURCES:
+                out = os.path.join(d, src + ".s")
+                compile_asm(out, src)
+                text += open(out).read()
     names = KERNELS.findall(text)
     bad = 0
     for name in names:
