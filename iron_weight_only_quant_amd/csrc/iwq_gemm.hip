@@ -1260,7 +1260,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       p.nsplit = nsplit;
       e = prefill_splitk_launch(p, st, false, true);
     } else {
-      e = prefill_b32_launch(p, 153, st);  // per channel: 151's NIB twin (same bits); grouped: 75
+      e = prefill_b32_launch(p, a.gpr == 1 ? 153 : 75, st);  // per channel: 151's NIB twin (same bits); grouped: 75
     }
     if (e != hipSuccess) {
       iwq::last_hip_error() = (int)e;
@@ -1372,7 +1372,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
-  } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) || variant == 97 || variant == 98 || variant == 99 || (variant >= 150 && variant <= 156) ||
+  } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) || variant == 97 || variant == 98 || variant == 99 || (variant >= 150 && variant <= 163) ||
               (variant > 81 && variant < 97)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {
     // prefill default since round 2 (iwq_prefill.hip: 32x32x16 MFMA, early barrier, per-channel

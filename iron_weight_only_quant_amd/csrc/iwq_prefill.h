@@ -23,6 +23,7 @@ struct PrefillArgs {
   float* ws = nullptr;     // split-K: fp32 partial tiles (prefill_splitk_bytes), else unused
   int nsplit = 1;          // split-K: number of K ranges
   int kps = 0;             // split-K: 64-k steps per range
+  int pgm = 0;             // grouped, 16x16x32 forms: scales / zeros held group-major, [gpr, N] (A/B)
 };
 
 // mid-size M (k_w4a16_mid): N % 64 == 0, K % 128 == 0, per-channel or group % 32 == 0; codes
@@ -51,7 +52,7 @@ hipError_t prefill_splitk_launch_s(const PrefillArgs& a, int mtw, hipStream_t st
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns);
 
 // 16x16x32 form of the prefill kernel (iwq_prefill16.hip), per channel: A/B variants 150 / 151
-bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr);
+bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st);
 
 }  // namespace iwq

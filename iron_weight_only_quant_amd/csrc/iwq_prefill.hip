@@ -2944,8 +2944,20 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
 // 16x16x32, 49 = 41; grouped: 40, 41 and 49 plain, 42/43 interleave / setprio, 45 early barrier,
 // 47 16x16x32.
 hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st) {
-  if (variant >= 150 && variant <= 156) {
-    if (prefill16_supported(a.M, a.N, a.K, a.gpr)) return prefill16_launch(a, variant, st);  // iwq_prefill16.hip
+  if (variant >= 158 && variant <= 160) {  // A/B: grouped 150 / 157 / 151 reading group-major parameters
+    if (a.gpr == 1 || !prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return hipErrorInvalidValue;
+    PrefillArgs b = a;
+    b.pgm = 1;
+    return prefill16_launch(b, variant == 158 ? 150 : (variant == 159 ? 157 : 151), st);
+  }
+  // 161 diagnostic; 162 / 163: one wave per SIMD (k_w4a16_b16q), per channel (grouped: 151 / 153)
+  if (variant >= 161 && variant <= 163) {
+    if (a.gpr != 1) variant = variant == 163 ? 153 : 151;
+    else if (prefill16_supported(a.M, a.N, a.K, 1, a.group)) return prefill16_launch(a, variant, st);
+    else return launch_w<false>(a, st);
+  }
+  if (variant >= 150 && variant <= 157) {
+    if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);  // iwq_prefill16.hip
     // grouped: 74 on the same code layout
     return (variant == 152 || variant == 153) ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }
@@ -2972,7 +2984,7 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
   // per channel, default: 74 on the 16x16x32 MFMA with waves 4-7 staggered half a K-step
   // (iwq_prefill16.hip, variant 151; round 4: +6-11 % over 74 on q / gate / down at M = 8192,
   // profiles/r04_ab_gemm_b16.jsonl)
-  if (variant == 0 && prefill16_supported(a.M, a.N, a.K, a.gpr)) return prefill16_launch(a, 151, st);
+  if (variant == 0 && prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, 151, st);
   switch (variant) {
     case 40: return launch<false, false, 0, false>(a, st);
     case 42: return launch<false, true, 1, false>(a, st);

@@ -40,7 +40,7 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr int TM = 256, TN = 256, TK = 64, THR = 512;
 constexpr int XS = TM * TK * 2;  // X bytes per stage (32 KiB)
 constexpr int CS = TN * TK / 2;  // code bytes per stage (8 KiB)
-constexpr int STAGE = XS + CS;
+constexpr int PS = 2 * TN * 4;   // grouped: 256 scales + 256 zero points, one dword each (2 KiB)
 
 __device__ __forceinline__ int xh(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) * 6); }
 __device__ __forceinline__ int cswz(int n) { return (n >> 3) & 1; }
@@ -61,6 +61,11 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
+// 2-byte LDS-DMA: lane l's halfword lands in dword l of the wave's 256-B slot
+__device__ __forceinline__ void glds2(const void* g, uint8_t* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 2, 0, 0);
+}
 
 template <int OFF>
 __device__ __forceinline__ h8 lds_rd(uint32_t addr) {
@@ -72,6 +77,12 @@ template <int OFF>
 __device__ __forceinline__ u32x2 lds_rd2(uint32_t addr) {
   u32x2 v;
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+// two dwords 64 B apart (grouped: the parameters of a lane's two columns)
+__device__ __forceinline__ u32x2 lds_rd_pair(uint32_t addr) {
+  u32x2 v;
+  asm volatile("ds_read2_b32 %0, %1 offset0:0 offset1:16" : "=v"(v) : "v"(addr));
   return v;
 }
 // re-defines v after its wait (see iwq_prefill.hip: keeps post-wait uses below the wait)
@@ -88,10 +99,25 @@ __device__ __forceinline__ void landed(T& v) {
 // the same bits as the row-major form
 // LAG (A/B): the staggered waves' barrier sits 16 MFMA pairs (half a K-step) or 8 pairs before the
 // others'; PRIO (A/B): static s_setprio 1 for waves 4-7 (1) or 0-3 (2) (cdna_hip_programming.md T5)
-template <bool STAGGER, bool NIB = false, int LAG = 16, int PRIO = 0>
+// GROUPED (group % 64 == 0): each K-step lies in one group, so a lane needs one (s, z) per column per
+// K-step; they ride with the stage (a sixth DMA piece per wave: the parameter image of iwq_prefill.hip's
+// 74) and the dequant applies s per weight, RN16((q - z) s) -- the reference's fp16 weight -- with no
+// epilogue scale.  Its stage is 42 KiB, so the staggered ring has 3 slots: a slot is refilled with the
+// K-step two ahead (AHEAD = 2), the barrier then waits for every piece this wave issued (vmcnt(0)), and
+// the late waves issue right after their own barrier (EARLY_ISSUE) for a full K-step of DMA lead.
+// NOSTORE: DIAGNOSTIC (wrong results): the epilogue computes but stores almost nothing (its cost)
+template <bool STAGGER, bool NIB = false, int LAG = 16, int PRIO = 0, bool GROUPED = false, bool EARLY_ISSUE = false,
+          bool NOSTORE = false>
 __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   static_assert(LAG == 16 || LAG == 8, "barrier between pairs 7/8 or after pair 15 of slice 0");
-  constexpr int NST = STAGGER ? 4 : 3;
+  static_assert(!EARLY_ISSUE || STAGGER, "only the staggered waves issue early");
+  constexpr int STAGE = XS + CS + (GROUPED ? PS : 0);
+  constexpr int PIECES = GROUPED ? 6 : 5;                  // DMA pieces per wave per K-step
+  constexpr int NST = (STAGGER && !GROUPED) ? 4 : 3;       // ring slots (160 / 126 / 120 KiB)
+  constexpr int AHEAD = STAGGER ? NST - 1 : 3;             // K-step distance of a refill
+  // vmcnt at a barrier: this wave's pieces of the stage being published have landed; the pieces of
+  // K-steps issued after it (AHEAD - 2 of them) may still fly
+  constexpr int VM_AHEAD = (AHEAD - 2) * PIECES;
   __shared__ __attribute__((aligned(16))) uint8_t smem[NST * STAGE];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -115,28 +141,42 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   }
   const int ccol = wid * 32 + (lane >> 1);
   const uint8_t* csrc = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  // grouped: waves 0-3 stage the scales of columns 64 (wid & 3) + lane, waves 4-7 the zero points
+  // (dword c of the parameter image: scale of column c; dword 256 + c: its zero point)
+  const _Float16* psrc = nullptr;
+  if constexpr (GROUPED) {
+    const _Float16* arr = (wid < 4 || !a.zeros) ? a.scales : a.zeros;
+    const int64_t c = n0 + (wid & 3) * 64 + lane;
+    psrc = arr + (a.pgm ? c : c * a.gpr);
+  }
+  const int64_t pstep = a.pgm ? a.N : 1;  // parameter stride between groups
   auto issue1 = [&](int kt, int stg, int i) {
     uint8_t* base = smem + stg * STAGE;
     if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
-    else glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    else if (i == 4) glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
+    else if constexpr (GROUPED) glds2(psrc + ((kt * TK) / a.group) * pstep, base + XS + CS + wid * 256);
   };
   auto issue = [&](int kt, int stg) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) issue1(kt, stg, i);
+    for (int i = 0; i < PIECES; ++i) issue1(kt, stg, i);
   };
 
   // this lane's two columns (16-column tiles 0, 1 of the wave) and their parameters
   const int col0 = n0 + wid * 32 + r16;
-  float sfl[2];
-  h2 zz[2], zl[2], zh[2];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int col = col0 + 16 * nt;
-    sfl[nt] = (float)gp<_Float16>(a.scales)[col];
-    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+  float sfl[2] = {1.0f, 1.0f};
+  h2 s2[2], zz[2], zl[2], zh[2];
+  auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
     zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = col0 + 16 * nt;
+      sfl[nt] = (float)gp<_Float16>(a.scales)[col];
+      set_zero(nt, a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym);
+    }
   }
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
   const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
@@ -154,17 +194,35 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
   const int ccl = wid * 32 + r16;
   const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+  const uint32_t lps = lbase + XS + CS + (uint32_t)(ccl * 4);  // grouped: scales of col0, col0 + 16
+  const uint32_t lpz = lps + TN * 4;                           // grouped: their zero points
+  u32x2 psv{}, pzv{};                                          // grouped: the raw parameter dwords
+  auto params_landed = [&]() {
+    if constexpr (GROUPED) {
+      landed(psv);
+      landed(pzv);
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)psv[nt]);
+        s2[nt] = h2{sc, sc};
+        set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pzv[nt]) : a.zsym);
+      }
+    }
+  };
 
   // weight pair j (k offsets 2j, 2j + 1) of code dword w, tile nt: (q - z) exactly (3 VALU; NIB:
   // 2, plus one shift per dword for pairs 2 and 3)
   auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    h2 d;
     if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      return (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
-      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+      d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
     }
+    if constexpr (GROUPED) d = d * s2[nt];  // RN16((q - z) s)
+    return d;
   };
   auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
 
@@ -195,7 +253,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   // slice 0 of a K-step (stage offset SO): rolling reads of frags 8..15 of slice 0 and 0..7 of
   // slice 1; slice 1's B fragments (the same code dwords' .y) dequantized on the way, one weight pair
   // per MFMA pair; MID runs between pairs 7 and 8, END after pair 15 (the staggered waves' barrier)
-#define IWQ_SLICE0(SO, MID, END)                                                          \
+#define IWQ_SLICE0(SO, MID, END, ISS)                                                     \
   {                                                                                       \
     const uint32_t a0 = la[0] + (SO), a1 = la[1] + (SO);                                  \
     h2 p[8];                                                                              \
@@ -208,12 +266,12 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     IWQ_PAIR(6, true, IWQ_RD(14, a0), p[6] = dqp(wc1.y, 2, 1));                           \
     IWQ_PAIR(7, true, IWQ_RD(15, a0), p[7] = dqp(wc1.y, 3, 1));                           \
     MID;                                                                                  \
-    IWQ_PAIR(8, true, IWQ_RD(0, a1), );                                                   \
-    IWQ_PAIR(9, true, IWQ_RD(1, a1), );                                                   \
-    IWQ_PAIR(10, true, IWQ_RD(2, a1), );                                                  \
-    IWQ_PAIR(11, true, IWQ_RD(3, a1), );                                                  \
-    IWQ_PAIR(12, true, IWQ_RD(4, a1), );                                                  \
-    IWQ_PAIR(13, true, IWQ_RD(5, a1), );                                                  \
+    IWQ_PAIR(8, true, IWQ_RD(0, a1), ISS(0));                                             \
+    IWQ_PAIR(9, true, IWQ_RD(1, a1), ISS(1));                                             \
+    IWQ_PAIR(10, true, IWQ_RD(2, a1), ISS(2));                                            \
+    IWQ_PAIR(11, true, IWQ_RD(3, a1), ISS(3));                                            \
+    IWQ_PAIR(12, true, IWQ_RD(4, a1), ISS(4));                                            \
+    IWQ_PAIR(13, true, IWQ_RD(5, a1), ISS(5));                                            \
     IWQ_PAIR(14, true, IWQ_RD(6, a1), );                                                  \
     IWQ_PAIR(15, true, IWQ_RD(7, a1), );                                                  \
     END;                                                                                  \
@@ -221,20 +279,26 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     b1 = frag(p + 4);                                                                     \
   }
 
-  // prologue: stages 0 .. NST-1 (K-steps clamped to nk - 1: re-loads nobody reads again)
+  // prologue: K-steps 0 .. AHEAD - 1 into slots 0 .. AHEAD - 1 (clamped to nk - 1: re-loads nobody
+  // reads again); the loop's K-step kt refills the next slot with K-step kt + AHEAD
   issue(0, 0);
   issue(nk > 1 ? 1 : 0, 1);
-  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
   __builtin_amdgcn_s_barrier();
-  issue(nk > 2 ? 2 : nk - 1, 2);  // (STAGGER: slot 3 receives K-step 3 after the first barrier)
+  if constexpr (AHEAD == 3) issue(nk > 2 ? 2 : nk - 1, 2);
   IWQ_PIN();
   wc0 = lds_rd2<0>(lc);
   wc1 = lds_rd2<512>(lc);
+  if constexpr (GROUPED) {
+    psv = lds_rd_pair(lps);
+    pzv = lds_rd_pair(lpz);
+  }
   IWQ_RD(0, la[0]); IWQ_RD(1, la[0]); IWQ_RD(2, la[0]); IWQ_RD(3, la[0]);
   IWQ_RD(4, la[0]); IWQ_RD(5, la[0]); IWQ_RD(6, la[0]); IWQ_RD(7, la[0]);
   IWQ_LGKM(0);
   landed(wc0);
   landed(wc1);
+  params_landed();
   IWQ_PIN();
   {
     h2 p[8];
@@ -247,9 +311,6 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     b1 = frag(p + 4);
   }
 
-  // vmcnt at a barrier (both rings): this wave's pieces of the stage being published have landed;
-  // the next K-step's 5 pieces (issued after the previous barrier) may still fly
-  constexpr int VM_AHEAD = 5;
   if constexpr (PRIO == 1) {
     if (late) __builtin_amdgcn_s_setprio(1);
   } else if constexpr (PRIO == 2) {
@@ -261,17 +322,21 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     const uint32_t sn = (uint32_t)(((kt + 1) % NST) * STAGE);
     // the slot refilled in this K-step and the K-step it receives (clamped: re-loads nobody reads)
     const int sd = STAGGER ? (kt + NST - 1) % NST : kt % NST;
-    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
+    const int kd = kt + AHEAD < nk ? kt + AHEAD : nk - 1;
     // waves 4-7 (STAGGER): their barrier between pairs 7 and 8 of slice 0, 16 MFMA pairs before the
     // others' -- stage kt + 1 published; the slot a DMA may refill before the next barrier holds
     // stage kt - 1, whose reads this wave retired in K-step kt - 1
+    // (EARLY_ISSUE: their refill right after it, pairs 8.. of slice 0)
+#define IWQ_ISS_LATE(I) \
+  if (EARLY_ISSUE && late && (I) < PIECES) issue1(kd, sd, I)
     IWQ_SLICE0(so, if (LAG == 16 && late) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
       __builtin_amdgcn_s_barrier();
     }, if (LAG == 8 && late) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
       __builtin_amdgcn_s_barrier();
-    })
+    }, IWQ_ISS_LATE)
+#undef IWQ_ISS_LATE
     // slice 1: pairs 0..7 read frags 8..15 of slice 1; pairs 8..15 read the next K-step's slice-0
     // frags 0..7 (after the barrier that publishes it), its codes, and issue this K-step's refill
     const uint32_t a1 = la[1] + so;
@@ -295,17 +360,23 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     // codes of stage kt + 1 (oldest of what follows), then the rolling reads of its slice 0
     u32x2 wn0 = lds_rd2<0>(lc + sn);
     u32x2 wn1 = lds_rd2<512>(lc + sn);
+    if constexpr (GROUPED) {  // older than the 4 A reads below: retired by the same lgkmcnt(4)
+      psv = lds_rd_pair(lps + sn);
+      pzv = lds_rd_pair(lpz + sn);
+    }
     const uint32_t na = la[0] + sn;
-    IWQ_PAIR(8, false, IWQ_RD(0, na), issue1(kd, sd, 0));
-    IWQ_PAIR(9, false, IWQ_RD(1, na), issue1(kd, sd, 1));
-    IWQ_PAIR(10, false, IWQ_RD(2, na), issue1(kd, sd, 2));
-    IWQ_PAIR(11, false, IWQ_RD(3, na), issue1(kd, sd, 3));
-    IWQ_LGKM(4);  // the code reads (older than the 4 A reads above) landed
+    const bool iss = !(EARLY_ISSUE && late);  // wave-uniform
+    IWQ_PAIR(8, false, IWQ_RD(0, na), if (iss) issue1(kd, sd, 0));
+    IWQ_PAIR(9, false, IWQ_RD(1, na), if (iss) issue1(kd, sd, 1));
+    IWQ_PAIR(10, false, IWQ_RD(2, na), if (iss) issue1(kd, sd, 2));
+    IWQ_PAIR(11, false, IWQ_RD(3, na), if (iss) issue1(kd, sd, 3));
+    IWQ_LGKM(4);  // the code (and parameter) reads, older than the 4 A reads above, landed
     landed(wn0);
     landed(wn1);
+    params_landed();
     h2 p[8];
-    IWQ_PAIR(12, false, IWQ_RD(4, na), issue1(kd, sd, 4); p[0] = dqp(wn0.x, 0, 0); p[1] = dqp(wn0.x, 1, 0));
-    IWQ_PAIR(13, false, IWQ_RD(5, na), p[2] = dqp(wn0.x, 2, 0); p[3] = dqp(wn0.x, 3, 0));
+    IWQ_PAIR(12, false, IWQ_RD(4, na), if (iss) issue1(kd, sd, 4); p[0] = dqp(wn0.x, 0, 0); p[1] = dqp(wn0.x, 1, 0));
+    IWQ_PAIR(13, false, IWQ_RD(5, na), if (iss && GROUPED) issue1(kd, sd, 5); p[2] = dqp(wn0.x, 2, 0); p[3] = dqp(wn0.x, 3, 0));
     IWQ_PAIR(14, false, IWQ_RD(6, na), p[4] = dqp(wn1.x, 0, 1); p[5] = dqp(wn1.x, 1, 1));
     IWQ_PAIR(15, false, IWQ_RD(7, na), p[6] = dqp(wn1.x, 2, 1); p[7] = dqp(wn1.x, 3, 1));
     b0 = frag(p);
@@ -316,7 +387,9 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   {
     // the last K-step: no next stage, no barrier
     const uint32_t so = (uint32_t)(((nk - 1) % NST) * STAGE);
-    IWQ_SLICE0(so, , )
+#define IWQ_NOP(I)
+    IWQ_SLICE0(so, , , IWQ_NOP)
+#undef IWQ_NOP
     const uint32_t a1 = la[1] + so;
     IWQ_PAIR(0, true, IWQ_RD(8, a1), );
     IWQ_PAIR(1, true, IWQ_RD(9, a1), );
@@ -349,27 +422,321 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = mt * 16 + r;
-      if (full || m0 + rr + 4 * g < a.M) {
+      if constexpr (NOSTORE) {
+        if (acc[mt][0][r] == 1.2345e-30f || acc[mt][1][r] == 1.2345e-30f) {
+          auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
+          p[0] = (_Float16)(opaque(acc[mt][0][r] * sfl[0]) + bc0);
+          p[16] = (_Float16)(opaque(acc[mt][1][r] * sfl[1]) + bc1);
+        }
+      } else if (full || m0 + rr + 4 * g < a.M) {
         auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
-        p[0] = (_Float16)(opaque(acc[mt][0][r] * sfl[0]) + bc0);
-        p[16] = (_Float16)(opaque(acc[mt][1][r] * sfl[1]) + bc1);
+        if constexpr (GROUPED) {
+          p[0] = (_Float16)(acc[mt][0][r] + bc0);
+          p[16] = (_Float16)(acc[mt][1][r] + bc1);
+        } else {
+          p[0] = (_Float16)(opaque(acc[mt][0][r] * sfl[0]) + bc0);
+          p[16] = (_Float16)(opaque(acc[mt][1][r] * sfl[1]) + bc1);
+        }
       }
     }
 }
+
+// k_w4a16_b16q: one wave per SIMD.  4 waves (256 threads), the same 256 x 256 tile; wave w owns all
+// 256 rows x columns 64 w .. 64 w + 63 = 16 x 4 tiles of 16x16, so each A fragment feeds FOUR MFMAs
+// (b16w: two) and the LDS reads per MFMA halve -- b16w's 8 waves read 256 KiB of A per K-step per CU
+// (~1024 of the 2048 LDS-array cycles the K-step's MFMAs take at 256 B/clk); here 128 KiB.  Each
+// weight is still dequantized once per workgroup (one pair of 2 per group of four MFMAs).  The 256
+// accumulators per lane sit in AGPRs (hipBLASLt's MT256x256x64_MI16x16 kernel for these shapes runs the
+// same one-wave-per-SIMD shape).  4-slot ring (160 KiB): the barrier sits early in slice 1 (after the
+// group that consumes fragment 3), publishes the next stage and frees the slot of the stage before the
+// running one (all its reads retired a K-step ago), which is refilled right after.
+// Per K-step and wave: slice 0 -- 16 groups of (wait, 4 MFMAs, rolling A read 4 fragments ahead, one
+// weight pair of slice 1's B); slice 1 -- groups 0-3, the barrier, the next stage's codes, 10 DMA
+// pieces spread over groups 4-13, the next stage's slice-0 B dequantized over groups 8-15.
+template <bool NIB>
+__global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
+  constexpr int NSTQ = 4;
+  constexpr int STAGE = XS + CS;  // 40 KiB
+  constexpr int PIECES = 10;      // DMA pieces per wave per K-step: 8 of X rows, 2 of codes
+  constexpr int VM_AHEAD = PIECES;  // at a barrier the pieces of the K-step after the published one fly
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTQ * STAGE];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int64_t crow = a.K / 2;
+  const int nk = a.K / TK;
+
+  // DMA sources: X rows (wid * 8 + i) * 8 + lane / 8, 16-B chunk lane % 8 from chunk (lane % 8) ^ h;
+  // codes: column wid * 64 + 32 j + lane / 2, chunk lane % 2 from chunk (lane % 2) ^ cswz
+  const _Float16* xsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (wid * 8 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3);
+  }
+  const uint8_t* csrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ccol = wid * 64 + 32 * j + (lane >> 1);
+    csrc[j] = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  }
+  auto issue1 = [&](int kt, int stg, int i) {
+    uint8_t* base = smem + stg * STAGE;
+    if (i < 8) glds16(xsrc[i] + kt * TK, base + (wid * 8 + i) * 1024);
+    else glds16(csrc[i - 8] + kt * (TK / 2), base + XS + (wid * 2 + i - 8) * 1024);
+  };
+  auto issue = [&](int kt, int stg) {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) issue1(kt, stg, i);
+  };
+
+  // this lane's four columns (16-column tiles 0..3 of the wave) and their parameters
+  const int col0 = n0 + wid * 64 + r16;
+  float sfl[4];
+  h2 zz[4], zl[4], zh[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int col = col0 + 16 * nt;
+    sfl[nt] = (float)gp<_Float16>(a.scales)[col];
+    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  // LDS byte addresses: A fragment (stage st, slice s, tile mt) = la[s] + st * STAGE + 2048 mt;
+  // codes of tile nt = lc + st * STAGE + 512 nt
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
+  const int ccl = wid * 64 + r16;
+  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    if constexpr (NIB) {
+      const uint32_t t = j >= 2 ? w >> 8 : w;
+      return (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+  };
+  auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
+
+  f4 acc[16][4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 af[8];
+  h8 b0[4], b1[4];  // B fragments of slice 0 / 1 (tiles 0..3)
+  u32x2 wc[4];      // the running K-step's code dwords per tile: .x slice 0, .y slice 1
+
+#define IWQ_RD(MT, ADDR) af[(MT) & 7] = lds_rd<((MT) & 15) * 2048>(ADDR)
+#define IWQ_MF4(MT, B)                                                                        \
+  acc[MT][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[0], acc[MT][0], 0, 0, 0); \
+  acc[MT][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[1], acc[MT][1], 0, 0, 0); \
+  acc[MT][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[2], acc[MT][2], 0, 0, 0); \
+  acc[MT][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[3], acc[MT][3], 0, 0, 0)
+  // group MT of a slice: the wait for its fragment (N newer LDS reads may stay in flight), its four
+  // MFMAs, then the rolling read (READ) and VALU / DMA work (WORK)
+#define IWQ_GRP(MT, N, B, READ, WORK) \
+  {                                   \
+    IWQ_LGKM(N);                      \
+    IWQ_PIN();                        \
+    IWQ_MF4(MT, B);                   \
+    READ;                             \
+    WORK;                             \
+    IWQ_PIN();                        \
+  }
+  // slice 0 (stage offset SO): rolling reads of fragments 4..15 of slice 0 and 0..3 of slice 1;
+  // slice 1's B (the same code dwords' .y) dequantized one pair per group
+#define IWQ_QSLICE0(SO)                                                            \
+  {                                                                                \
+    const uint32_t a0 = la[0] + (SO), a1 = la[1] + (SO);                           \
+    h2 p[16];                                                                      \
+    IWQ_GRP(0, 3, b0, IWQ_RD(4, a0), p[0] = dqp(wc[0].y, 0, 0));                   \
+    IWQ_GRP(1, 3, b0, IWQ_RD(5, a0), p[1] = dqp(wc[0].y, 1, 0));                   \
+    IWQ_GRP(2, 3, b0, IWQ_RD(6, a0), p[2] = dqp(wc[0].y, 2, 0));                   \
+    IWQ_GRP(3, 3, b0, IWQ_RD(7, a0), p[3] = dqp(wc[0].y, 3, 0));                   \
+    IWQ_GRP(4, 3, b0, IWQ_RD(8, a0), p[4] = dqp(wc[1].y, 0, 1));                   \
+    IWQ_GRP(5, 3, b0, IWQ_RD(9, a0), p[5] = dqp(wc[1].y, 1, 1));                   \
+    IWQ_GRP(6, 3, b0, IWQ_RD(10, a0), p[6] = dqp(wc[1].y, 2, 1));                  \
+    IWQ_GRP(7, 3, b0, IWQ_RD(11, a0), p[7] = dqp(wc[1].y, 3, 1));                  \
+    IWQ_GRP(8, 3, b0, IWQ_RD(12, a0), p[8] = dqp(wc[2].y, 0, 2));                  \
+    IWQ_GRP(9, 3, b0, IWQ_RD(13, a0), p[9] = dqp(wc[2].y, 1, 2));                  \
+    IWQ_GRP(10, 3, b0, IWQ_RD(14, a0), p[10] = dqp(wc[2].y, 2, 2));                \
+    IWQ_GRP(11, 3, b0, IWQ_RD(15, a0), p[11] = dqp(wc[2].y, 3, 2));                \
+    IWQ_GRP(12, 3, b0, IWQ_RD(0, a1), p[12] = dqp(wc[3].y, 0, 3));                 \
+    IWQ_GRP(13, 3, b0, IWQ_RD(1, a1), p[13] = dqp(wc[3].y, 1, 3));                 \
+    IWQ_GRP(14, 3, b0, IWQ_RD(2, a1), p[14] = dqp(wc[3].y, 2, 3));                 \
+    IWQ_GRP(15, 3, b0, IWQ_RD(3, a1), p[15] = dqp(wc[3].y, 3, 3));                 \
+    b1[0] = frag(p);                                                               \
+    b1[1] = frag(p + 4);                                                           \
+    b1[2] = frag(p + 8);                                                           \
+    b1[3] = frag(p + 12);                                                          \
+  }
+
+  // prologue: K-steps 0, 1, 2 into slots 0, 1, 2 (clamped to nk - 1: re-loads nobody reads again)
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  issue(nk > 2 ? 2 : nk - 1, 2);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+  wc[0] = lds_rd2<0>(lc);
+  wc[1] = lds_rd2<512>(lc);
+  wc[2] = lds_rd2<1024>(lc);
+  wc[3] = lds_rd2<1536>(lc);
+  IWQ_RD(0, la[0]); IWQ_RD(1, la[0]); IWQ_RD(2, la[0]); IWQ_RD(3, la[0]);
+  IWQ_LGKM(0);
+  landed(wc[0]);
+  landed(wc[1]);
+  landed(wc[2]);
+  landed(wc[3]);
+  IWQ_PIN();
+  {
+    h2 p[16];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[4 * nt + j] = dqp(wc[nt].x, j, nt);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b0[nt] = frag(p + 4 * nt);
+  }
+
+  // the last K-step is peeled (a branch in the body made the compiler keep two register images)
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NSTQ) * STAGE);
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSTQ) * STAGE);
+    const int sd = (kt + NSTQ - 1) % NSTQ;         // the slot of stage kt - 1, refilled after the barrier
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;  // ... with K-step kt + 3 (clamped: re-loads nobody reads)
+    IWQ_QSLICE0(so)
+    const uint32_t a1 = la[1] + so;
+    const uint32_t na = la[0] + sn;
+    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), );
+    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), );
+    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), );
+    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), );
+    // stage kt + 1 landed (this wave's part; K-step kt + 2's pieces may fly): publish it.  Every read
+    // of stage kt - 1 retired a K-step ago, so its slot is refilled below.
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    u32x2 wn[4];
+    IWQ_GRP(4, 3, b1, wn[0] = lds_rd2<0>(lc + sn); wn[1] = lds_rd2<512>(lc + sn); wn[2] = lds_rd2<1024>(lc + sn);
+            wn[3] = lds_rd2<1536>(lc + sn); IWQ_RD(8, a1), issue1(kd, sd, 0));
+    IWQ_GRP(5, 7, b1, IWQ_RD(9, a1), issue1(kd, sd, 1));
+    IWQ_GRP(6, 7, b1, IWQ_RD(10, a1), issue1(kd, sd, 2));
+    IWQ_GRP(7, 7, b1, IWQ_RD(11, a1), issue1(kd, sd, 3));
+    h2 p[16];
+    IWQ_LGKM(3);  // fragment 8 and everything older (the code reads) landed
+    landed(wn[0]);
+    landed(wn[1]);
+    landed(wn[2]);
+    landed(wn[3]);
+    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(kd, sd, 4); p[0] = dqp(wn[0].x, 0, 0); p[1] = dqp(wn[0].x, 1, 0));
+    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), issue1(kd, sd, 5); p[2] = dqp(wn[0].x, 2, 0); p[3] = dqp(wn[0].x, 3, 0));
+    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(kd, sd, 6); p[4] = dqp(wn[1].x, 0, 1); p[5] = dqp(wn[1].x, 1, 1));
+    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), issue1(kd, sd, 7); p[6] = dqp(wn[1].x, 2, 1); p[7] = dqp(wn[1].x, 3, 1));
+    IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(kd, sd, 8); p[8] = dqp(wn[2].x, 0, 2); p[9] = dqp(wn[2].x, 1, 2));
+    IWQ_GRP(13, 3, b1, IWQ_RD(1, na), issue1(kd, sd, 9); p[10] = dqp(wn[2].x, 2, 2); p[11] = dqp(wn[2].x, 3, 2));
+    IWQ_GRP(14, 3, b1, IWQ_RD(2, na), p[12] = dqp(wn[3].x, 0, 3); p[13] = dqp(wn[3].x, 1, 3));
+    IWQ_GRP(15, 3, b1, IWQ_RD(3, na), p[14] = dqp(wn[3].x, 2, 3); p[15] = dqp(wn[3].x, 3, 3));
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      b0[nt] = frag(p + 4 * nt);
+      wc[nt] = wn[nt];
+    }
+  }
+  {
+    // the last K-step: no next stage, no barrier
+    const uint32_t so = (uint32_t)(((nk - 1) % NSTQ) * STAGE);
+    IWQ_QSLICE0(so)
+    const uint32_t a1 = la[1] + so;
+    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), );
+    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), );
+    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), );
+    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), );
+    IWQ_GRP(4, 3, b1, IWQ_RD(8, a1), );
+    IWQ_GRP(5, 3, b1, IWQ_RD(9, a1), );
+    IWQ_GRP(6, 3, b1, IWQ_RD(10, a1), );
+    IWQ_GRP(7, 3, b1, IWQ_RD(11, a1), );
+    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), );
+    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), );
+    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), );
+    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), );
+    IWQ_GRP(12, 3, b1, , );
+    IWQ_GRP(13, 2, b1, , );
+    IWQ_GRP(14, 1, b1, , );
+    IWQ_GRP(15, 0, b1, , );
+  }
+  // no LDS-DMA may still be landing when the workgroup retires (the CU's next workgroup owns the LDS)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_QSLICE0
+#undef IWQ_GRP
+#undef IWQ_MF4
+#undef IWQ_RD
+
+  // epilogue: lane holds rows 16 mt + 4 g + r of columns col0 + 16 nt
+  float bc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) bc[nt] = a.bias ? (float)gp<_Float16>(a.bias)[col0 + 16 * nt] : 0.0f;
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;  // row pitch, bytes
+  char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * g) * a.ldy + col0) * 2;
+  const bool full = m0 + TM <= a.M;
+#pragma unroll
+  for (int mt = 0; mt < 16; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = mt * 16 + r;
+      if (full || m0 + rr + 4 * g < a.M) {
+        auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) p[16 * nt] = (_Float16)(opaque(acc[mt][nt][r] * sfl[nt]) + bc[nt]);
+      }
+    }
+}
+
 #undef IWQ_LGKM
 #undef IWQ_PIN
 
 }  // namespace
 
-// 16x16x32 forms of 74 (per channel): variants 150 (3-slot ring), 151 (4-slot ring, waves 4-7
-// staggered half a K-step: the per-channel default since round 4), 152 / 153 the same on NIB codes
-bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr) {
-  return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && gpr == 1;
+// 16x16x32 forms of 74: variants 150 (3-slot ring), 151 (4-slot ring, waves 4-7 staggered half a
+// K-step: the per-channel default since round 4), 152 / 153 the same on NIB codes; grouped weights
+// (group % 64 == 0): 150 / 152 the 3-slot ring, 151 / 153 staggered on 3 slots with the late waves
+// issuing early, 157 staggered issuing in slice 1 (A/B)
+bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
+  return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || (group % TK == 0 && K % group == 0));
 }
 
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const dim3 grid((unsigned)blocks), blk(THR);
+  if (a.gpr != 1) {
+    switch (variant) {
+      case 150: hipLaunchKernelGGL((k_w4a16_b16w<false, false, 16, 0, true>), grid, blk, 0, st, a); break;
+      case 152: hipLaunchKernelGGL((k_w4a16_b16w<false, true, 16, 0, true>), grid, blk, 0, st, a); break;
+      case 153: hipLaunchKernelGGL((k_w4a16_b16w<true, true, 16, 0, true, true>), grid, blk, 0, st, a); break;
+      case 157: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, true, false>), grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, true, true>), grid, blk, 0, st, a); break;
+    }
+    return hipGetLastError();
+  }
   switch (variant) {
     case 150: hipLaunchKernelGGL((k_w4a16_b16w<false>), grid, blk, 0, st, a); break;
     case 152: hipLaunchKernelGGL((k_w4a16_b16w<false, true>), grid, blk, 0, st, a); break;
@@ -377,6 +744,11 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
     case 154: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 8>), grid, blk, 0, st, a); break;    // A/B
     case 155: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 1>), grid, blk, 0, st, a); break;
     case 156: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 2>), grid, blk, 0, st, a); break;
+    case 162: hipLaunchKernelGGL((k_w4a16_b16q<false>), grid, dim3(256), 0, st, a); break;
+    case 163: hipLaunchKernelGGL((k_w4a16_b16q<true>), grid, dim3(256), 0, st, a); break;
+    case 161:  // DIAGNOSTIC: 151 without the output stores
+      hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, false, false, true>), grid, blk, 0, st, a);
+      break;
     default: hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a); break;
   }
   return hipGetLastError();

@@ -27,7 +27,8 @@ def nib_layout(codes, N, K):
     return out.reshape(N, K // 2).contiguous()
 
 
-NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99, 152, 153)
+NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99, 152, 153, 163)
+GM_VARIANTS = (158, 159, 160)  # grouped parameters held group-major
 
 
 def main():
@@ -66,8 +67,13 @@ def main():
         for v in [int(t) for t in toks]:
             fl = kernels.gemm_variant_flags(v)
             cd = nib if v in NIB_VARIANTS else r.codes
-            arms[f"v{v}"] = (lambda fl=fl, cd=cd: kernels.w4a16_gemm(x, cd, r.scales, r.zeros, 4, a.group, N,
-                                                                     flags=fl, out=y))
+            sc, zr = r.scales, r.zeros
+            if v in GM_VARIANTS:  # group-major parameters, [gpr, N]
+                gpr = sc.numel() // N
+                sc = sc.reshape(N, gpr).t().contiguous().reshape(r.scales.shape)
+                zr = None if zr is None else zr.reshape(N, gpr).t().contiguous().reshape(r.zeros.shape)
+            arms[f"v{v}"] = (lambda fl=fl, cd=cd, sc=sc, zr=zr: kernels.w4a16_gemm(x, cd, sc, zr, 4, a.group, N,
+                                                                                   flags=fl, out=y))
         for f in arms.values():
             f()
         torch.cuda.synchronize()

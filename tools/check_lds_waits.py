@@ -1,5 +1,5 @@
 """ISA lint for the hand-ordered prefill kernels (iwq_prefill.hip: k_w4a16_b32w / b32v / b32s / w4h / w4b;
-iwq_prefill16.hip: k_w4a16_b16w).
+iwq_prefill16.hip: k_w4a16_b16w, k_w4a16_b16q).
 
 Those kernels issue their LDS reads and writes as inline asm and count the lgkmcnt waits by hand,
 which the compiler cannot see: a register an asm ds_read fills is only valid once a wait has retired
@@ -27,7 +27,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "iron_weight_only_quant_amd", "csrc")
-KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v|b16w)\w*):", re.M)
+KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v|b16w|b16q)\w*):", re.M)
 SOURCES = ("iwq_prefill.hip", "iwq_prefill16.hip")
 
 
