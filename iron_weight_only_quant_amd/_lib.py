@@ -12,7 +12,9 @@ import threading
 import torch  # imported first: torch's libamdhip64.so.7 becomes THE HIP runtime of the process
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "libiwq.so")
+# IWQ_AB=1: the A/B library (every kernel variant; iron_weight_only_quant_amd/build.py) instead of the
+# product one
+LIB_PATH = os.path.join(HERE, "_lib", "libiwq_ab.so" if os.environ.get("IWQ_AB", "0") == "1" else "libiwq.so")
 
 IWQ_F16, IWQ_BF16, IWQ_F32 = 0, 1, 2
 DTYPE_CODE = {torch.float16: IWQ_F16, torch.bfloat16: IWQ_BF16, torch.float32: IWQ_F32}
@@ -67,7 +69,8 @@ def load():
         if _lib is not None:
             return _lib
         if not os.path.exists(LIB_PATH):
-            raise OSError(f"iwq HIP library not built: {LIB_PATH} missing (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+            raise OSError(f"iwq HIP library not built: {LIB_PATH} missing (run `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'`; the A/B library: `IWQ_AB=1 python -m iron_weight_only_quant_amd.build --ab`)")
         lib = ctypes.CDLL(LIB_PATH)
         i64, i32, u32, vp, u64 = ctypes.c_int64, ctypes.c_int, ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint64
         lib.iwq_workspace_bytes.argtypes = [i64, i64, i64, i32]
@@ -141,6 +144,11 @@ def load():
         lib.iwq_selftest_division.restype = i32
         _lib = lib
         return lib
+
+
+def ab_built():
+    """True when the loaded library carries the A/B kernel variants (IWQ_AB build)."""
+    return load().iwq_build_info().endswith(b"ab=1")
 
 
 def status_string(status):

@@ -6,6 +6,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(OUT_DIR, "libiwq.so")
+# IWQ_AB=1: the A/B library (every kernel variant kept for timing and its bit-identity tests,
+# csrc/iwq_common.cuh), built beside the product one from its own objects; _lib.py loads it when
+# IWQ_AB=1 is set in the environment.
+AB_OUT_DIR = os.path.join(OUT_DIR, "ab")
+LIB_AB = os.path.join(OUT_DIR, "libiwq_ab.so")
+
+
+def ab_requested():
+    return os.environ.get("IWQ_AB", "0") == "1"
 SOURCES = ["iwq_minmax.hip", "iwq_batched.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
            "iwq_fpunpack.hip", "iwq_codes.hip", "iwq_prefill16.hip", "iwq_fpdt.hip"]
 DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h",
@@ -19,27 +28,31 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
          "-Wno-unused-function", "--offload-compress"]
 
 
-def library_path():
-    return LIB
+def library_path(ab=None):
+    return LIB_AB if (ab_requested() if ab is None else ab) else LIB
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(ab=False):
+    lib = LIB_AB if ab else LIB
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(HERE, "..", "include", "iwq.h")]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build_library(force=False, verbose=True):
+def build_library(force=False, verbose=True, ab=None):
     """Compile each translation unit in parallel (-fgpu-rdc not needed: no cross-TU device calls),
-    then link the shared library."""
-    if not force and not _stale():
-        return LIB
+    then link the shared library (ab: the A/B library, default from IWQ_AB)."""
+    ab = ab_requested() if ab is None else ab
+    lib = LIB_AB if ab else LIB
+    if not force and not _stale(ab):
+        return lib
     from concurrent.futures import ThreadPoolExecutor
-    os.makedirs(OUT_DIR, exist_ok=True)
-    objs = [os.path.join(OUT_DIR, os.path.splitext(s)[0] + ".o") for s in SOURCES]
-    compile_flags = [f for f in FLAGS if f != "-shared"]
+    out_dir = AB_OUT_DIR if ab else OUT_DIR
+    os.makedirs(out_dir, exist_ok=True)
+    objs = [os.path.join(out_dir, os.path.splitext(s)[0] + ".o") for s in SOURCES]
+    compile_flags = [f for f in FLAGS if f != "-shared"] + (["-DIWQ_AB=1"] if ab else [])
 
     def cc(src_obj):
         src, obj = src_obj
@@ -59,15 +72,15 @@ def build_library(force=False, verbose=True):
     todo = [so for so in zip(SOURCES, objs) if obj_stale(so)]
     with ThreadPoolExecutor(max_workers=max(1, min(len(todo), os.cpu_count() or 1))) as ex:
         list(ex.map(cc, todo))
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print("[iwq build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
     import sys
-    build_library(force="--force" in sys.argv)
+    build_library(force="--force" in sys.argv, ab=True if "--ab" in sys.argv else None)

@@ -13,6 +13,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// IWQ_AB=1 (build.py --ab / IWQ_AB=1 in the environment -> _lib/libiwq_ab.so): also compile the kernel
+// variants kept for A/B timing and their bit-identity tests (flags bits 16..23 that no default path
+// takes).  The product library (IWQ_AB=0) carries the defaults plus the forms the tests pin, and
+// answers any other variant with IWQ_ERR_ARG.
+#ifndef IWQ_AB
+#define IWQ_AB 0
+#endif
+
 namespace iwq {
 
 // last HIP error of this host thread, shared by every translation unit (iwq_last_hip_error)

@@ -928,9 +928,12 @@ hipError_t launch_apx_double_lut_v(const FpArgs& a, hipStream_t st) {
 template <int G>
 hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
   // default: V4 (11 % faster than the round-2 form, bit-identical; profiles/r03_ab_apxd.jsonl)
+#if IWQ_AB
   if (a.variant == 1) return launch_apx_double_lut_v<G, 1>(a, st);
   if (a.variant == 2) return launch_apx_double_lut_v<G, 2>(a, st);
   if (a.variant == 3) return launch_apx_double_lut_v<G, 0>(a, st);
+#endif
+  if (a.variant != 0) return hipErrorInvalidValue;  // A/B forms: IWQ_AB builds
   return launch_apx_double_lut_v<G, 4>(a, st);
 }
 

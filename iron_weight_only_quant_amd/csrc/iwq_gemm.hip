@@ -1236,6 +1236,12 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   a.gshift = (g & (g - 1)) == 0 ? __builtin_ctzll((unsigned long long)g) : -1;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const unsigned variant = (flags >> 16) & 0xFFu;
+  // the product library takes the default (0) and, at M > 16 on row-major codes, the two fallback
+  // kernels for shapes the prefill kernels refuse: k_w4a16 (1) and k_w4a16_big (2); every other
+  // variant is an A/B form (IWQ_AB builds)
+  if (!IWQ_AB && variant != 0 &&
+      !((variant == 1 || variant == 2) && M > 16 && !(flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_NIB_CODES))))
+    return IWQ_ERR_ARG;
   // default at M > 16: the split-K prefill where it is modelled faster (M >= 256: whenever a split
   // helps; 16 < M < 256: against the mid-M kernel) and the caller gave the workspace it needs
   int short_ns = 0;
@@ -1260,7 +1266,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       p.nsplit = nsplit;
       e = prefill_splitk_launch(p, st, false, true);
     } else {
-      e = prefill_b32_launch(p, a.gpr == 1 ? 153 : 75, st);  // per channel: 151's NIB twin (same bits); grouped: 75
+      e = prefill_b32_launch(p, 0, st, true);  // the default's NIB twin (same bits)
     }
     if (e != hipSuccess) {
       iwq::last_hip_error() = (int)e;
@@ -1271,6 +1277,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
     if (M > 16) return IWQ_ERR_ARG;
     switch (variant) {  // same shapes as the row-major variants of the same number (A/B)
+#if IWQ_AB
       case 1:
       case 2: launch_gemv<4, 8, 1, 0, true>(a, st, true); break;
       case 4: launch_gemv<4, 4, 2, 0, true>(a, st, true); break;
@@ -1294,6 +1301,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 104: launch_gemv<2, 16, 1, 1, true>(a, st, true); break;
       case 25: launch_gemv<2, 8, 1, 0, true>(a, st, true, false); break;  // per-element scale (A/B)
       case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false); break;
+#endif
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
@@ -1303,6 +1311,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     }
   } else if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
     switch (variant) {
+#if IWQ_AB
       case 1:  // previous decode kernel (A/B reference)
         if (K >= 4096) hipLaunchKernelGGL(k_w4a16_decode<8>, dim3((unsigned)(N / 16)), dim3(512), 0, st, a);
         else hipLaunchKernelGGL(k_w4a16_decode<4>, dim3((unsigned)(N / 16)), dim3(256), 0, st, a);
@@ -1332,6 +1341,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 15: launch_gemv_p<4, 8, 1>(a, st); break;
       case 16: launch_gemv_p<2, 4, 1>(a, st); break;
       case 17: launch_gemv_p<4, 4, 1>(a, st); break;
+#endif
       default:  // best or within 5 % of best, M in {1,4,16} (r01 sweep); column tiles for M >= 4
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, false>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, false>(a, st);
@@ -1401,10 +1411,12 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     const int64_t blocks = ((M + BG_M - 1) / BG_M) * (N / BG_N);
     if (a.gpr != 1)
       hipLaunchKernelGGL((k_w4a16_big<64, false, true>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+#if IWQ_AB
     else if (variant == 23 && K % 128 == 0)
       hipLaunchKernelGGL((k_w4a16_big<128>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
     else if (variant == 24)
       hipLaunchKernelGGL((k_w4a16_big<64, true>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
+#endif
     else
       hipLaunchKernelGGL((k_w4a16_big<64>), dim3((unsigned)blocks), dim3(BG_THR), 0, st, a);
   } else {

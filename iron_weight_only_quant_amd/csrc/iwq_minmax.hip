@@ -146,6 +146,7 @@ __global__ __launch_bounds__(BLOCK) void k_probe(const iwq_batch_entry* entries,
 }
 
 hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
+#if IWQ_AB
   switch (v) {
     case 1: return launch_variant_t<4, true, true, true>(a, st);
     case 2: return launch_variant_t<4, true, false, true>(a, st);
@@ -204,6 +205,11 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     IWQ_PROBE_POL(115, 3, true) IWQ_PROBE_POL(116, 4, true) IWQ_PROBE_POL(117, 5, true)
 #undef IWQ_PROBE_POL
   }
+#else
+  (void)v;
+  (void)a;
+  (void)st;
+#endif
   return hipErrorInvalidValue;
 }
 
@@ -314,8 +320,10 @@ hipError_t launch_col_v(int variant, const ColArgs& a, hipStream_t st) {
     if ((variant == 4 && a.g == 64) || ((variant == 0 || variant == 4) && a.g == 32))
       return launch_col_wide<DT, SYM, CODES>(a, st);
   }
+#if IWQ_AB
   if (variant == 1) return launch_col_t<DT, SYM, CODES, 8, 32>(a, st);
   if (variant == 2) return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
+#endif
   if (variant == 3 || a.g == 256) return launch_col_t<DT, SYM, CODES, 16, 16>(a, st);  // 16 rows/thread at g=256
   return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
 }
@@ -423,7 +431,7 @@ hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, 
   if (variant == 0 || variant == 7 || variant == 9) {
     hipError_t e = hipSuccess;
     if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e,
-                                              variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT))
+                                              IWQ_AB && variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT))
       return e;
   }
   const int64_t nunits = numel / 8;
@@ -432,6 +440,7 @@ hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, 
   if (blocks > need) blocks = need;
   if (blocks > TENSOR_PARTS_MAX) blocks = TENSOR_PARTS_MAX;
   if (blocks < 1) blocks = 1;
+#if IWQ_AB
   if (variant == 1)
     launch_tensor_pair<DT, SYM, CODES, true, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   else if (variant == 3)
@@ -441,6 +450,7 @@ hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, 
   else if (variant == 5)
     launch_tensor_pair<DT, SYM, CODES, false, false, 2>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   else
+#endif
     launch_tensor_pair<DT, SYM, CODES, false, false>(w, out, codes, scales, zeros, nunits, blocks, ws, n_bits, nan_flag, st);
   return hipGetLastError();
 }
@@ -525,6 +535,10 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
   const bool al = aligned16(w) && (!out_deq || aligned16(out_deq)) && (ld_w * eb) % 16 == 0 &&
                   (!out_deq || (ld_out * eb) % 16 == 0) && (!out_codes || aligned16(out_codes));
   const bool fastbits = n_bits <= 8;
+  // product library: the default, and per tensor the pair forced (6: the host's retry) and the
+  // test-only abort (9); every other variant is an A/B form (IWQ_AB builds)
+  const int variant = (int)((flags >> 16) & 0xFFu);
+  if (!IWQ_AB && variant != 0 && !(group == IWQ_GROUP_PER_TENSOR && (variant == 6 || variant == 9))) return IWQ_ERR_ARG;
 
   if (!generic && quant_dim == 0 && group > 0 && group >= 8 && group <= 512 && is_pow2(group) && al &&
       fastbits && ld_w == cols && (!out_deq || ld_out == cols)) {
@@ -542,8 +556,7 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     const int64_t need = iwq_workspace_bytes(rows, cols, group, quant_dim);
     if (!workspace || workspace_bytes < need || !aligned16(workspace)) return IWQ_ERR_WORKSPACE;
     IWQ_HIP(launch_tensor(dtype, sym, codes, w, out_deq, out_codes, out_scales, sym ? nullptr : out_zeros,
-                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s,
-                          (int)((flags >> 16) & 0xFFu)));
+                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s, variant));
     return IWQ_OK;
   }
   if (!generic && quant_dim == 0 && group != IWQ_GROUP_PER_TENSOR && L % 8 == 0 && L <= ROW_MAX_L && al && fastbits) {
@@ -578,7 +591,7 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     a.g = L;  // rows per group (L = group, or rows for per-channel)
     a.n_bits = n_bits;
     a.nan_flag = nan_flag;
-    IWQ_HIP(launch_col(dtype, sym, codes, (int)((flags >> 16) & 0xFFu), a, s));
+    IWQ_HIP(launch_col(dtype, sym, codes, variant, a, s));
     return IWQ_OK;
   }
   // universal path
@@ -651,6 +664,7 @@ int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entr
   // states with IWQ_FLAG_BATCH_CODES that every entry carries out_codes.
   const int codes = (flags & IWQ_FLAG_BATCH_CODES) ? (n_bits <= 4 ? 4 : 8) : 0;
   const int variant = (int)((flags >> 16) & 0xFFu);
+  if (!IWQ_AB && variant != 0) return IWQ_ERR_ARG;  // A/B forms: IWQ_AB builds
   if (variant != 0 && dtype == IWQ_F16 && group == 128 && !symmetric && codes == 0) {
     IWQ_HIP(launch_variant(variant, a, static_cast<hipStream_t>(stream)));
     return IWQ_OK;

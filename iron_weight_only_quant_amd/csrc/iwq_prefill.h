@@ -34,7 +34,8 @@ hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t
 // N % 256 == 0, K % 64 == 0, per-channel or group % 64 == 0
 bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);
 // variant: 0 = default; A/B variants documented at the dispatch in iwq_prefill.hip
-hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st);
+// nib: codes in the NIB layout (variant 0 only)
+hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st, bool nib = false);
 
 // split-K form of the prefill kernel for M where the 256 x 256 tiles leave CUs idle: number of K
 // ranges for the problem (1 = no split; force > 1 overrides the rule), the fp32 workspace it needs,

@@ -2779,10 +2779,12 @@ hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t
   if (variant == 0) variant = a.M <= 32 ? 50 : (a.M <= 64 ? 52 : 53);
   switch (variant) {
     case 50: return launch_mid<2, 8, 2, 1>(a, tiled, st);
-    case 51: return launch_mid<2, 8, 1, 2>(a, tiled, st);
     case 53: return launch_mid<2, 8, 4, 2>(a, tiled, st);
+#if IWQ_AB
+    case 51: return launch_mid<2, 8, 1, 2>(a, tiled, st);
     case 54: return launch_mid<2, 8, 1, 4>(a, tiled, st);
     case 55: return launch_mid<2, 8, 2, 4>(a, tiled, st);
+#endif
     default: return launch_mid<2, 8, 2, 2>(a, tiled, st);
   }
 }
@@ -2884,9 +2886,14 @@ hipError_t prefill_splitk_launch(const PrefillArgs& a0, hipStream_t st, bool leg
   a.kps = (nk + a.nsplit - 1) / a.nsplit;
   const dim3 grid((unsigned)(tiles * a.nsplit));
   // the partials: 74's hand-ordered kernel (legacy: k_w4a16_b32e, the round-2 first version)
+#if IWQ_AB
   if (legacy && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32e<true, false, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
   else if (legacy) hipLaunchKernelGGL((k_w4a16_b32e<false, true, 2, false, false, false, true>), grid, dim3(THR), 0, st, a);
-  else if (nib && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<true, true, true>), grid, dim3(THR), 0, st, a);
+  else
+#else
+  if (legacy) return hipErrorInvalidValue;
+#endif
+  if (nib && a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<true, true, true>), grid, dim3(THR), 0, st, a);
   else if (nib) hipLaunchKernelGGL((k_w4a16_b32w<true, false, true>), grid, dim3(THR), 0, st, a);
   else if (a.gpr != 1) hipLaunchKernelGGL((k_w4a16_b32w<false, true, true>), grid, dim3(THR), 0, st, a);
   else hipLaunchKernelGGL((k_w4a16_b32w<false, false, true>), grid, dim3(THR), 0, st, a);
@@ -2943,7 +2950,17 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
 // 44 exact + interleave, 45 early barrier factored, 46 early barrier exact, 47 / 48 the same on
 // 16x16x32, 49 = 41; grouped: 40, 41 and 49 plain, 42/43 interleave / setprio, 45 early barrier,
 // 47 16x16x32.
-hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st) {
+hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st, bool nib) {
+  if (variant == 0) {
+    // per channel: 74 on the 16x16x32 MFMA with waves 4-7 staggered half a K-step (iwq_prefill16.hip
+    // 151, NIB twin 153: same bits; round 4: +6-11 % over 74 on q / gate / down at M = 8192,
+    // profiles/r04_ab_gemm_b16.jsonl); grouped: 74 / its NIB twin 75
+    if (a.gpr == 1 && prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, nib ? 153 : 151, st);
+    if (a.gpr == 1) return nib ? launch_w<true>(a, st) : launch_w<false>(a, st);
+    return nib ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
+  }
+#if IWQ_AB
+  if (nib) return hipErrorInvalidValue;
   if (variant >= 158 && variant <= 160) {  // A/B: grouped 150 / 157 / 151 reading group-major parameters
     if (a.gpr == 1 || !prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return hipErrorInvalidValue;
     PrefillArgs b = a;
@@ -2981,10 +2998,6 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
       default: return launch_w<false, true>(a, st);  // 74: +7-8 % over 45 (r02_ab_gemm_b32w_grouped.jsonl)
     }
   }
-  // per channel, default: 74 on the 16x16x32 MFMA with waves 4-7 staggered half a K-step
-  // (iwq_prefill16.hip, variant 151; round 4: +6-11 % over 74 on q / gate / down at M = 8192,
-  // profiles/r04_ab_gemm_b16.jsonl)
-  if (variant == 0 && prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, 151, st);
   switch (variant) {
     case 40: return launch<false, false, 0, false>(a, st);
     case 42: return launch<false, true, 1, false>(a, st);
@@ -3034,6 +3047,9 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st)
     case 81: return launch_w4b<true>(a, st);            // the same on NIB codes
     default: return launch_w<false>(a, st);
   }
+#else
+  return hipErrorInvalidValue;  // A/B variants: IWQ_AB builds only
+#endif
 }
 
 }  // namespace iwq

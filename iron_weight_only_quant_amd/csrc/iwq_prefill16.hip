@@ -727,6 +727,12 @@ bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const dim3 grid((unsigned)blocks), blk(THR);
+  if (a.gpr == 1 && (variant == 151 || variant == 153)) {  // the product forms
+    if (variant == 153) hipLaunchKernelGGL((k_w4a16_b16w<true, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a);
+    return hipGetLastError();
+  }
+#if IWQ_AB
   if (a.gpr != 1) {
     switch (variant) {
       case 150: hipLaunchKernelGGL((k_w4a16_b16w<false, false, 16, 0, true>), grid, blk, 0, st, a); break;
@@ -740,8 +746,7 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
   switch (variant) {
     case 150: hipLaunchKernelGGL((k_w4a16_b16w<false>), grid, blk, 0, st, a); break;
     case 152: hipLaunchKernelGGL((k_w4a16_b16w<false, true>), grid, blk, 0, st, a); break;
-    case 153: hipLaunchKernelGGL((k_w4a16_b16w<true, true>), grid, blk, 0, st, a); break;
-    case 154: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 8>), grid, blk, 0, st, a); break;    // A/B
+    case 154: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 8>), grid, blk, 0, st, a); break;
     case 155: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 1>), grid, blk, 0, st, a); break;
     case 156: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 2>), grid, blk, 0, st, a); break;
     case 162: hipLaunchKernelGGL((k_w4a16_b16q<false>), grid, dim3(256), 0, st, a); break;
@@ -752,6 +757,9 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
     default: hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a); break;
   }
   return hipGetLastError();
+#else
+  return hipErrorInvalidValue;  // A/B forms: IWQ_AB builds only
+#endif
 }
 
 }  // namespace iwq

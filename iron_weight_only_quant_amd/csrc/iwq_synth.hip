@@ -85,7 +85,11 @@ int iwq_selftest_division(uint64_t* d_counts, void* stream) {
 }
 
 const char* iwq_build_info(void) {
-  return "iwq 0.1 gfx950 (-O3 -ffp-contract=off, IEEE fp32 div, denormals preserved)";
+#if IWQ_AB
+  return "iwq 0.1 gfx950 (-O3 -ffp-contract=off, IEEE fp32 div, denormals preserved) ab=1";
+#else
+  return "iwq 0.1 gfx950 (-O3 -ffp-contract=off, IEEE fp32 div, denormals preserved) ab=0";
+#endif
 }
 
 }  // extern "C"

@@ -18,6 +18,26 @@ DEV = "cuda:0"
 TD = {"float16": torch.float16, "bfloat16": torch.bfloat16, "float32": torch.float32}
 
 
+def _ab_built():
+    try:
+        from iron_weight_only_quant_amd import _lib
+        return _lib.ab_built()
+    except OSError:
+        return False
+
+
+# The A/B kernel variants (flags bits 16..23 no default path takes) live in the IWQ_AB library only
+# (IWQ_AB=1: iron_weight_only_quant_amd/build.py --ab, _lib/libiwq_ab.so); their bit-identity checks
+# run there.  The product library refuses them (IWQ_ERR_ARG), tested below.
+AB = _ab_built()
+needs_ab = pytest.mark.skipif(not AB, reason="A/B kernel variants: IWQ_AB=1 library")
+
+
+def abv(*vs):
+    """The A/B variants vs, in an IWQ_AB build; none otherwise."""
+    return tuple(vs) if AB else ()
+
+
 def to_dev(a, dtype):
     a = np.ascontiguousarray(a)
     if dtype == "bfloat16":
@@ -43,6 +63,28 @@ def test_native_library_is_loaded(K):
     lib = _lib.load()
     assert os.path.exists(_lib.LIB_PATH)
     assert b"gfx950" in lib.iwq_build_info()
+
+
+def test_product_library_refuses_ab_variants(K):
+    """The product library answers an A/B variant with IWQ_ERR_ARG (no silent default); the pinned
+    ones (gemm fallbacks 1 / 2 at M > 16, per-tensor 6 / 9) run."""
+    if AB:
+        pytest.skip("IWQ_AB library: every variant is built")
+    from iron_weight_only_quant_amd import _lib as L
+    w = torch.empty(256, 512, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 3)
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = torch.randn(32, 512, device=DEV).half()
+    for v in (3, 45, 74, 150, 162):
+        with pytest.raises(L.IwqError) as e:
+            K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, 256, flags=K.gemm_variant_flags(v))
+        assert e.value.status == L.IWQ_ERR_ARG, v
+    for v in (1, 2):
+        K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, 256, flags=K.gemm_variant_flags(v))
+    with pytest.raises(L.IwqError):
+        K.quantize_minmax(w, 4, 128, False, 0, flags=K.gemm_variant_flags(3))
+    for v in (6, 9):
+        K.quantize_minmax(w, 4, -1, False, 0, flags=K.gemm_variant_flags(v)).settle()
 
 
 def test_division_selftest(K):
@@ -565,7 +607,7 @@ def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     # default (decode kernel for M <= 16), the tiled prefill kernel, and every decode variant
-    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in range(1, 18) if M <= 16):
+    for flags in (0, 1) + tuple(K.gemm_variant_flags(v) for v in abv(*range(1, 18)) if M <= 16):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, bits, group, N, b, flags=flags)
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (flags, float(err.max()))
@@ -588,7 +630,7 @@ def test_gemv_persistent_many_groups(K, Kd, M):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    for v in (0, 14, 15, 16, 17):
+    for v in (0,) + abv(14, 15, 16, 17):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, 128, N, b, flags=K.gemm_variant_flags(v))
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (v, float(err.max()))
@@ -616,7 +658,7 @@ def test_gemv_tiled_layout_identical(K, group):
     # number (18-20 have the default's S = 8); out= writes in place
     x = (torch.randn(5, Kd, device=DEV) * 0.5).half()
     y = torch.empty(5, N, dtype=torch.float16, device=DEV)
-    for v in (1, 2, 4, 5, 7, 8, 9, 10, 12, 13, 18, 19, 20, 21, 22, 23, 24):
+    for v in abv(1, 2, 4, 5, 7, 8, 9, 10, 12, 13, 18, 19, 20, 21, 22, 23, 24):
         rv = v if v in (2, 4, 5, 7, 8, 9, 10, 12, 13) else (2 if v == 1 else 0)
         y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(rv))
         y1 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v),
@@ -648,10 +690,14 @@ def test_gemv_tiled_layout_identical(K, group):
     t3 = K.tile_codes(r3.codes, N3, K3)
     for m in (1, 3):
         x = (torch.randn(m, K3, device=DEV) * 0.5).half()
+        y_rm = K.w4a16_gemm(x, r3.codes, r3.scales, r3.zeros, 4, group, N3)
         for codes, tl in ((r3.codes, False), (t3, True)):
-            ref = K.w4a16_gemm(x, codes, r3.scales, r3.zeros, 4, group, N3, flags=K.gemm_variant_flags(13), tiled=tl)
             y = K.w4a16_gemm(x, codes, r3.scales, r3.zeros, 4, group, N3, tiled=tl)
-            assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), (m, tl)
+            assert torch.equal(y_rm.view(torch.int16), y.view(torch.int16)), (m, tl)
+            if AB:
+                ref = K.w4a16_gemm(x, codes, r3.scales, r3.zeros, 4, group, N3, flags=K.gemm_variant_flags(13),
+                                   tiled=tl)
+                assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), (m, tl)
             want = x.float() @ r3.out.float().t()
             torch.testing.assert_close(y.float(), want, rtol=2e-2, atol=2e-2)
     # M = 2 with X over the LDS budget (K = 16384): two column tiles per wave, same bits as variant 18
@@ -662,14 +708,20 @@ def test_gemv_tiled_layout_identical(K, group):
     del w4
     t4 = K.tile_codes(r4.codes, N4, K4)
     x = (torch.randn(2, K4, device=DEV) * 0.5).half()
+    y_rm = K.w4a16_gemm(x, r4.codes, r4.scales, r4.zeros, 4, group, N4)
+    torch.testing.assert_close(y_rm.float(), x.float() @ r4.out.float().t(), rtol=2e-2, atol=2e-2)
     for codes, tl in ((r4.codes, False), (t4, True)):
-        ref = K.w4a16_gemm(x, codes, r4.scales, r4.zeros, 4, group, N4, flags=K.gemm_variant_flags(18), tiled=tl)
         y = K.w4a16_gemm(x, codes, r4.scales, r4.zeros, 4, group, N4, tiled=tl)
-        assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), tl
+        assert torch.equal(y_rm.view(torch.int16), y.view(torch.int16)), tl
+        if AB:
+            ref = K.w4a16_gemm(x, codes, r4.scales, r4.zeros, 4, group, N4, flags=K.gemm_variant_flags(18), tiled=tl)
+            assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), tl
     del r4, t4
     for m in (1, 4, 9, 16):
         x = (torch.randn(m, K2, device=DEV) * 0.5).half()
-        ref = K.w4a16_gemm(x, r2.codes, r2.scales, r2.zeros, 4, group, N2, flags=K.gemm_variant_flags(18))
+        ref = K.w4a16_gemm(x, r2.codes, r2.scales, r2.zeros, 4, group, N2,
+                           flags=K.gemm_variant_flags(18 if AB else 0))
+        torch.testing.assert_close(ref.float(), x.float() @ r2.out.float().t(), rtol=2e-2, atol=2e-2)
         for codes, tl in ((r2.codes, False), (t2, True)):
             y = K.w4a16_gemm(x, codes, r2.scales, r2.zeros, 4, group, N2, tiled=tl)
             assert torch.equal(ref.view(torch.int16), y.view(torch.int16)), (m, tl)
@@ -684,7 +736,7 @@ def test_w4a16_gemm_identity_layout(K):
     y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
     assert torch.equal(y, r.out.t().contiguous())
     for m in (1, 5, 16):  # decode kernels: rows of the identity pick weight columns exactly
-        for v in list(range(0, 18)) + [21, 22, 23, 24]:
+        for v in (0,) + abv(*range(1, 18), 21, 22, 23, 24):
             y = K.w4a16_gemm(x[:m].contiguous(), r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
             assert torch.equal(y, r.out.t()[:m].contiguous()), (m, v)
 
@@ -775,7 +827,7 @@ def test_per_tensor_fast_path(K, dtype):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
         # + pair variants 1 (non-temporal), 3 (apply walks backwards), 4 / 5 (apply unrolled), 6 (the
         # pair forced), one-pass variant 7 (NV vectors per thread)
-        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4, 5, 6, 7)]:
+        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (6,) + abv(1, 3, 4, 5, 7)]:
             r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
             assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
             assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)
@@ -843,7 +895,7 @@ def test_quant_dim1_register_kernel(K, dtype):
     for g in (32, 64, 128, 256):
         for bits, sym in ((4, False), (8, True), (3, False)):
             exp = O.quantlinear_int(x, bits, g, sym, 1, dtype)
-            for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (1, 3, 4)]:
+            for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in abv(1, 3, 4)]:
                 r = K.quantize_minmax(xd, bits, g, sym, 1, want_codes=True, flags=flags)
                 assert bits_equal(to_np(r.out), exp.dequant), (g, bits, sym, flags)
                 assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (g, bits, sym, flags)
@@ -874,7 +926,7 @@ def test_w4a16_prefill_big_tile(K, M, sym, group):
     # variant 2: the round-1 k_w4a16_big (the default is iwq_prefill.hip since round 2)
     y_big = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(2))
     assert bool(((y_big.float() - ref).abs() <= tol).all())
-    if group == -2:
+    if group == -2 and AB:
         for v in (24,):  # k-slice-outer: same BK, same accumulation order as k_w4a16_big
             yv = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
             assert torch.equal(yv, y_big), v
@@ -918,6 +970,42 @@ def nib_layout(codes, N, K):
 B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45, 152: 150, 153: 151, 163: 162}
 
 
+@pytest.mark.parametrize("M", [300, 512, 1024])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("group", [-2, 128, 64])
+def test_w4a16_prefill_default(K, M, sym, group):
+    """The product prefill path (default dispatch, row-major and NIB codes, with and without the split-K
+    workspace) vs an fp32 GEMM on the bit-exact dequantized weight; both code layouts give the same
+    bits wherever they take the same kernel."""
+    N, Kd = 512, 4352
+    torch.manual_seed(2)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 93)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    nib = K.nib_codes(r.codes, N, Kd)
+    y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
+    assert bool(((y0.float() - ref).abs() <= tol).all()), float((y0.float() - ref).abs().max())
+    assert torch.equal(y0, K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, nib=True))
+    # without a workspace (iwq_w4a16_gemm): the unsplit kernels, row-major and NIB, same bits
+    L = K.L
+    lib = L.load()
+    ys = []
+    for cd, fl in ((r.codes, 0), (nib, L.IWQ_FLAG_NIB_CODES)):
+        y1 = torch.empty(M, N, dtype=torch.float16, device=DEV)
+        st = lib.iwq_w4a16_gemm(L.ptr(x), M, Kd, Kd, L.ptr(cd), L.ptr(r.scales), L.ptr(r.zeros), 4, group, N,
+                                L.ptr(b), L.ptr(y1), N, fl, L.stream_handle(x.device))
+        assert st == 0, st
+        assert bool(((y1.float() - ref).abs() <= tol).all())
+        ys.append(y1)
+    if M >= 512:  # below, a row-major call without the split's workspace takes the mid-M kernel
+        assert torch.equal(ys[0], ys[1])
+
+
+@needs_ab
 @pytest.mark.parametrize("M", [300, 512, 1024])
 @pytest.mark.parametrize("sym", [False, True])
 @pytest.mark.parametrize("group", [-2, 128, 64])
@@ -988,13 +1076,13 @@ def test_w4a16_nib_default(K, M, group):
     y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
     y1 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, nib=True)
     assert torch.equal(y0, y1)
-    # without a workspace the NIB path runs unsplit: 74 vs 75 on the same shapes
-    y74 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(74))
-    y75 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(75))
-    assert torch.equal(y74, y75)
-    y151 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(151))
-    y153 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(153))
-    assert torch.equal(y151, y153)
+    if AB:  # without a workspace the NIB path runs unsplit: 74 vs 75, 151 vs 153 on the same shapes
+        y74 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(74))
+        y75 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(75))
+        assert torch.equal(y74, y75)
+        y151 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(151))
+        y153 = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(153))
+        assert torch.equal(y151, y153)
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     assert bool(((y1.float() - ref).abs() <= tol).all())
@@ -1064,7 +1152,7 @@ def test_w4a16_prefill_splitk(K, M, sym, group):
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     ys = {}
-    for v in (0, 82, 84, 88, 95, 96):
+    for v in (0,) + abv(82, 84, 88, 95, 96):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (v, float(err.max()))
@@ -1073,10 +1161,10 @@ def test_w4a16_prefill_splitk(K, M, sym, group):
         ys[v] = y
     # partials from the hand-ordered kernel (default) and the first split kernel (96): same k order,
     # same reduce -> same bits (below M = 256 this small weight takes the mid-M kernel by default)
-    if M >= 256:
+    if M >= 256 and AB:
         assert torch.equal(ys[0], ys[96])
     xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
-    for v in (84, 95):
+    for v in (0,) + abv(84, 95):
         y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, r.out[:, :M].t().contiguous()), v
 
@@ -1096,14 +1184,14 @@ def test_w4a16_short_tile_split(K, M, group):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    for v in (110, 112, 117, 130, 132, 140):
+    for v in (0,) + abv(110, 112, 117, 130, 132, 140):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (v, float(err.max()))
         y2 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y2), v
     xi = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
-    for v in (112, 132):
+    for v in (0,) + abv(112, 132):
         y = K.w4a16_gemm(xi, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, r.out[:, :M].t().contiguous()), v
 
@@ -1123,13 +1211,15 @@ def test_w4a16_midm_split_default(K):
     ref = x.float() @ r.out.float().t()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
     y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N)
-    y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(130))
-    assert torch.equal(y0, y4)
     assert bool(((y0.float() - ref).abs() <= tol).all())
     x2 = (torch.randn(200, Kd, device=DEV) * 0.5).half()
     z0 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N)
-    z4 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
-    assert torch.equal(z0, z4)
+    torch.testing.assert_close(z0.float(), x2.float() @ r.out.float().t(), rtol=2e-2, atol=2e-2)
+    if AB:
+        y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(130))
+        assert torch.equal(y0, y4)
+        z4 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
+        assert torch.equal(z0, z4)
 
 
 def test_w4a16_splitk_workspace_rule(K):
@@ -1168,7 +1258,7 @@ def test_w4a16_prefill_b32_identity(K, group):
     w[:, 128:256] *= 0.25  # a different scale per group along k
     r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
     x = torch.eye(Kd, device=DEV, dtype=torch.float16)
-    for v in B32_ALL:
+    for v in (0,) + abv(*B32_ALL):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, r.out.t().contiguous()), v
 
@@ -1187,6 +1277,10 @@ def test_w4a16_prefill_short_k(K, Kd):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b)
+    assert bool(((y0.float() - ref).abs() <= tol).all())
+    if not AB:
+        return
     y45 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(45))
     assert bool(((y45.float() - ref).abs() <= tol).all())
     for v in (70, 74, 76, 78, 79, 80):
@@ -1223,7 +1317,7 @@ def test_w4a16_mid(K, M, sym, group):
     b = (torch.randn(N, device=DEV) * 0.1).half()
     ref = x.float() @ r.out.float().t() + b.float()
     tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
-    for v in MID_VARIANTS + (0,):
+    for v in abv(*MID_VARIANTS) + (0,):
         y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
         err = (y.float() - ref).abs()
         assert bool((err <= tol).all()), (v, float(err.max()))
@@ -1237,6 +1331,6 @@ def test_w4a16_mid_identity(K):
         r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
         for M in (48, 130):
             x = torch.eye(Kd, device=DEV, dtype=torch.float16)[:M].contiguous()
-            for v in MID_VARIANTS:
+            for v in (0,) + abv(*MID_VARIANTS):
                 y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
                 assert torch.equal(y, r.out.t()[:M].contiguous()), (group, M, v)

@@ -33,7 +33,7 @@ SOURCES = ("iwq_prefill.hip", "iwq_prefill16.hip")
 
 def compile_asm(out, src="iwq_prefill.hip"):
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-           "--offload-device-only", "-S", os.path.join(CSRC, src), "-I", CSRC, "-o", out]
+           "-DIWQ_AB=1", "--offload-device-only", "-S", os.path.join(CSRC, src), "-I", CSRC, "-o", out]  # every variant
     subprocess.run(cmd, check=True, capture_output=True)
 
 
@@ -157,7 +157,7 @@ def store_hazard_all():
                 continue
             out = os.path.join(d, f + ".s")
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
-                            "-ffp-contract=off", "--offload-device-only", "-S", os.path.join(CSRC, f),
+                            "-ffp-contract=off", "-DIWQ_AB=1", "--offload-device-only", "-S", os.path.join(CSRC, f),
                             "-I", CSRC, "-o", out], check=True, capture_output=True)
             found = check_store_hazard(open(out).read().split("\n"))
             bad += len(found)
