@@ -2967,11 +2967,12 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st,
     b.pgm = 1;
     return prefill16_launch(b, variant == 158 ? 150 : (variant == 159 ? 157 : 151), st);
   }
-  // 161 diagnostic; 162 / 163: one wave per SIMD (k_w4a16_b16q), per channel (grouped: 151 / 153)
-  if (variant >= 161 && variant <= 163) {
-    if (a.gpr != 1) variant = variant == 163 ? 153 : 151;
-    else if (prefill16_supported(a.M, a.N, a.K, 1, a.group)) return prefill16_launch(a, variant, st);
-    else return launch_w<false>(a, st);
+  // 161 diagnostic (per channel; grouped: 151); 162 / 163 (164 / 165 interleaved): one wave per SIMD
+  // (k_w4a16_b16q), NIB codes for the odd ones
+  if (variant == 161 && a.gpr != 1) variant = 151;
+  if (variant >= 161 && variant <= 165) {
+    if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);
+    return (variant & 1) ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }
   if (variant >= 150 && variant <= 157) {
     if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);  // iwq_prefill16.hip

@@ -447,19 +447,29 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
 // (~1024 of the 2048 LDS-array cycles the K-step's MFMAs take at 256 B/clk); here 128 KiB.  Each
 // weight is still dequantized once per workgroup (one pair of 2 per group of four MFMAs).  The 256
 // accumulators per lane sit in AGPRs (hipBLASLt's MT256x256x64_MI16x16 kernel for these shapes runs the
-// same one-wave-per-SIMD shape).  4-slot ring (160 KiB): the barrier sits early in slice 1 (after the
-// group that consumes fragment 3), publishes the next stage and frees the slot of the stage before the
-// running one (all its reads retired a K-step ago), which is refilled right after.
+// same one-wave-per-SIMD shape).
+// Rings: X in 4 slots of 32 KiB, codes (+ grouped parameters) in 3 slots of 8 (10) KiB: 152 (158) KiB.
+// The barrier sits early in slice 1 (after the group that consumes fragment 3) and publishes the next
+// stage; after it the X slot of the stage before the running one and the code slot of the running
+// one (its codes were read a K-step ago) are refilled with K-step kt + 3.
 // Per K-step and wave: slice 0 -- 16 groups of (wait, 4 MFMAs, rolling A read 4 fragments ahead, one
-// weight pair of slice 1's B); slice 1 -- groups 0-3, the barrier, the next stage's codes, 10 DMA
-// pieces spread over groups 4-13, the next stage's slice-0 B dequantized over groups 8-15.
-template <bool NIB>
+// weight pair of slice 1's B); slice 1 -- groups 0-3, the barrier, the next stage's codes (and
+// parameters), the DMA pieces spread one per group from group 4, the next stage's slice-0 B
+// dequantized over groups 8-15.
+// IL: the work of a group (rolling read, DMA piece, dequant pairs) placed between its four MFMAs (one
+// slot after each) instead of after the fourth, so the MFMA pipe is not left idle while one wave
+// issues it.
+// GROUPED (group % 64 == 0): one (s, z) per column per K-step, staged with the codes (b16w's parameter
+// image), applied per weight (RN16((q - z) s)), no epilogue scale.
+template <bool NIB, bool IL = false, bool GROUPED = false>
 __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
-  constexpr int NSTQ = 4;
-  constexpr int STAGE = XS + CS;  // 40 KiB
-  constexpr int PIECES = 10;      // DMA pieces per wave per K-step: 8 of X rows, 2 of codes
+  constexpr int NSX = 4, NSC = 3;             // X / code ring slots
+  constexpr int CST = CS + (GROUPED ? PS : 0);  // code slot bytes
+  constexpr int CBASE = NSX * XS;             // code ring offset (128 KiB)
+  constexpr int PIECES = GROUPED ? 12 : 10;   // DMA pieces per wave per K-step: 8 X, 2 codes, 2 parameters
   constexpr int VM_AHEAD = PIECES;  // at a barrier the pieces of the K-step after the published one fly
-  __shared__ __attribute__((aligned(16))) uint8_t smem[NSTQ * STAGE];
+  constexpr int NCR = GROUPED ? 8 : 4;  // LDS reads of a stage's codes (+ parameters)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSX * XS + NSC * CST];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -471,7 +481,8 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   const int nk = a.K / TK;
 
   // DMA sources: X rows (wid * 8 + i) * 8 + lane / 8, 16-B chunk lane % 8 from chunk (lane % 8) ^ h;
-  // codes: column wid * 64 + 32 j + lane / 2, chunk lane % 2 from chunk (lane % 2) ^ cswz
+  // codes: column wid * 64 + 32 j + lane / 2, chunk lane % 2 from chunk (lane % 2) ^ cswz; grouped:
+  // the scale and zero point of column wid * 64 + lane (dword c / 256 + c of the parameter image)
   const _Float16* xsrc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -485,28 +496,46 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
     const int ccol = wid * 64 + 32 * j + (lane >> 1);
     csrc[j] = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
   }
-  auto issue1 = [&](int kt, int stg, int i) {
-    uint8_t* base = smem + stg * STAGE;
-    if (i < 8) glds16(xsrc[i] + kt * TK, base + (wid * 8 + i) * 1024);
-    else glds16(csrc[i - 8] + kt * (TK / 2), base + XS + (wid * 2 + i - 8) * 1024);
+  const _Float16* psrc[2] = {nullptr, nullptr};
+  int64_t pstep = 1;
+  if constexpr (GROUPED) {
+    const int64_t c = n0 + wid * 64 + lane;
+    const int64_t off = a.pgm ? c : c * a.gpr;
+    psrc[0] = a.scales + off;
+    psrc[1] = (a.zeros ? a.zeros : a.scales) + off;
+    pstep = a.pgm ? a.N : 1;
+  }
+  // piece i of K-step kt into X slot xs / code slot cs
+  auto issue1 = [&](int kt, int xs, int cs, int i) {
+    if (i < 8) {
+      glds16(xsrc[i] + kt * TK, smem + xs * XS + (wid * 8 + i) * 1024);
+    } else if (i < 10) {
+      glds16(csrc[i - 8] + kt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
+    } else if constexpr (GROUPED) {
+      glds2(psrc[i - 10] + ((kt * TK) / a.group) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+    }
   };
-  auto issue = [&](int kt, int stg) {
+  auto issue = [&](int kt, int s) {
 #pragma unroll
-    for (int i = 0; i < PIECES; ++i) issue1(kt, stg, i);
+    for (int i = 0; i < PIECES; ++i) issue1(kt, s, s, i);
   };
 
   // this lane's four columns (16-column tiles 0..3 of the wave) and their parameters
   const int col0 = n0 + wid * 64 + r16;
-  float sfl[4];
-  h2 zz[4], zl[4], zh[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int col = col0 + 16 * nt;
-    sfl[nt] = (float)gp<_Float16>(a.scales)[col];
-    const float zf = a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym;
+  float sfl[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  h2 s2[4], zz[4], zl[4], zh[4];
+  auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
     zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = col0 + 16 * nt;
+      sfl[nt] = (float)gp<_Float16>(a.scales)[col];
+      set_zero(nt, a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym);
+    }
   }
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
   const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
@@ -516,23 +545,61 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
   asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
 
-  // LDS byte addresses: A fragment (stage st, slice s, tile mt) = la[s] + st * STAGE + 2048 mt;
-  // codes of tile nt = lc + st * STAGE + 512 nt
+  // LDS byte addresses: A fragment (X slot st, slice s, tile mt) = la[s] + st * XS + 2048 mt;
+  // codes of tile nt (code slot st) = lc + st * CST + 512 nt; grouped: scales of tiles (0, 1) / (2, 3)
+  // at lps / lps + 128, zero points 1 KiB on
   const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
   uint32_t la[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
   const int ccl = wid * 64 + r16;
-  const uint32_t lc = lbase + XS + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+  const uint32_t lc = lbase + CBASE + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+  const uint32_t lps = lbase + CBASE + CS + (uint32_t)(ccl * 4);
+  u32x2 pv[4];  // grouped: raw parameter dwords (scales of tiles 0/1, 2/3; zero points of 0/1, 2/3)
+  auto set_params = [&](int nt) {
+    if constexpr (GROUPED) {
+      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
+      s2[nt] = h2{sc, sc};
+      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+    }
+  };
+  // the code (+ parameter) reads of code slot offset CO into W / pv, in this order
+  auto read_codes = [&](u32x2* w, uint32_t co) {
+    w[0] = lds_rd2<0>(lc + co);
+    w[1] = lds_rd2<512>(lc + co);
+    w[2] = lds_rd2<1024>(lc + co);
+    w[3] = lds_rd2<1536>(lc + co);
+    if constexpr (GROUPED) {
+      pv[0] = lds_rd_pair(lps + co);
+      pv[1] = lds_rd_pair(lps + co + 128);
+      pv[2] = lds_rd_pair(lps + co + 1024);
+      pv[3] = lds_rd_pair(lps + co + 1152);
+    }
+  };
+  auto codes_landed = [&](u32x2* w) {
+    landed(w[0]);
+    landed(w[1]);
+    landed(w[2]);
+    landed(w[3]);
+    if constexpr (GROUPED) {
+      landed(pv[0]);
+      landed(pv[1]);
+      landed(pv[2]);
+      landed(pv[3]);
+    }
+  };
 
   auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    h2 d;
     if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      return (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
-      return as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+      d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
     }
+    if constexpr (GROUPED) d = d * s2[nt];  // RN16((q - z) s)
+    return d;
   };
   auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
 
@@ -546,116 +613,134 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   u32x2 wc[4];      // the running K-step's code dwords per tile: .x slice 0, .y slice 1
 
 #define IWQ_RD(MT, ADDR) af[(MT) & 7] = lds_rd<((MT) & 15) * 2048>(ADDR)
-#define IWQ_MF4(MT, B)                                                                        \
-  acc[MT][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[0], acc[MT][0], 0, 0, 0); \
-  acc[MT][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[1], acc[MT][1], 0, 0, 0); \
-  acc[MT][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[2], acc[MT][2], 0, 0, 0); \
-  acc[MT][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[3], acc[MT][3], 0, 0, 0)
+#define IWQ_LGKMN(N) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory")
+#define IWQ_MF1(MT, NT, B) \
+  acc[MT][NT] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[NT], acc[MT][NT], 0, 0, 0)
   // group MT of a slice: the wait for its fragment (N newer LDS reads may stay in flight), its four
-  // MFMAs, then the rolling read (READ) and VALU / DMA work (WORK)
-#define IWQ_GRP(MT, N, B, READ, WORK) \
-  {                                   \
-    IWQ_LGKM(N);                      \
-    IWQ_PIN();                        \
-    IWQ_MF4(MT, B);                   \
-    READ;                             \
-    WORK;                             \
-    IWQ_PIN();                        \
+  // MFMAs and the work slots W0..W3 (in this order; IL: W_i right after MFMA i)
+#define IWQ_GRP(MT, N, B, W0, W1, W2, W3) \
+  {                                       \
+    IWQ_LGKMN(N);                         \
+    IWQ_PIN();                            \
+    if constexpr (IL) {                   \
+      IWQ_MF1(MT, 0, B);                  \
+      W0;                                 \
+      IWQ_PIN();                          \
+      IWQ_MF1(MT, 1, B);                  \
+      W1;                                 \
+      IWQ_PIN();                          \
+      IWQ_MF1(MT, 2, B);                  \
+      W2;                                 \
+      IWQ_PIN();                          \
+      IWQ_MF1(MT, 3, B);                  \
+      W3;                                 \
+    } else {                              \
+      IWQ_MF1(MT, 0, B);                  \
+      IWQ_MF1(MT, 1, B);                  \
+      IWQ_MF1(MT, 2, B);                  \
+      IWQ_MF1(MT, 3, B);                  \
+      W0;                                 \
+      W1;                                 \
+      W2;                                 \
+      W3;                                 \
+    }                                     \
+    IWQ_PIN();                            \
   }
-  // slice 0 (stage offset SO): rolling reads of fragments 4..15 of slice 0 and 0..3 of slice 1;
+  // slice 0 (X slot offset SO): rolling reads of fragments 4..15 of slice 0 and 0..3 of slice 1;
   // slice 1's B (the same code dwords' .y) dequantized one pair per group
-#define IWQ_QSLICE0(SO)                                                            \
-  {                                                                                \
-    const uint32_t a0 = la[0] + (SO), a1 = la[1] + (SO);                           \
-    h2 p[16];                                                                      \
-    IWQ_GRP(0, 3, b0, IWQ_RD(4, a0), p[0] = dqp(wc[0].y, 0, 0));                   \
-    IWQ_GRP(1, 3, b0, IWQ_RD(5, a0), p[1] = dqp(wc[0].y, 1, 0));                   \
-    IWQ_GRP(2, 3, b0, IWQ_RD(6, a0), p[2] = dqp(wc[0].y, 2, 0));                   \
-    IWQ_GRP(3, 3, b0, IWQ_RD(7, a0), p[3] = dqp(wc[0].y, 3, 0));                   \
-    IWQ_GRP(4, 3, b0, IWQ_RD(8, a0), p[4] = dqp(wc[1].y, 0, 1));                   \
-    IWQ_GRP(5, 3, b0, IWQ_RD(9, a0), p[5] = dqp(wc[1].y, 1, 1));                   \
-    IWQ_GRP(6, 3, b0, IWQ_RD(10, a0), p[6] = dqp(wc[1].y, 2, 1));                  \
-    IWQ_GRP(7, 3, b0, IWQ_RD(11, a0), p[7] = dqp(wc[1].y, 3, 1));                  \
-    IWQ_GRP(8, 3, b0, IWQ_RD(12, a0), p[8] = dqp(wc[2].y, 0, 2));                  \
-    IWQ_GRP(9, 3, b0, IWQ_RD(13, a0), p[9] = dqp(wc[2].y, 1, 2));                  \
-    IWQ_GRP(10, 3, b0, IWQ_RD(14, a0), p[10] = dqp(wc[2].y, 2, 2));                \
-    IWQ_GRP(11, 3, b0, IWQ_RD(15, a0), p[11] = dqp(wc[2].y, 3, 2));                \
-    IWQ_GRP(12, 3, b0, IWQ_RD(0, a1), p[12] = dqp(wc[3].y, 0, 3));                 \
-    IWQ_GRP(13, 3, b0, IWQ_RD(1, a1), p[13] = dqp(wc[3].y, 1, 3));                 \
-    IWQ_GRP(14, 3, b0, IWQ_RD(2, a1), p[14] = dqp(wc[3].y, 2, 3));                 \
-    IWQ_GRP(15, 3, b0, IWQ_RD(3, a1), p[15] = dqp(wc[3].y, 3, 3));                 \
-    b1[0] = frag(p);                                                               \
-    b1[1] = frag(p + 4);                                                           \
-    b1[2] = frag(p + 8);                                                           \
-    b1[3] = frag(p + 12);                                                          \
+#define IWQ_QSLICE0(SO)                                                     \
+  {                                                                         \
+    const uint32_t a0 = la[0] + (SO), a1 = la[1] + (SO);                    \
+    h2 p[16];                                                               \
+    IWQ_GRP(0, 3, b0, IWQ_RD(4, a0), p[0] = dqp(wc[0].y, 0, 0), , );         \
+    IWQ_GRP(1, 3, b0, IWQ_RD(5, a0), p[1] = dqp(wc[0].y, 1, 0), , );         \
+    IWQ_GRP(2, 3, b0, IWQ_RD(6, a0), p[2] = dqp(wc[0].y, 2, 0), , );         \
+    IWQ_GRP(3, 3, b0, IWQ_RD(7, a0), p[3] = dqp(wc[0].y, 3, 0), , );         \
+    IWQ_GRP(4, 3, b0, IWQ_RD(8, a0), p[4] = dqp(wc[1].y, 0, 1), , );         \
+    IWQ_GRP(5, 3, b0, IWQ_RD(9, a0), p[5] = dqp(wc[1].y, 1, 1), , );         \
+    IWQ_GRP(6, 3, b0, IWQ_RD(10, a0), p[6] = dqp(wc[1].y, 2, 1), , );        \
+    IWQ_GRP(7, 3, b0, IWQ_RD(11, a0), p[7] = dqp(wc[1].y, 3, 1), , );        \
+    IWQ_GRP(8, 3, b0, IWQ_RD(12, a0), p[8] = dqp(wc[2].y, 0, 2), , );        \
+    IWQ_GRP(9, 3, b0, IWQ_RD(13, a0), p[9] = dqp(wc[2].y, 1, 2), , );        \
+    IWQ_GRP(10, 3, b0, IWQ_RD(14, a0), p[10] = dqp(wc[2].y, 2, 2), , );      \
+    IWQ_GRP(11, 3, b0, IWQ_RD(15, a0), p[11] = dqp(wc[2].y, 3, 2), , );      \
+    IWQ_GRP(12, 3, b0, IWQ_RD(0, a1), p[12] = dqp(wc[3].y, 0, 3), , );       \
+    IWQ_GRP(13, 3, b0, IWQ_RD(1, a1), p[13] = dqp(wc[3].y, 1, 3), , );       \
+    IWQ_GRP(14, 3, b0, IWQ_RD(2, a1), p[14] = dqp(wc[3].y, 2, 3), , );       \
+    IWQ_GRP(15, 3, b0, IWQ_RD(3, a1), p[15] = dqp(wc[3].y, 3, 3), , );       \
+    b1[0] = frag(p);                                                        \
+    b1[1] = frag(p + 4);                                                    \
+    b1[2] = frag(p + 8);                                                    \
+    b1[3] = frag(p + 12);                                                   \
   }
 
-  // prologue: K-steps 0, 1, 2 into slots 0, 1, 2 (clamped to nk - 1: re-loads nobody reads again)
+  // prologue: K-steps 0, 1, 2 into slots 0, 1, 2 of both rings (clamped to nk - 1: re-loads nobody
+  // reads again)
   issue(0, 0);
   issue(nk > 1 ? 1 : 0, 1);
   issue(nk > 2 ? 2 : nk - 1, 2);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
   __builtin_amdgcn_s_barrier();
   IWQ_PIN();
-  wc[0] = lds_rd2<0>(lc);
-  wc[1] = lds_rd2<512>(lc);
-  wc[2] = lds_rd2<1024>(lc);
-  wc[3] = lds_rd2<1536>(lc);
+  read_codes(wc, 0);
   IWQ_RD(0, la[0]); IWQ_RD(1, la[0]); IWQ_RD(2, la[0]); IWQ_RD(3, la[0]);
   IWQ_LGKM(0);
-  landed(wc[0]);
-  landed(wc[1]);
-  landed(wc[2]);
-  landed(wc[3]);
+  codes_landed(wc);
   IWQ_PIN();
   {
     h2 p[16];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt) {
+      set_params(nt);
 #pragma unroll
       for (int j = 0; j < 4; ++j) p[4 * nt + j] = dqp(wc[nt].x, j, nt);
+    }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) b0[nt] = frag(p + 4 * nt);
   }
 
   // the last K-step is peeled (a branch in the body made the compiler keep two register images)
   for (int kt = 0; kt + 1 < nk; ++kt) {
-    const uint32_t so = (uint32_t)((kt % NSTQ) * STAGE);
-    const uint32_t sn = (uint32_t)(((kt + 1) % NSTQ) * STAGE);
-    const int sd = (kt + NSTQ - 1) % NSTQ;         // the slot of stage kt - 1, refilled after the barrier
-    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;  // ... with K-step kt + 3 (clamped: re-loads nobody reads)
+    const uint32_t so = (uint32_t)((kt % NSX) * XS);
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSX) * XS);
+    const uint32_t cn = (uint32_t)(((kt + 1) % NSC) * CST);
+    // after the barrier: X slot of stage kt - 1 and code slot of stage kt get K-step kt + 3 (clamped:
+    // re-loads nobody reads)
+    const int xd = (kt + 3) % NSX, cd = kt % NSC;
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
     IWQ_QSLICE0(so)
     const uint32_t a1 = la[1] + so;
     const uint32_t na = la[0] + sn;
-    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), );
-    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), );
-    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), );
-    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), );
-    // stage kt + 1 landed (this wave's part; K-step kt + 2's pieces may fly): publish it.  Every read
-    // of stage kt - 1 retired a K-step ago, so its slot is refilled below.
+    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), , , );
+    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), , , );
+    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), , , );
+    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), , , );
+    // stage kt + 1 landed (this wave's part; K-step kt + 2's pieces may fly): publish it
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
     __builtin_amdgcn_s_barrier();
     IWQ_PIN();
     u32x2 wn[4];
-    IWQ_GRP(4, 3, b1, wn[0] = lds_rd2<0>(lc + sn); wn[1] = lds_rd2<512>(lc + sn); wn[2] = lds_rd2<1024>(lc + sn);
-            wn[3] = lds_rd2<1536>(lc + sn); IWQ_RD(8, a1), issue1(kd, sd, 0));
-    IWQ_GRP(5, 7, b1, IWQ_RD(9, a1), issue1(kd, sd, 1));
-    IWQ_GRP(6, 7, b1, IWQ_RD(10, a1), issue1(kd, sd, 2));
-    IWQ_GRP(7, 7, b1, IWQ_RD(11, a1), issue1(kd, sd, 3));
+    // the code (+ parameter) reads of stage kt + 1 are older than fragment 8's: NCR more reads in
+    // flight at groups 5-7
+    IWQ_GRP(4, 3, b1, read_codes(wn, cn), IWQ_RD(8, a1), issue1(kd, xd, cd, 0), );
+    IWQ_GRP(5, 3 + NCR, b1, IWQ_RD(9, a1), issue1(kd, xd, cd, 1), , );
+    IWQ_GRP(6, 3 + NCR, b1, IWQ_RD(10, a1), issue1(kd, xd, cd, 2), , );
+    IWQ_GRP(7, 3 + NCR, b1, IWQ_RD(11, a1), issue1(kd, xd, cd, 3), , );
     h2 p[16];
     IWQ_LGKM(3);  // fragment 8 and everything older (the code reads) landed
-    landed(wn[0]);
-    landed(wn[1]);
-    landed(wn[2]);
-    landed(wn[3]);
-    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(kd, sd, 4); p[0] = dqp(wn[0].x, 0, 0); p[1] = dqp(wn[0].x, 1, 0));
-    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), issue1(kd, sd, 5); p[2] = dqp(wn[0].x, 2, 0); p[3] = dqp(wn[0].x, 3, 0));
-    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(kd, sd, 6); p[4] = dqp(wn[1].x, 0, 1); p[5] = dqp(wn[1].x, 1, 1));
-    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), issue1(kd, sd, 7); p[6] = dqp(wn[1].x, 2, 1); p[7] = dqp(wn[1].x, 3, 1));
-    IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(kd, sd, 8); p[8] = dqp(wn[2].x, 0, 2); p[9] = dqp(wn[2].x, 1, 2));
-    IWQ_GRP(13, 3, b1, IWQ_RD(1, na), issue1(kd, sd, 9); p[10] = dqp(wn[2].x, 2, 2); p[11] = dqp(wn[2].x, 3, 2));
-    IWQ_GRP(14, 3, b1, IWQ_RD(2, na), p[12] = dqp(wn[3].x, 0, 3); p[13] = dqp(wn[3].x, 1, 3));
-    IWQ_GRP(15, 3, b1, IWQ_RD(3, na), p[14] = dqp(wn[3].x, 2, 3); p[15] = dqp(wn[3].x, 3, 3));
+    codes_landed(wn);
+    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(kd, xd, cd, 4); set_params(0), p[0] = dqp(wn[0].x, 0, 0),
+            p[1] = dqp(wn[0].x, 1, 0));
+    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), issue1(kd, xd, cd, 5), p[2] = dqp(wn[0].x, 2, 0), p[3] = dqp(wn[0].x, 3, 0));
+    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(kd, xd, cd, 6); set_params(1), p[4] = dqp(wn[1].x, 0, 1),
+            p[5] = dqp(wn[1].x, 1, 1));
+    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), issue1(kd, xd, cd, 7), p[6] = dqp(wn[1].x, 2, 1), p[7] = dqp(wn[1].x, 3, 1));
+    IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(kd, xd, cd, 8); set_params(2), p[8] = dqp(wn[2].x, 0, 2),
+            p[9] = dqp(wn[2].x, 1, 2));
+    IWQ_GRP(13, 3, b1, IWQ_RD(1, na), issue1(kd, xd, cd, 9), p[10] = dqp(wn[2].x, 2, 2), p[11] = dqp(wn[2].x, 3, 2));
+    IWQ_GRP(14, 3, b1, IWQ_RD(2, na), issue1(kd, xd, cd, 10); set_params(3), p[12] = dqp(wn[3].x, 0, 3),
+            p[13] = dqp(wn[3].x, 1, 3));
+    IWQ_GRP(15, 3, b1, IWQ_RD(3, na), issue1(kd, xd, cd, 11), p[14] = dqp(wn[3].x, 2, 3), p[15] = dqp(wn[3].x, 3, 3));
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       b0[nt] = frag(p + 4 * nt);
@@ -664,32 +749,33 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   }
   {
     // the last K-step: no next stage, no barrier
-    const uint32_t so = (uint32_t)(((nk - 1) % NSTQ) * STAGE);
+    const uint32_t so = (uint32_t)(((nk - 1) % NSX) * XS);
     IWQ_QSLICE0(so)
     const uint32_t a1 = la[1] + so;
-    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), );
-    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), );
-    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), );
-    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), );
-    IWQ_GRP(4, 3, b1, IWQ_RD(8, a1), );
-    IWQ_GRP(5, 3, b1, IWQ_RD(9, a1), );
-    IWQ_GRP(6, 3, b1, IWQ_RD(10, a1), );
-    IWQ_GRP(7, 3, b1, IWQ_RD(11, a1), );
-    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), );
-    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), );
-    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), );
-    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), );
-    IWQ_GRP(12, 3, b1, , );
-    IWQ_GRP(13, 2, b1, , );
-    IWQ_GRP(14, 1, b1, , );
-    IWQ_GRP(15, 0, b1, , );
+    IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), , , );
+    IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), , , );
+    IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), , , );
+    IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), , , );
+    IWQ_GRP(4, 3, b1, IWQ_RD(8, a1), , , );
+    IWQ_GRP(5, 3, b1, IWQ_RD(9, a1), , , );
+    IWQ_GRP(6, 3, b1, IWQ_RD(10, a1), , , );
+    IWQ_GRP(7, 3, b1, IWQ_RD(11, a1), , , );
+    IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), , , );
+    IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), , , );
+    IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), , , );
+    IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), , , );
+    IWQ_GRP(12, 3, b1, , , , );
+    IWQ_GRP(13, 2, b1, , , , );
+    IWQ_GRP(14, 1, b1, , , , );
+    IWQ_GRP(15, 0, b1, , , , );
   }
   // no LDS-DMA may still be landing when the workgroup retires (the CU's next workgroup owns the LDS)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #undef IWQ_QSLICE0
 #undef IWQ_GRP
-#undef IWQ_MF4
+#undef IWQ_MF1
 #undef IWQ_RD
+#undef IWQ_LGKMN
 
   // epilogue: lane holds rows 16 mt + 4 g + r of columns col0 + 16 nt
   float bc[4];
@@ -706,7 +792,10 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
       if (full || m0 + rr + 4 * g < a.M) {
         auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) p[16 * nt] = (_Float16)(opaque(acc[mt][nt][r] * sfl[nt]) + bc[nt]);
+        for (int nt = 0; nt < 4; ++nt) {
+          if constexpr (GROUPED) p[16 * nt] = (_Float16)(acc[mt][nt][r] + bc[nt]);
+          else p[16 * nt] = (_Float16)(opaque(acc[mt][nt][r] * sfl[nt]) + bc[nt]);
+        }
       }
     }
 }
@@ -739,6 +828,10 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
       case 152: hipLaunchKernelGGL((k_w4a16_b16w<false, true, 16, 0, true>), grid, blk, 0, st, a); break;
       case 153: hipLaunchKernelGGL((k_w4a16_b16w<true, true, 16, 0, true, true>), grid, blk, 0, st, a); break;
       case 157: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, true, false>), grid, blk, 0, st, a); break;
+      case 162: hipLaunchKernelGGL((k_w4a16_b16q<false, false, true>), grid, dim3(256), 0, st, a); break;
+      case 163: hipLaunchKernelGGL((k_w4a16_b16q<true, false, true>), grid, dim3(256), 0, st, a); break;
+      case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true, true>), grid, dim3(256), 0, st, a); break;
+      case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true, true>), grid, dim3(256), 0, st, a); break;
       default: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, true, true>), grid, blk, 0, st, a); break;
     }
     return hipGetLastError();
@@ -751,6 +844,8 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
     case 156: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 2>), grid, blk, 0, st, a); break;
     case 162: hipLaunchKernelGGL((k_w4a16_b16q<false>), grid, dim3(256), 0, st, a); break;
     case 163: hipLaunchKernelGGL((k_w4a16_b16q<true>), grid, dim3(256), 0, st, a); break;
+    case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true>), grid, dim3(256), 0, st, a); break;
+    case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true>), grid, dim3(256), 0, st, a); break;
     case 161:  // DIAGNOSTIC: 151 without the output stores
       hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, false, false, true>), grid, blk, 0, st, a);
       break;

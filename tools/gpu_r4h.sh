@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-4 session H: one-wave-per-SIMD prefill (162-165, per channel and grouped): A/B-library parity + timing
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+run() { local name=$1 tmo=$2; shift 2; echo "=== $name"; timeout -k 10 $tmo "$@" > $OUT/$name.log 2>&1; local st=$?; tail -3 $OUT/$name.log; echo "=== $name exit $st"; return $st; }
+export IWQ_AB=1
+run t_ab_h 500 python -u -m pytest tests/test_gpu_parity.py -x -q -k "prefill_b32 or nib_default or short_k" --timeout 200 --timeout-method thread -p no:cacheprovider
+[ $? -eq 0 ] || exit 1
+run ab_h_pc 400 python tools/ab_gemm.py --variants 151,153,162,163,164,165 --rounds 7
+[ $? -eq 0 ] || exit 3
+run ab_h_g128 400 python tools/ab_gemm.py --group 128 --variants 74,150,162,163,164,165 --rounds 7
+[ $? -eq 0 ] || exit 3
+run ab_h_pc70 400 python tools/ab_gemm.py --variants 151,153,163,164,165 --shapes 70b_q,70b_gate,70b_down --rounds 5
