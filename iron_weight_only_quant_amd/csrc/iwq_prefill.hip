@@ -2968,11 +2968,13 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st,
     return prefill16_launch(b, variant == 158 ? 150 : (variant == 159 ? 157 : 151), st);
   }
   // 161 diagnostic (per channel; grouped: 151); 162 / 163 (164 / 165 interleaved): one wave per SIMD
-  // (k_w4a16_b16q), NIB codes for the odd ones
-  if (variant == 161 && a.gpr != 1) variant = 151;
-  if (variant >= 161 && variant <= 165) {
+  // (k_w4a16_b16q), NIB codes for the odd ones; 168 / 169 / 170: k_w4a16_b16r reading 4 / 6 / 6
+  // groups ahead (NIB, NIB, row-major)
+  if ((variant == 161 || variant == 166 || variant == 167) && a.gpr != 1) variant = 151;  // diagnostics
+  if (variant >= 161 && variant <= 170) {
     if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);
-    return (variant & 1) ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
+    const bool nibv = variant == 163 || variant == 165 || variant == 168 || variant == 169;
+    return nibv ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }
   if (variant >= 150 && variant <= 157) {
     if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);  // iwq_prefill16.hip

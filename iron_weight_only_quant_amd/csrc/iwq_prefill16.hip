@@ -461,7 +461,9 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
 // issues it.
 // GROUPED (group % 64 == 0): one (s, z) per column per K-step, staged with the codes (b16w's parameter
 // image), applied per weight (RN16((q - z) s)), no epilogue scale.
-template <bool NIB, bool IL = false, bool GROUPED = false>
+// DIAG (DIAGNOSTIC, wrong results): 1 = no barrier in the loop (its cost), 2 = no dequant VALU (the
+// code dwords go to the MFMA as they are)
+template <bool NIB, bool IL = false, bool GROUPED = false, int DIAG = 0>
 __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   constexpr int NSX = 4, NSC = 3;             // X / code ring slots
   constexpr int CST = CS + (GROUPED ? PS : 0);  // code slot bytes
@@ -591,7 +593,9 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
 
   auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
     h2 d;
-    if constexpr (NIB) {
+    if constexpr (DIAG == 2) {
+      return as_h2(j & 1 ? w >> 1 : w);
+    } else if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
       d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
     } else {
@@ -717,7 +721,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
     IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), , , );
     // stage kt + 1 landed (this wave's part; K-step kt + 2's pieces may fly): publish it
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (DIAG != 1) __builtin_amdgcn_s_barrier();
     IWQ_PIN();
     u32x2 wn[4];
     // the code (+ parameter) reads of stage kt + 1 are older than fragment 8's: NCR more reads in
@@ -800,6 +804,320 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
     }
 }
 
+// k_w4a16_b16r: k_w4a16_b16q (one wave per SIMD, IL work slots) with the rolling A reads D groups
+// ahead instead of 4 (D - 1 reads in flight at every MFMA group; the fragment ring holds 8), written
+// with compile-time group indices.  The next stage's slice-0 dequant then runs over groups D + 4 .. 15.
+template <int I>
+struct ic {
+  static constexpr int v = I;
+};
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(ic<B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+template <bool NIB, int D, bool GROUPED = false>
+__global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
+  static_assert(D >= 2 && D <= 7, "fragment ring of 8");
+  constexpr int NSX = 4, NSC = 3;
+  constexpr int CST = CS + (GROUPED ? PS : 0);
+  constexpr int CBASE = NSX * XS;
+  constexpr int PIECES = GROUPED ? 12 : 10;
+  constexpr int VM_AHEAD = PIECES;
+  constexpr int NCR = GROUPED ? 8 : 4;
+  static_assert(4 + PIECES <= 16, "DMA pieces fit groups 4..15");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSX * XS + NSC * CST];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int tiles_n = a.N / TN;
+  const int64_t t = swizzled_block(blockIdx.x, (int64_t)gridDim.x);
+  const int m0 = (int)(t / tiles_n) * TM, n0 = (int)(t % tiles_n) * TN;
+  const int64_t crow = a.K / 2;
+  const int nk = a.K / TK;
+
+  const _Float16* xsrc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = (wid * 8 + i) * 8 + (lane >> 3);
+    const int gm = m0 + row < a.M ? m0 + row : a.M - 1;
+    xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3);
+  }
+  const uint8_t* csrc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int ccol = wid * 64 + 32 * j + (lane >> 1);
+    csrc[j] = a.codes + (int64_t)(n0 + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+  }
+  const _Float16* psrc[2] = {nullptr, nullptr};
+  int64_t pstep = 1;
+  if constexpr (GROUPED) {
+    const int64_t c = n0 + wid * 64 + lane;
+    const int64_t off = a.pgm ? c : c * a.gpr;
+    psrc[0] = a.scales + off;
+    psrc[1] = (a.zeros ? a.zeros : a.scales) + off;
+    pstep = a.pgm ? a.N : 1;
+  }
+  auto issue1 = [&](int kt, int xs, int cs, int i) {
+    if (i < 8) {
+      glds16(xsrc[i] + kt * TK, smem + xs * XS + (wid * 8 + i) * 1024);
+    } else if (i < 10) {
+      glds16(csrc[i - 8] + kt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
+    } else if constexpr (GROUPED) {
+      glds2(psrc[i - 10] + ((kt * TK) / a.group) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+    }
+  };
+  auto issue = [&](int kt, int s) {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) issue1(kt, s, s, i);
+  };
+
+  const int col0 = n0 + wid * 64 + r16;
+  float sfl[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  h2 s2[4], zz[4], zl[4], zh[4];
+  auto set_zero = [&](int nt, float zf) {
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  if constexpr (!GROUPED) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = col0 + 16 * nt;
+      sfl[nt] = (float)gp<_Float16>(a.scales)[col];
+      set_zero(nt, a.zeros ? (float)gp<_Float16>(a.zeros)[col] : a.zsym);
+    }
+  }
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
+  const int ccl = wid * 64 + r16;
+  const uint32_t lc = lbase + CBASE + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+  const uint32_t lps = lbase + CBASE + CS + (uint32_t)(ccl * 4);
+  u32x2 pv[4];
+  auto set_params = [&](int nt) {
+    if constexpr (GROUPED) {
+      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
+      s2[nt] = h2{sc, sc};
+      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+    }
+  };
+  auto read_codes = [&](u32x2* w, uint32_t co) {
+    w[0] = lds_rd2<0>(lc + co);
+    w[1] = lds_rd2<512>(lc + co);
+    w[2] = lds_rd2<1024>(lc + co);
+    w[3] = lds_rd2<1536>(lc + co);
+    if constexpr (GROUPED) {
+      pv[0] = lds_rd_pair(lps + co);
+      pv[1] = lds_rd_pair(lps + co + 128);
+      pv[2] = lds_rd_pair(lps + co + 1024);
+      pv[3] = lds_rd_pair(lps + co + 1152);
+    }
+  };
+  auto codes_landed = [&](u32x2* w) {
+    landed(w[0]);
+    landed(w[1]);
+    landed(w[2]);
+    landed(w[3]);
+    if constexpr (GROUPED) {
+      landed(pv[0]);
+      landed(pv[1]);
+      landed(pv[2]);
+      landed(pv[3]);
+    }
+  };
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    h2 d;
+    if constexpr (NIB) {
+      const uint32_t t = j >= 2 ? w >> 8 : w;
+      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+    if constexpr (GROUPED) d = d * s2[nt];
+    return d;
+  };
+  auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
+
+  f4 acc[16][4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 af[8];
+  h8 b0[4], b1[4];
+  u32x2 wc[4];
+
+  // fragment F (0..31: slice F / 16) of the stage at X offset SO into the ring
+  auto rd = [&](auto fc, uint32_t so) __attribute__((always_inline)) {
+    constexpr int F = decltype(fc)::v;
+    af[F & 7] = lds_rd<(F & 15) * 2048>(la[F >> 4] + so);
+  };
+  // group MT: wait until N newer LDS reads remain, then MFMA nt / work slot nt for nt = 0..3
+  auto grp = [&](auto mc, auto nc, h8* B, auto&& w0, auto&& w1, auto&& w2, auto&& w3) __attribute__((always_inline)) {
+    constexpr int MT = decltype(mc)::v;
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(decltype(nc)::v) : "memory");
+    IWQ_PIN();
+    acc[MT][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[MT & 7], B[0], acc[MT][0], 0, 0, 0);
+    w0();
+    IWQ_PIN();
+    acc[MT][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[MT & 7], B[1], acc[MT][1], 0, 0, 0);
+    w1();
+    IWQ_PIN();
+    acc[MT][2] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[MT & 7], B[2], acc[MT][2], 0, 0, 0);
+    w2();
+    IWQ_PIN();
+    acc[MT][3] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[MT & 7], B[3], acc[MT][3], 0, 0, 0);
+    w3();
+    IWQ_PIN();
+  };
+  auto nop = []() __attribute__((always_inline)) {};
+
+  // slice 0: group MT reads fragment MT + D (slice 1's first D at MT >= 16 - D); slice 1's B
+  // dequantized one pair per group
+  auto slice0 = [&](uint32_t so) __attribute__((always_inline)) {
+    h2 p[16];
+    sfor<0, 16>([&](auto mc) __attribute__((always_inline)) {
+      constexpr int MT = decltype(mc)::v;
+      grp(mc, ic<D - 1>{}, b0, [&]() __attribute__((always_inline)) { rd(ic<MT + D>{}, so); },
+          [&]() __attribute__((always_inline)) { p[MT] = dqp(wc[MT >> 2].y, MT & 3, MT >> 2); }, nop, nop);
+    });
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b1[nt] = frag(p + 4 * nt);
+  };
+
+  issue(0, 0);
+  issue(nk > 1 ? 1 : 0, 1);
+  issue(nk > 2 ? 2 : nk - 1, 2);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+  read_codes(wc, 0);
+  sfor<0, D>([&](auto fc) __attribute__((always_inline)) { rd(fc, 0u); });
+  IWQ_LGKM(0);
+  codes_landed(wc);
+  IWQ_PIN();
+  {
+    h2 p[16];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      set_params(nt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[4 * nt + j] = dqp(wc[nt].x, j, nt);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b0[nt] = frag(p + 4 * nt);
+  }
+
+  constexpr int G0 = D + 4;  // first group with the next stage's codes landed
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const uint32_t so = (uint32_t)((kt % NSX) * XS);
+    const uint32_t sn = (uint32_t)(((kt + 1) % NSX) * XS);
+    const uint32_t cn = (uint32_t)(((kt + 1) % NSC) * CST);
+    const int xd = (kt + 3) % NSX, cd = kt % NSC;
+    const int kd = kt + 3 < nk ? kt + 3 : nk - 1;
+    slice0(so);
+    // slice 1: group MT reads fragment 16 + MT + D of this stage, or (MT + D >= 16) the next stage's
+    // slice-0 fragment MT + D - 16 (after the barrier)
+    auto rd1 = [&](auto mc) __attribute__((always_inline)) {
+      constexpr int F = decltype(mc)::v + D;
+      if constexpr (F < 16) rd(ic<16 + F>{}, so);
+      else rd(ic<F - 16>{}, sn);
+    };
+    sfor<0, 4>([&](auto mc) __attribute__((always_inline)) {
+      grp(mc, ic<D - 1>{}, b1, [&]() __attribute__((always_inline)) { rd1(mc); }, nop, nop, nop);
+    });
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+    __builtin_amdgcn_s_barrier();
+    IWQ_PIN();
+    u32x2 wn[4];
+    h2 p[16];
+    sfor<4, 16>([&](auto mc) __attribute__((always_inline)) {
+      constexpr int MT = decltype(mc)::v;
+      // newer reads than fragment MT's: D - 1 fragments, plus the code reads (group 4, before its
+      // fragment read) while they are younger than fragment MT (MT < D + 4)
+      constexpr int N = (MT >= 5 && MT < G0) ? D - 1 + NCR : D - 1;
+      // this group's share of the next stage's 16 dequant pairs (groups G0..15)
+      constexpr int NG = 16 - G0;
+      constexpr int PB = MT >= G0 ? (16 * (MT - G0)) / NG : 0;
+      constexpr int PE = MT >= G0 ? (16 * (MT - G0 + 1)) / NG : 0;
+      constexpr int PM = (PB + PE) / 2;
+      auto dq = [&](auto bc, auto ec) __attribute__((always_inline)) {
+        sfor<decltype(bc)::v, decltype(ec)::v>([&](auto qc) __attribute__((always_inline)) {
+          constexpr int Q = decltype(qc)::v;
+          if constexpr ((Q & 3) == 0) set_params(Q >> 2);
+          p[Q] = dqp(wn[Q >> 2].x, Q & 3, Q >> 2);
+        });
+      };
+      grp(mc, ic<N>{}, b1,
+          [&]() __attribute__((always_inline)) {
+            if constexpr (MT == 4) read_codes(wn, cn);
+            if constexpr (MT == G0) codes_landed(wn);
+            rd1(mc);
+          },
+          [&]() __attribute__((always_inline)) {
+            if constexpr (MT - 4 < PIECES) issue1(kd, xd, cd, MT - 4);
+          },
+          [&]() __attribute__((always_inline)) { dq(ic<PB>{}, ic<PM>{}); },
+          [&]() __attribute__((always_inline)) { dq(ic<PM>{}, ic<PE>{}); });
+    });
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      b0[nt] = frag(p + 4 * nt);
+      wc[nt] = wn[nt];
+    }
+  }
+  {
+    const uint32_t so = (uint32_t)(((nk - 1) % NSX) * XS);
+    slice0(so);
+    sfor<0, 16>([&](auto mc) __attribute__((always_inline)) {
+      constexpr int MT = decltype(mc)::v;
+      constexpr int N = (D - 1 < 15 - MT) ? D - 1 : 15 - MT;
+      grp(mc, ic<N>{}, b1,
+          [&]() __attribute__((always_inline)) {
+            if constexpr (MT + D < 16) rd(ic<16 + MT + D>{}, so);
+          },
+          nop, nop, nop);
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float bc[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) bc[nt] = a.bias ? (float)gp<_Float16>(a.bias)[col0 + 16 * nt] : 0.0f;
+  const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;
+  char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * g) * a.ldy + col0) * 2;
+  const bool full = m0 + TM <= a.M;
+#pragma unroll
+  for (int mt = 0; mt < 16; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = mt * 16 + r;
+      if (full || m0 + rr + 4 * g < a.M) {
+        auto p = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          if constexpr (GROUPED) p[16 * nt] = (_Float16)(acc[mt][nt][r] + bc[nt]);
+          else p[16 * nt] = (_Float16)(opaque(acc[mt][nt][r] * sfl[nt]) + bc[nt]);
+        }
+      }
+    }
+}
+
 #undef IWQ_LGKM
 #undef IWQ_PIN
 
@@ -832,6 +1150,9 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
       case 163: hipLaunchKernelGGL((k_w4a16_b16q<true, false, true>), grid, dim3(256), 0, st, a); break;
       case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true, true>), grid, dim3(256), 0, st, a); break;
       case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true, true>), grid, dim3(256), 0, st, a); break;
+      case 168: hipLaunchKernelGGL((k_w4a16_b16r<true, 4, true>), grid, dim3(256), 0, st, a); break;
+      case 169: hipLaunchKernelGGL((k_w4a16_b16r<true, 6, true>), grid, dim3(256), 0, st, a); break;
+      case 170: hipLaunchKernelGGL((k_w4a16_b16r<false, 6, true>), grid, dim3(256), 0, st, a); break;
       default: hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, true, true>), grid, blk, 0, st, a); break;
     }
     return hipGetLastError();
@@ -846,6 +1167,11 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
     case 163: hipLaunchKernelGGL((k_w4a16_b16q<true>), grid, dim3(256), 0, st, a); break;
     case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true>), grid, dim3(256), 0, st, a); break;
     case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true>), grid, dim3(256), 0, st, a); break;
+    case 168: hipLaunchKernelGGL((k_w4a16_b16r<true, 4>), grid, dim3(256), 0, st, a); break;
+    case 169: hipLaunchKernelGGL((k_w4a16_b16r<true, 6>), grid, dim3(256), 0, st, a); break;
+    case 170: hipLaunchKernelGGL((k_w4a16_b16r<false, 6>), grid, dim3(256), 0, st, a); break;
+    case 166: hipLaunchKernelGGL((k_w4a16_b16q<true, true, false, 1>), grid, dim3(256), 0, st, a); break;  // DIAG
+    case 167: hipLaunchKernelGGL((k_w4a16_b16q<true, true, false, 2>), grid, dim3(256), 0, st, a); break;  // DIAG
     case 161:  // DIAGNOSTIC: 151 without the output stores
       hipLaunchKernelGGL((k_w4a16_b16w<true, false, 16, 0, false, false, true>), grid, blk, 0, st, a);
       break;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round-4 session J: b16r (read-ahead depth) parity + A/B
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+run() { local name=$1 tmo=$2; shift 2; echo "=== $name"; timeout -k 10 $tmo "$@" > $OUT/$name.log 2>&1; local st=$?; tail -3 $OUT/$name.log; echo "=== $name exit $st"; return $st; }
+export IWQ_AB=1
+run t_ab_j 500 python -u -m pytest tests/test_gpu_parity.py -x -q -k "prefill_b32 or nib_default or short_k" --timeout 200 --timeout-method thread -p no:cacheprovider
+[ $? -eq 0 ] || exit 1
+run ab_j_pc 400 python tools/ab_gemm.py --variants 165,168,169,170 --shapes q_proj,gate_proj,down_proj,70b_q --rounds 7
+[ $? -eq 0 ] || exit 3
+run ab_j_g128 400 python tools/ab_gemm.py --group 128 --variants 150,165,168,169,170 --rounds 5
