@@ -68,10 +68,11 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
 
 // Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
 // selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
-template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true, bool GS = false, bool SKEL = false>
+template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true, bool GS = false, bool SKEL = false,
+          bool BATCHED = true>
 hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st, int max_blocks_per_cu = 8) {
   static int cache[64] = {0};
-  auto kern = k_group<DT_F16, 128, false, 0, true, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>;
+  auto kern = k_group<DT_F16, 128, false, 0, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int per_cu = resident_blocks_per_cu(kern, cache);
@@ -212,6 +213,33 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
 #endif
   return hipErrorInvalidValue;
 }
+
+#if IWQ_AB
+// A/B forms of the single-tensor walk (fp16, g = 128, asymmetric, no codes; one launch per weight,
+// pseudo_quantize_tensor's drop-in call; tools/single_trace.py): 1 / 2 the two defaults forced
+// (contiguous UNROLL 4 + prefetch / grid-stride UNROLL 4), 3 / 4 contiguous UNROLL 2 / 1 + prefetch,
+// 5 / 6 grid-stride UNROLL 2 / 1, 7 / 8 contiguous UNROLL 4 / 2 + prefetch on half the resident waves,
+// 9 grid-stride + prefetch, 10 / 11 UNROLL 8 grid-stride / contiguous, 12 / 13 the walks of 1 / 2
+// without the arithmetic (roofline probes: wrong results)
+hipError_t launch_single_variant(int v, const GroupArgs& a, hipStream_t st) {
+  switch (v) {
+    case 1: return launch_variant_t<4, true, true, true, true, false, false, false>(a, st);
+    case 2: return launch_variant_t<4, false, true, true, true, true, false, false>(a, st);
+    case 3: return launch_variant_t<2, true, true, true, true, false, false, false>(a, st);
+    case 4: return launch_variant_t<1, true, true, true, true, false, false, false>(a, st);
+    case 5: return launch_variant_t<2, false, true, true, true, true, false, false>(a, st);
+    case 6: return launch_variant_t<1, false, true, true, true, true, false, false>(a, st);
+    case 7: return launch_variant_t<4, true, true, true, true, false, false, false>(a, st, 4);
+    case 8: return launch_variant_t<2, true, true, true, true, false, false, false>(a, st, 4);
+    case 9: return launch_variant_t<4, true, true, true, true, true, false, false>(a, st);      // grid-stride + prefetch
+    case 10: return launch_variant_t<8, false, true, true, true, true, false, false>(a, st);    // grid-stride UNROLL 8
+    case 11: return launch_variant_t<8, true, true, true, true, false, false, false>(a, st);    // contiguous UNROLL 8
+    case 12: return launch_variant_t<4, true, true, true, true, false, true, false>(a, st);     // 1's walk, no arithmetic
+    case 13: return launch_variant_t<4, false, true, true, true, true, true, false>(a, st);     // 2's walk, no arithmetic
+  }
+  return hipErrorInvalidValue;
+}
+#endif
 
 template <int DT, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_g(int64_t g, const GroupArgs& a, hipStream_t st) {
@@ -548,6 +576,12 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     a.n_entries = 1;
     a.n_bits = n_bits;
     a.nan_flag = nan_flag;
+#if IWQ_AB
+    if (variant != 0 && dtype == IWQ_F16 && group == 128 && !sym && codes == 0) {
+      IWQ_HIP(launch_single_variant(variant, a, s));
+      return IWQ_OK;
+    }
+#endif
     IWQ_HIP(launch_group<false>(dtype, group, sym, codes, a, s));
     return IWQ_OK;
   }
