@@ -75,9 +75,15 @@ enum iwq_status {
                                         IWQ_ERR_ARG with a variant, TILED or FORCE_GENERIC        */
 /* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
  * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
- * (40-49 / 60-81 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first split-K
- * kernel; iwq_prefill.hip / iwq_gemm.hip list them).  NIB-layout variants (66, 67, 69, 71, 75, 77,
- * 81) expect codes repacked so that nibble p of a code dword holds k = (0,2,4,6,1,3,5,7)[p]. */
+ * (40-49 / 60-81 / 150-172 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first
+ * split-K kernel; iwq_prefill.hip / iwq_prefill16.hip / iwq_gemm.hip list them).  NIB-layout variants
+ * (66, 67, 69, 71, 75, 77, 81, 152, 153, 163, 165, 168, 169, 172) expect codes repacked so that nibble
+ * p of a code dword holds k = (0,2,4,6,1,3,5,7)[p].
+ * The product library (libiwq.so) carries only the defaults and the variants the tests pin: 0;
+ * iwq_w4a16_gemm 1 / 2 at M > 16 on row-major codes (the k_w4a16 / k_w4a16_big fallbacks);
+ * per-tensor iwq_quantize_minmax 6 (the two-kernel form, the host's retry) and 9 (test-only abort).
+ * Any other variant returns IWQ_ERR_ARG there; the A/B library (libiwq_ab.so, built with IWQ_AB=1)
+ * has them all, and iwq_build_info() ends in "ab=1". */
 #define IWQ_FLAG_VARIANT(v) (((unsigned)(v) & 0xFFu) << 16)
 
 /* Bytes of device workspace iwq_quantize_minmax needs for this problem (0 if none). */

@@ -2952,10 +2952,12 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
 // 47 16x16x32.
 hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st, bool nib) {
   if (variant == 0) {
-    // per channel: 74 on the 16x16x32 MFMA with waves 4-7 staggered half a K-step (iwq_prefill16.hip
-    // 151, NIB twin 153: same bits; round 4: +6-11 % over 74 on q / gate / down at M = 8192,
-    // profiles/r04_ab_gemm_b16.jsonl); grouped: 74 / its NIB twin 75
-    if (a.gpr == 1 && prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, nib ? 153 : 151, st);
+    // 74 on the 16x16x32 MFMA (iwq_prefill16.hip; NIB twins give the same bits): per channel with
+    // waves 4-7 staggered half a K-step (151 / 153; round 4: +6-11 % over 74 on q / gate / down at
+    // M = 8192, profiles/r04_ab_gemm_b16.jsonl), grouped on the 3-slot ring (150 / 152: +6-8 % over
+    // 74 at g128 on q / gate / down and 70B q / down, profiles/r04_ab_gemm_grouped16.jsonl)
+    if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group))
+      return prefill16_launch(a, a.gpr == 1 ? (nib ? 153 : 151) : (nib ? 152 : 150), st);
     if (a.gpr == 1) return nib ? launch_w<true>(a, st) : launch_w<false>(a, st);
     return nib ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }
@@ -2969,11 +2971,11 @@ hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st,
   }
   // 161 diagnostic (per channel; grouped: 151); 162 / 163 (164 / 165 interleaved): one wave per SIMD
   // (k_w4a16_b16q), NIB codes for the odd ones; 168 / 169 / 170: k_w4a16_b16r reading 4 / 6 / 6
-  // groups ahead (NIB, NIB, row-major)
+  // groups ahead (NIB, NIB, row-major); 171 / 172: persistent k_w4a16_b16p (row-major / NIB)
   if ((variant == 161 || variant == 166 || variant == 167) && a.gpr != 1) variant = 151;  // diagnostics
-  if (variant >= 161 && variant <= 170) {
+  if (variant >= 161 && variant <= 172) {
     if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group)) return prefill16_launch(a, variant, st);
-    const bool nibv = variant == 163 || variant == 165 || variant == 168 || variant == 169;
+    const bool nibv = variant == 163 || variant == 165 || variant == 168 || variant == 169 || variant == 172;
     return nibv ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }
   if (variant >= 150 && variant <= 157) {

@@ -804,6 +804,319 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
     }
 }
 
+// k_w4a16_b16p: k_w4a16_b16q (IL) as a PERSISTENT kernel: gridDim <= CUs workgroups, workgroup b
+// takes tiles swizzled_block(b + j * gridDim) (the non-persistent grid's XCD placement), and the
+// K-steps of its tiles form ONE stream through the rings: the DMA runs three K-steps ahead across tile
+// boundaries, so a tile starts with its first stages already resident (no prologue wait) and the
+// previous tile's epilogue overlaps the next tile's loads.  Every K-step stages one (s, z) per column
+// in the code ring (per channel too: group = K, the tile's parameters), so the per-channel zero point
+// switches with the stream; the per-channel scale stays in the epilogue (captured as the stream moves
+// to the next tile).  The issue cursor (tile, K-step, DMA source pointers) is wave-uniform state
+// advanced once per K-step; past the last step it re-loads the last step into the freed slot.
+template <bool NIB, bool GROUPED>
+__global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
+  constexpr int NSX = 4, NSC = 3;
+  constexpr int CST = CS + PS;
+  constexpr int CBASE = NSX * XS;
+  constexpr int PIECES = 12;  // 8 X, 2 codes, 2 parameters
+  constexpr int VM_AHEAD = PIECES;
+  constexpr int NCR = 8;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NSX * XS + NSC * CST];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int tiles_n = a.N / TN;
+  const int64_t ntiles = (int64_t)((a.M + TM - 1) / TM) * tiles_n;
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  const int my_tiles = (int)((ntiles - b + G - 1) / G);
+  const int64_t crow = a.K / 2;
+  const int nk = a.K / TK;
+  const int64_t pgr = GROUPED ? a.gpr : 1;  // parameters per row
+  const int pgroup = GROUPED ? a.group : a.K;
+
+  // ---- the DMA issue cursor: tile ij, K-step ikt, and that tile's per-lane source pointers
+  int ij = 0, ikt = 0;
+  const _Float16* xsrc[8];
+  const uint8_t* csrc[2];
+  const _Float16* psrc[2];
+  auto set_issue_tile = [&](int j) {
+    const int64_t t = swizzled_block(b + (int64_t)j * G, ntiles);
+    const int m0i = (int)(t / tiles_n) * TM, n0i = (int)(t % tiles_n) * TN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = (wid * 8 + i) * 8 + (lane >> 3);
+      const int gm = m0i + row < a.M ? m0i + row : a.M - 1;
+      xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3);
+    }
+#pragma unroll
+    for (int j2 = 0; j2 < 2; ++j2) {
+      const int ccol = wid * 64 + 32 * j2 + (lane >> 1);
+      csrc[j2] = a.codes + (int64_t)(n0i + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+    }
+    const int64_t c = n0i + wid * 64 + lane;
+    const int64_t off = (GROUPED && a.pgm) ? c : c * pgr;
+    psrc[0] = a.scales + off;
+    psrc[1] = (a.zeros ? a.zeros : a.scales) + off;
+  };
+  const int64_t pstep = (GROUPED && a.pgm) ? a.N : 1;
+  // piece i of the cursor's K-step into X slot xs / code slot cs
+  auto issue1 = [&](int xs, int cs, int i) {
+    if (i < 8) {
+      glds16(xsrc[i] + ikt * TK, smem + xs * XS + (wid * 8 + i) * 1024);
+    } else if (i < 10) {
+      glds16(csrc[i - 8] + ikt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
+    } else {
+      glds2(psrc[i - 10] + ((ikt * TK) / pgroup) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+    }
+  };
+  auto advance_issue = [&]() {
+    if (ikt + 1 < nk) {
+      ++ikt;
+    } else if (ij + 1 < my_tiles) {
+      ++ij;
+      ikt = 0;
+      set_issue_tile(ij);
+    }  // else: stay on the last K-step (re-loads into freed slots nobody reads)
+  };
+
+  // ---- the compute side: tile j (m0, n0), its epilogue scale / bias per column
+  int m0 = 0, n0 = 0;
+  auto set_tile = [&](int j) {
+    const int64_t t = swizzled_block(b + (int64_t)j * G, ntiles);
+    m0 = (int)(t / tiles_n) * TM;
+    n0 = (int)(t % tiles_n) * TN;
+  };
+  float sepi[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  h2 s2[4], zz[4], zl[4], zh[4];
+  auto set_zero = [&](int nt, float zf) {
+    zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+    zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
+    zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
+  const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
+  const uint32_t m1_s = __builtin_amdgcn_readfirstlane(0x00F000F0u);
+  uint32_t magic_v, mg64, mg54;
+  asm volatile("v_mov_b32 %0, 0x54006400" : "=v"(magic_v));
+  asm volatile("v_mov_b32 %0, 0x64006400" : "=v"(mg64));
+  asm volatile("v_mov_b32 %0, 0x54005400" : "=v"(mg54));
+
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint8_t*)(smem));
+  uint32_t la[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) la[s] = lbase + (uint32_t)(r16 * 128 + (((2 * g + s) ^ xh(r16)) << 4));
+  const int ccl = wid * 64 + r16;
+  const uint32_t lc = lbase + CBASE + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
+  const uint32_t lps = lbase + CBASE + CS + (uint32_t)(ccl * 4);
+  u32x2 pv[4];
+  // the parameters of the stage just read: grouped every K-step; per channel only where a tile
+  // starts (the stage's tile changes), first handing the running tile's scale to the epilogue
+  auto set_params = [&](int nt, bool tile_start) {
+    if (GROUPED || tile_start) {
+      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
+      if constexpr (!GROUPED) sepi[nt] = (float)s2[nt].x;
+      s2[nt] = h2{sc, sc};
+      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+    }
+  };
+  auto read_codes = [&](u32x2* w, uint32_t co) {
+    w[0] = lds_rd2<0>(lc + co);
+    w[1] = lds_rd2<512>(lc + co);
+    w[2] = lds_rd2<1024>(lc + co);
+    w[3] = lds_rd2<1536>(lc + co);
+    pv[0] = lds_rd_pair(lps + co);
+    pv[1] = lds_rd_pair(lps + co + 128);
+    pv[2] = lds_rd_pair(lps + co + 1024);
+    pv[3] = lds_rd_pair(lps + co + 1152);
+  };
+  auto codes_landed = [&](u32x2* w) {
+    landed(w[0]);
+    landed(w[1]);
+    landed(w[2]);
+    landed(w[3]);
+    landed(pv[0]);
+    landed(pv[1]);
+    landed(pv[2]);
+    landed(pv[3]);
+  };
+  auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
+    h2 d;
+    if constexpr (NIB) {
+      const uint32_t t = j >= 2 ? w >> 8 : w;
+      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+    } else {
+      const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
+      d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
+    }
+    if constexpr (GROUPED) d = d * s2[nt];
+    return d;
+  };
+  auto frag = [](const h2* p) -> h8 { return h8{p[0].x, p[0].y, p[1].x, p[1].y, p[2].x, p[2].y, p[3].x, p[3].y}; };
+
+  f4 acc[16][4];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 af[8];
+  h8 b0[4], b1[4];
+  u32x2 wc[4];
+
+#define IWQ_RD(MT, ADDR) af[(MT) & 7] = lds_rd<((MT) & 15) * 2048>(ADDR)
+#define IWQ_LGKMN(N) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory")
+#define IWQ_MF1(MT, NT, B) \
+  acc[MT][NT] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[(MT) & 7], B[NT], acc[MT][NT], 0, 0, 0)
+#define IWQ_GRP(MT, N, B, W0, W1, W2, W3) \
+  {                                       \
+    IWQ_LGKMN(N);                         \
+    IWQ_PIN();                            \
+    IWQ_MF1(MT, 0, B);                    \
+    W0;                                   \
+    IWQ_PIN();                            \
+    IWQ_MF1(MT, 1, B);                    \
+    W1;                                   \
+    IWQ_PIN();                            \
+    IWQ_MF1(MT, 2, B);                    \
+    W2;                                   \
+    IWQ_PIN();                            \
+    IWQ_MF1(MT, 3, B);                    \
+    W3;                                   \
+    IWQ_PIN();                            \
+  }
+
+  if (my_tiles <= 0) return;  // (gridDim <= tiles by construction)
+  set_issue_tile(0);
+  // prologue: the stream's K-steps 0, 1, 2 into slots 0, 1, 2 of both rings
+#pragma unroll
+  for (int s0 = 0; s0 < 3; ++s0) {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) issue1(s0, s0, i);
+    advance_issue();
+  }
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+  __builtin_amdgcn_s_barrier();
+  IWQ_PIN();
+  read_codes(wc, 0);
+  IWQ_RD(0, la[0]); IWQ_RD(1, la[0]); IWQ_RD(2, la[0]); IWQ_RD(3, la[0]);
+  IWQ_LGKM(0);
+  codes_landed(wc);
+  IWQ_PIN();
+  {
+    h2 p[16];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      set_params(nt, true);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[4 * nt + j] = dqp(wc[nt].x, j, nt);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b0[nt] = frag(p + 4 * nt);
+  }
+
+  int64_t sg = 0;  // global K-step of the stream (ring slots)
+  for (int j = 0; j < my_tiles; ++j) {
+    set_tile(j);
+    for (int kt = 0; kt < nk; ++kt, ++sg) {
+      const uint32_t so = (uint32_t)((sg % NSX) * XS);
+      const uint32_t sn = (uint32_t)(((sg + 1) % NSX) * XS);
+      const uint32_t cn = (uint32_t)(((sg + 1) % NSC) * CST);
+      const int xd = (int)((sg + 3) % NSX), cd = (int)(sg % NSC);
+      const bool next_tile = kt + 1 == nk;  // the stage read in slice 1 starts a tile (or is a re-load)
+      {
+        const uint32_t a0 = la[0] + so, a1 = la[1] + so;
+        h2 p[16];
+        IWQ_GRP(0, 3, b0, IWQ_RD(4, a0), p[0] = dqp(wc[0].y, 0, 0), , );
+        IWQ_GRP(1, 3, b0, IWQ_RD(5, a0), p[1] = dqp(wc[0].y, 1, 0), , );
+        IWQ_GRP(2, 3, b0, IWQ_RD(6, a0), p[2] = dqp(wc[0].y, 2, 0), , );
+        IWQ_GRP(3, 3, b0, IWQ_RD(7, a0), p[3] = dqp(wc[0].y, 3, 0), , );
+        IWQ_GRP(4, 3, b0, IWQ_RD(8, a0), p[4] = dqp(wc[1].y, 0, 1), , );
+        IWQ_GRP(5, 3, b0, IWQ_RD(9, a0), p[5] = dqp(wc[1].y, 1, 1), , );
+        IWQ_GRP(6, 3, b0, IWQ_RD(10, a0), p[6] = dqp(wc[1].y, 2, 1), , );
+        IWQ_GRP(7, 3, b0, IWQ_RD(11, a0), p[7] = dqp(wc[1].y, 3, 1), , );
+        IWQ_GRP(8, 3, b0, IWQ_RD(12, a0), p[8] = dqp(wc[2].y, 0, 2), , );
+        IWQ_GRP(9, 3, b0, IWQ_RD(13, a0), p[9] = dqp(wc[2].y, 1, 2), , );
+        IWQ_GRP(10, 3, b0, IWQ_RD(14, a0), p[10] = dqp(wc[2].y, 2, 2), , );
+        IWQ_GRP(11, 3, b0, IWQ_RD(15, a0), p[11] = dqp(wc[2].y, 3, 2), , );
+        IWQ_GRP(12, 3, b0, IWQ_RD(0, a1), p[12] = dqp(wc[3].y, 0, 3), , );
+        IWQ_GRP(13, 3, b0, IWQ_RD(1, a1), p[13] = dqp(wc[3].y, 1, 3), , );
+        IWQ_GRP(14, 3, b0, IWQ_RD(2, a1), p[14] = dqp(wc[3].y, 2, 3), , );
+        IWQ_GRP(15, 3, b0, IWQ_RD(3, a1), p[15] = dqp(wc[3].y, 3, 3), , );
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) b1[nt] = frag(p + 4 * nt);
+      }
+      const uint32_t a1 = la[1] + so;
+      const uint32_t na = la[0] + sn;
+      IWQ_GRP(0, 3, b1, IWQ_RD(4, a1), , , );
+      IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), , , );
+      IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), , , );
+      IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), , , );
+      // the stream's next stage landed (this wave's part): publish it
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
+      __builtin_amdgcn_s_barrier();
+      IWQ_PIN();
+      u32x2 wn[4];
+      IWQ_GRP(4, 3, b1, read_codes(wn, cn), IWQ_RD(8, a1), issue1(xd, cd, 0), );
+      IWQ_GRP(5, 3 + NCR, b1, IWQ_RD(9, a1), issue1(xd, cd, 1), , );
+      IWQ_GRP(6, 3 + NCR, b1, IWQ_RD(10, a1), issue1(xd, cd, 2), , );
+      IWQ_GRP(7, 3 + NCR, b1, IWQ_RD(11, a1), issue1(xd, cd, 3), , );
+      h2 p[16];
+      IWQ_LGKM(3);
+      codes_landed(wn);
+      IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(xd, cd, 4); set_params(0, next_tile), p[0] = dqp(wn[0].x, 0, 0),
+              p[1] = dqp(wn[0].x, 1, 0));
+      IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), issue1(xd, cd, 5), p[2] = dqp(wn[0].x, 2, 0), p[3] = dqp(wn[0].x, 3, 0));
+      IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(xd, cd, 6); set_params(1, next_tile), p[4] = dqp(wn[1].x, 0, 1),
+              p[5] = dqp(wn[1].x, 1, 1));
+      IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), issue1(xd, cd, 7), p[6] = dqp(wn[1].x, 2, 1), p[7] = dqp(wn[1].x, 3, 1));
+      IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(xd, cd, 8); set_params(2, next_tile), p[8] = dqp(wn[2].x, 0, 2),
+              p[9] = dqp(wn[2].x, 1, 2));
+      IWQ_GRP(13, 3, b1, IWQ_RD(1, na), issue1(xd, cd, 9), p[10] = dqp(wn[2].x, 2, 2), p[11] = dqp(wn[2].x, 3, 2));
+      IWQ_GRP(14, 3, b1, IWQ_RD(2, na), issue1(xd, cd, 10); set_params(3, next_tile), p[12] = dqp(wn[3].x, 0, 3),
+              p[13] = dqp(wn[3].x, 1, 3));
+      IWQ_GRP(15, 3, b1, IWQ_RD(3, na), issue1(xd, cd, 11); advance_issue(), p[14] = dqp(wn[3].x, 2, 3),
+              p[15] = dqp(wn[3].x, 3, 3));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        b0[nt] = frag(p + 4 * nt);
+        wc[nt] = wn[nt];
+      }
+    }
+    // epilogue of tile j (its accumulators complete; the stream's next stages are in flight / landed)
+    const int col0 = n0 + wid * 64 + r16;
+    float bc[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bc[nt] = a.bias ? (float)gp<_Float16>(a.bias)[col0 + 16 * nt] : 0.0f;
+    const int64_t ld2 = __builtin_amdgcn_readfirstlane((int)a.ldy) * (int64_t)2;
+    char* yl = reinterpret_cast<char*>(a.y) + ((int64_t)(m0 + 4 * g) * a.ldy + col0) * 2;
+    const bool full = m0 + TM <= a.M;
+#pragma unroll
+    for (int mt = 0; mt < 16; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = mt * 16 + r;
+        if (full || m0 + rr + 4 * g < a.M) {
+          auto q = gp<_Float16>(static_cast<void*>(yl + (int64_t)rr * ld2));
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            if constexpr (GROUPED) q[16 * nt] = (_Float16)(acc[mt][nt][r] + bc[nt]);
+            else q[16 * nt] = (_Float16)(opaque(acc[mt][nt][r] * sepi[nt]) + bc[nt]);
+          }
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  // no LDS-DMA may still be landing when the workgroup retires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef IWQ_GRP
+#undef IWQ_MF1
+#undef IWQ_LGKMN
+#undef IWQ_RD
+}
+
 // k_w4a16_b16r: k_w4a16_b16q (one wave per SIMD, IL work slots) with the rolling A reads D groups
 // ahead instead of 4 (D - 1 reads in flight at every MFMA group; the fragment ring holds 8), written
 // with compile-time group indices.  The next stage's slice-0 dequant then runs over groups D + 4 .. 15.
@@ -1127,6 +1440,19 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
 // K-step: the per-channel default since round 4), 152 / 153 the same on NIB codes; grouped weights
 // (group % 64 == 0): 150 / 152 the 3-slot ring, 151 / 153 staggered on 3 slots with the late waves
 // issuing early, 157 staggered issuing in slice 1 (A/B)
+// CUs of the current device (one persistent workgroup each: 152-158 KiB of LDS)
+static int persistent_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
   return M >= 1 && N % TN == 0 && K % TK == 0 && K >= TK && (gpr == 1 || (group % TK == 0 && K % group == 0));
 }
@@ -1134,9 +1460,15 @@ bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const dim3 grid((unsigned)blocks), blk(THR);
-  if (a.gpr == 1 && (variant == 151 || variant == 153)) {  // the product forms
+  // the product forms: per channel 151 / 153 (staggered, 4-slot ring), grouped 150 / 152 (3-slot ring)
+  if (a.gpr == 1 && (variant == 151 || variant == 153)) {
     if (variant == 153) hipLaunchKernelGGL((k_w4a16_b16w<true, true>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.gpr != 1 && (variant == 150 || variant == 152)) {
+    if (variant == 152) hipLaunchKernelGGL((k_w4a16_b16w<false, true, 16, 0, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_w4a16_b16w<false, false, 16, 0, true>), grid, blk, 0, st, a);
     return hipGetLastError();
   }
 #if IWQ_AB
@@ -1150,6 +1482,13 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
       case 163: hipLaunchKernelGGL((k_w4a16_b16q<true, false, true>), grid, dim3(256), 0, st, a); break;
       case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true, true>), grid, dim3(256), 0, st, a); break;
       case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true, true>), grid, dim3(256), 0, st, a); break;
+      case 171:
+      case 172: {
+        const dim3 pg((unsigned)(blocks < persistent_cus() ? blocks : persistent_cus()));
+        if (variant == 172) hipLaunchKernelGGL((k_w4a16_b16p<true, true>), pg, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_w4a16_b16p<false, true>), pg, dim3(256), 0, st, a);
+        break;
+      }
       case 168: hipLaunchKernelGGL((k_w4a16_b16r<true, 4, true>), grid, dim3(256), 0, st, a); break;
       case 169: hipLaunchKernelGGL((k_w4a16_b16r<true, 6, true>), grid, dim3(256), 0, st, a); break;
       case 170: hipLaunchKernelGGL((k_w4a16_b16r<false, 6, true>), grid, dim3(256), 0, st, a); break;
@@ -1167,6 +1506,13 @@ hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
     case 163: hipLaunchKernelGGL((k_w4a16_b16q<true>), grid, dim3(256), 0, st, a); break;
     case 164: hipLaunchKernelGGL((k_w4a16_b16q<false, true>), grid, dim3(256), 0, st, a); break;
     case 165: hipLaunchKernelGGL((k_w4a16_b16q<true, true>), grid, dim3(256), 0, st, a); break;
+    case 171:
+    case 172: {  // persistent one-wave-per-SIMD (k_w4a16_b16p), row-major / NIB
+      const dim3 pg((unsigned)(blocks < persistent_cus() ? blocks : persistent_cus()));
+      if (variant == 172) hipLaunchKernelGGL((k_w4a16_b16p<true, false>), pg, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((k_w4a16_b16p<false, false>), pg, dim3(256), 0, st, a);
+      break;
+    }
     case 168: hipLaunchKernelGGL((k_w4a16_b16r<true, 4>), grid, dim3(256), 0, st, a); break;
     case 169: hipLaunchKernelGGL((k_w4a16_b16r<true, 6>), grid, dim3(256), 0, st, a); break;
     case 170: hipLaunchKernelGGL((k_w4a16_b16r<false, 6>), grid, dim3(256), 0, st, a); break;

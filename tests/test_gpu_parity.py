@@ -952,8 +952,8 @@ def test_w4a16_prefill_big_identity(K):
 # neither the k order nor the accumulation order, so those join the 32x32x16 sets.
 # 150 / 151 / 154-157: 74 on the 16x16x32 MFMA (iwq_prefill16.hip; per channel and group % 64 == 0)
 B32_SETS_PC = ((40, 44, 46, 61, 64), (41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 73, 74, 76, 78, 79, 80, 97, 98), (47,),
-               (48,), (150, 151, 154, 155, 156, 157, 162, 164, 170))
-B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80, 98), (47,), (150, 151, 154, 155, 156, 157, 162, 164, 170))
+               (48,), (150, 151, 154, 155, 156, 157, 162, 164, 170, 171))
+B32_SETS_G = ((40, 41, 42, 43, 45, 60, 62, 63, 65, 68, 70, 74, 76, 78, 79, 80, 98), (47,), (150, 151, 154, 155, 156, 157, 162, 164, 170, 171))
 B32_ALL = tuple(v for vs in B32_SETS_PC for v in vs)
 
 
@@ -967,7 +967,7 @@ def nib_layout(codes, N, K):
 
 
 # NIB-layout variants: same k order and accumulation order as their row-major twins
-B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45, 152: 150, 153: 151, 163: 162, 165: 164, 168: 170, 169: 170}
+B32_NIB = {66: 45, 67: 46, 69: 45, 71: 45, 75: 45, 77: 45, 81: 45, 99: 45, 152: 150, 153: 151, 163: 162, 165: 164, 168: 170, 169: 170, 172: 171}
 
 
 @pytest.mark.parametrize("M", [300, 512, 1024])
@@ -1035,7 +1035,7 @@ def test_w4a16_prefill_b32(K, M, sym, group):
         if group != -2 and v in (67, 71, 77, 81, 99):
             continue  # grouped: one exact kernel, variant 66
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
-        assert torch.equal(y, ys[twin if group == -2 or v in (152, 153, 163, 165, 168, 169) else 45]), (v, twin)  # grouped: 75 = 45
+        assert torch.equal(y, ys[twin if group == -2 or v in (152, 153, 163, 165, 168, 169, 172) else 45]), (v, twin)  # grouped: 75 = 45
 
 
 def test_nib_codes_layout(K):
@@ -1294,9 +1294,33 @@ def test_w4a16_prefill_short_k(K, Kd):
         y = K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y45), v
     y150 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(150))
-    for v, cd in ((151, r.codes), (152, nib), (153, nib), (162, r.codes), (163, nib), (164, r.codes), (165, nib), (168, nib), (169, nib), (170, r.codes)):  # 16x16x32 forms: one set of bits
+    for v, cd in ((151, r.codes), (152, nib), (153, nib), (162, r.codes), (163, nib), (164, r.codes), (165, nib), (168, nib), (169, nib), (170, r.codes), (171, r.codes), (172, nib)):  # 16x16x32 forms: one set of bits
         y = K.w4a16_gemm(x, cd, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
         assert torch.equal(y, y150), v
+
+
+@needs_ab
+@pytest.mark.parametrize("M", [2560, 2600])
+@pytest.mark.parametrize("group", [-2, 128])
+def test_w4a16_prefill_persistent_many_tiles(K, M, group):
+    """The persistent prefill (k_w4a16_b16p, 171 / NIB 172) with more tiles than CUs (320 / 352
+    tiles: workgroups walk two, the DMA stream crossing tile boundaries; a partial last row tile at
+    M = 2600): the bits of the one-tile-per-workgroup forms (162 / 151), within fp32 tolerance."""
+    N, Kd = 8192, 512
+    torch.manual_seed(21)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 99)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    nib = nib_layout(r.codes, N, Kd)
+    y162 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(162))
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool(((y162.float() - ref).abs() <= tol).all())
+    for v, cd in ((171, r.codes), (172, nib), (151, r.codes)):
+        y = K.w4a16_gemm(x, cd, r.scales, r.zeros, 4, group, N, b, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y, y162), v
 
 
 MID_VARIANTS = (50, 51, 52, 53, 54, 55)  # k_w4a16_mid: (MT row tiles, CT column tiles) shapes

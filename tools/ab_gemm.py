@@ -27,7 +27,7 @@ def nib_layout(codes, N, K):
     return out.reshape(N, K // 2).contiguous()
 
 
-NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99, 152, 153, 163, 165, 168, 169)
+NIB_VARIANTS = (66, 67, 69, 71, 75, 77, 81, 99, 152, 153, 163, 165, 168, 169, 172)
 GM_VARIANTS = (158, 159, 160)  # grouped parameters held group-major
 
 

@@ -27,7 +27,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "iron_weight_only_quant_amd", "csrc")
-KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v|b16w|b16q|b16r)\w*):", re.M)
+KERNELS = re.compile(r"^(_ZN3iwq12_GLOBAL__N_1\d+k_w4a16_(?:b32w|b32v|b32s|w4h|w4b|h2v|b16w|b16q|b16r|b16p)\w*):", re.M)
 SOURCES = ("iwq_prefill.hip", "iwq_prefill16.hip")
 
 

@@ -24,13 +24,14 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--inplace", action="store_true", help="write the dequantized weight over the input")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels as K
     fl = K.gemm_variant_flags(a.variant)
     for shp in a.shapes.split(","):
         r, c = (int(v) for v in shp.split("x"))
         ws = [torch.empty(r, c, dtype=torch.float16, device="cuda") for _ in range(a.calls)]
-        outs = [torch.empty_like(w) for w in ws]
+        outs = ws if a.inplace else [torch.empty_like(w) for w in ws]
         for i, w in enumerate(ws):
             K.fill_synthetic(w, 100 + i)
         fns = [(lambda i=i: K.quantize_minmax(ws[i], a.bits, a.group, False, 0, out=outs[i], flags=fl))
@@ -63,7 +64,7 @@ def main():
         n = r * c
         alg = n * 4 + (n // a.group) * 4
         us = ts[len(ts) // 2]
-        print(json.dumps({"shape": shp, "variant": a.variant, "us_per_call": round(us, 2),
+        print(json.dumps({"shape": shp, "variant": a.variant, "inplace": a.inplace, "us_per_call": round(us, 2),
                           "frac": round(alg / (us * 1e-6) / 8e12, 4)}), flush=True)
         del g, ws, outs, fns
         torch.cuda.empty_cache()
