@@ -808,19 +808,21 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
 // takes tiles swizzled_block(b + j * gridDim) (the non-persistent grid's XCD placement), and the
 // K-steps of its tiles form ONE stream through the rings: the DMA runs three K-steps ahead across tile
 // boundaries, so a tile starts with its first stages already resident (no prologue wait) and the
-// previous tile's epilogue overlaps the next tile's loads.  Every K-step stages one (s, z) per column
-// in the code ring (per channel too: group = K, the tile's parameters), so the per-channel zero point
-// switches with the stream; the per-channel scale stays in the epilogue (captured as the stream moves
-// to the next tile).  The issue cursor (tile, K-step, DMA source pointers) is wave-uniform state
-// advanced once per K-step; past the last step it re-loads the last step into the freed slot.
+// previous tile's epilogue overlaps the next tile's loads.  Grouped: the (s, z) of every K-step ride
+// in the code ring (b16q).  Per channel: the next tile's scales / zero points are loaded (global,
+// 8 per lane) in the last K-step of a tile, right after its barrier, and waited for (vmcnt past the
+// 4 DMA pieces issued after them) before the next tile's first dequant; the running tile's scale
+// moves to the epilogue then.  The issue cursor (tile, K-step, DMA source pointers, parameter
+// group) is wave-uniform state advanced once per K-step; past the last step it re-loads the last
+// step into the freed slot.
 template <bool NIB, bool GROUPED>
 __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   constexpr int NSX = 4, NSC = 3;
-  constexpr int CST = CS + PS;
+  constexpr int CST = CS + (GROUPED ? PS : 0);
   constexpr int CBASE = NSX * XS;
-  constexpr int PIECES = 12;  // 8 X, 2 codes, 2 parameters
+  constexpr int PIECES = GROUPED ? 12 : 10;
   constexpr int VM_AHEAD = PIECES;
-  constexpr int NCR = 8;
+  constexpr int NCR = GROUPED ? 8 : 4;
   __shared__ __attribute__((aligned(16))) uint8_t smem[NSX * XS + NSC * CST];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -832,14 +834,14 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   const int my_tiles = (int)((ntiles - b + G - 1) / G);
   const int64_t crow = a.K / 2;
   const int nk = a.K / TK;
-  const int64_t pgr = GROUPED ? a.gpr : 1;  // parameters per row
-  const int pgroup = GROUPED ? a.group : a.K;
+  const int ksg = GROUPED ? a.group / TK : 1;  // K-steps per parameter group
 
-  // ---- the DMA issue cursor: tile ij, K-step ikt, and that tile's per-lane source pointers
-  int ij = 0, ikt = 0;
+  // ---- the DMA issue cursor: tile ij, K-step ikt (group ipg, ipr K-steps left in it), source pointers
+  int ij = 0, ikt = 0, ipg = 0, ipr = ksg;
   const _Float16* xsrc[8];
   const uint8_t* csrc[2];
-  const _Float16* psrc[2];
+  const _Float16* psrc[2] = {nullptr, nullptr};
+  const int64_t pstep = (GROUPED && a.pgm) ? a.N : 1;
   auto set_issue_tile = [&](int j) {
     const int64_t t = swizzled_block(b + (int64_t)j * G, ntiles);
     const int m0i = (int)(t / tiles_n) * TM, n0i = (int)(t % tiles_n) * TN;
@@ -854,38 +856,44 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
       const int ccol = wid * 64 + 32 * j2 + (lane >> 1);
       csrc[j2] = a.codes + (int64_t)(n0i + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
     }
-    const int64_t c = n0i + wid * 64 + lane;
-    const int64_t off = (GROUPED && a.pgm) ? c : c * pgr;
-    psrc[0] = a.scales + off;
-    psrc[1] = (a.zeros ? a.zeros : a.scales) + off;
+    if constexpr (GROUPED) {
+      const int64_t c = n0i + wid * 64 + lane;
+      const int64_t off = a.pgm ? c : c * a.gpr;
+      psrc[0] = a.scales + off;
+      psrc[1] = (a.zeros ? a.zeros : a.scales) + off;
+    }
   };
-  const int64_t pstep = (GROUPED && a.pgm) ? a.N : 1;
-  // piece i of the cursor's K-step into X slot xs / code slot cs
   auto issue1 = [&](int xs, int cs, int i) {
     if (i < 8) {
       glds16(xsrc[i] + ikt * TK, smem + xs * XS + (wid * 8 + i) * 1024);
     } else if (i < 10) {
       glds16(csrc[i - 8] + ikt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
-    } else {
-      glds2(psrc[i - 10] + ((ikt * TK) / pgroup) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+    } else if constexpr (GROUPED) {
+      glds2(psrc[i - 10] + ipg * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
     }
   };
   auto advance_issue = [&]() {
     if (ikt + 1 < nk) {
       ++ikt;
+      if (--ipr == 0) {
+        ++ipg;
+        ipr = ksg;
+      }
     } else if (ij + 1 < my_tiles) {
       ++ij;
       ikt = 0;
+      ipg = 0;
+      ipr = ksg;
       set_issue_tile(ij);
     }  // else: stay on the last K-step (re-loads into freed slots nobody reads)
   };
 
-  // ---- the compute side: tile j (m0, n0), its epilogue scale / bias per column
+  // ---- the compute side
   int m0 = 0, n0 = 0;
-  auto set_tile = [&](int j) {
+  auto tile_mn = [&](int j, int& mm, int& nn) {
     const int64_t t = swizzled_block(b + (int64_t)j * G, ntiles);
-    m0 = (int)(t / tiles_n) * TM;
-    n0 = (int)(t % tiles_n) * TN;
+    mm = (int)(t / tiles_n) * TM;
+    nn = (int)(t % tiles_n) * TN;
   };
   float sepi[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   h2 s2[4], zz[4], zl[4], zh[4];
@@ -893,6 +901,29 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
     zh[nt] = h2{(_Float16)(64.0f + zf), (_Float16)(64.0f + zf)};
+  };
+  // per channel: the parameters of tile j's columns as raw halves (pcs scales, pcz zero points)
+  uint16_t pcs[4] = {0, 0, 0, 0}, pcz[4] = {0, 0, 0, 0};
+  auto load_pc = [&](int j) {
+    int mm, nn;
+    tile_mn(j, mm, nn);
+    const int col = nn + wid * 64 + r16;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      pcs[nt] = gp<uint16_t>(a.scales)[col + 16 * nt];
+      pcz[nt] = a.zeros ? gp<uint16_t>(a.zeros)[col + 16 * nt] : (uint16_t)0;
+    }
+  };
+  auto use_pc = [&]() {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      landed(pcs[nt]);
+      landed(pcz[nt]);
+      sepi[nt] = (float)s2[nt].x;
+      const _Float16 sc = __builtin_bit_cast(_Float16, pcs[nt]);
+      s2[nt] = h2{sc, sc};
+      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, pcz[nt]) : a.zsym);
+    }
   };
   const uint32_t mask_s = __builtin_amdgcn_readfirstlane(0x00F0000Fu);
   const uint32_t m0_s = __builtin_amdgcn_readfirstlane(0x000F000Fu);
@@ -910,12 +941,9 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   const uint32_t lc = lbase + CBASE + (uint32_t)(ccl * 32 + (((g >> 1) ^ cswz(ccl)) << 4) + ((g & 1) << 3));
   const uint32_t lps = lbase + CBASE + CS + (uint32_t)(ccl * 4);
   u32x2 pv[4];
-  // the parameters of the stage just read: grouped every K-step; per channel only where a tile
-  // starts (the stage's tile changes), first handing the running tile's scale to the epilogue
-  auto set_params = [&](int nt, bool tile_start) {
-    if (GROUPED || tile_start) {
+  auto set_params = [&](int nt) {  // grouped: the stage's (s, z)
+    if constexpr (GROUPED) {
       const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
-      if constexpr (!GROUPED) sepi[nt] = (float)s2[nt].x;
       s2[nt] = h2{sc, sc};
       set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
     }
@@ -925,20 +953,24 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
     w[1] = lds_rd2<512>(lc + co);
     w[2] = lds_rd2<1024>(lc + co);
     w[3] = lds_rd2<1536>(lc + co);
-    pv[0] = lds_rd_pair(lps + co);
-    pv[1] = lds_rd_pair(lps + co + 128);
-    pv[2] = lds_rd_pair(lps + co + 1024);
-    pv[3] = lds_rd_pair(lps + co + 1152);
+    if constexpr (GROUPED) {
+      pv[0] = lds_rd_pair(lps + co);
+      pv[1] = lds_rd_pair(lps + co + 128);
+      pv[2] = lds_rd_pair(lps + co + 1024);
+      pv[3] = lds_rd_pair(lps + co + 1152);
+    }
   };
   auto codes_landed = [&](u32x2* w) {
     landed(w[0]);
     landed(w[1]);
     landed(w[2]);
     landed(w[3]);
-    landed(pv[0]);
-    landed(pv[1]);
-    landed(pv[2]);
-    landed(pv[3]);
+    if constexpr (GROUPED) {
+      landed(pv[0]);
+      landed(pv[1]);
+      landed(pv[2]);
+      landed(pv[3]);
+    }
   };
   auto dqp = [&](uint32_t w, int j, int nt) -> h2 {
     h2 d;
@@ -987,6 +1019,11 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
 
   if (my_tiles <= 0) return;  // (gridDim <= tiles by construction)
   set_issue_tile(0);
+  if constexpr (!GROUPED) {
+    load_pc(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    use_pc();
+  }
   // prologue: the stream's K-steps 0, 1, 2 into slots 0, 1, 2 of both rings
 #pragma unroll
   for (int s0 = 0; s0 < 3; ++s0) {
@@ -1006,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
     h2 p[16];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      set_params(nt, true);
+      set_params(nt);
 #pragma unroll
       for (int j = 0; j < 4; ++j) p[4 * nt + j] = dqp(wc[nt].x, j, nt);
     }
@@ -1014,15 +1051,17 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
     for (int nt = 0; nt < 4; ++nt) b0[nt] = frag(p + 4 * nt);
   }
 
-  int64_t sg = 0;  // global K-step of the stream (ring slots)
+  // ring slots of the running K-step: X sx (of 4), codes sc (of 3)
+  int sx = 0, sc = 0;
   for (int j = 0; j < my_tiles; ++j) {
-    set_tile(j);
-    for (int kt = 0; kt < nk; ++kt, ++sg) {
-      const uint32_t so = (uint32_t)((sg % NSX) * XS);
-      const uint32_t sn = (uint32_t)(((sg + 1) % NSX) * XS);
-      const uint32_t cn = (uint32_t)(((sg + 1) % NSC) * CST);
-      const int xd = (int)((sg + 3) % NSX), cd = (int)(sg % NSC);
-      const bool next_tile = kt + 1 == nk;  // the stage read in slice 1 starts a tile (or is a re-load)
+    tile_mn(j, m0, n0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int sxn = (sx + 1) & 3, scn = sc == 2 ? 0 : sc + 1;
+      const uint32_t so = (uint32_t)(sx * XS);
+      const uint32_t sn = (uint32_t)(sxn * XS);
+      const uint32_t cn = (uint32_t)(scn * CST);
+      const int xd = (sx + 3) & 3, cd = sc;  // refilled after the barrier with the cursor's K-step
+      const bool last = kt + 1 == nk;         // wave-uniform: the next stage starts a tile (or re-loads)
       {
         const uint32_t a0 = la[0] + so, a1 = la[1] + so;
         h2 p[16];
@@ -1051,9 +1090,14 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
       IWQ_GRP(1, 3, b1, IWQ_RD(5, a1), , , );
       IWQ_GRP(2, 3, b1, IWQ_RD(6, a1), , , );
       IWQ_GRP(3, 3, b1, IWQ_RD(7, a1), , , );
-      // the stream's next stage landed (this wave's part): publish it
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VM_AHEAD) : "memory");
       __builtin_amdgcn_s_barrier();
+      IWQ_PIN();
+      // per channel, last K-step of the tile: the next tile's parameters (before this step's DMA
+      // pieces; the clamped cursor past the last tile re-reads the same tile's)
+      if constexpr (!GROUPED) {
+        if (last) load_pc(j + 1 < my_tiles ? j + 1 : j);
+      }
       IWQ_PIN();
       u32x2 wn[4];
       IWQ_GRP(4, 3, b1, read_codes(wn, cn), IWQ_RD(8, a1), issue1(xd, cd, 0), );
@@ -1063,26 +1107,35 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
       h2 p[16];
       IWQ_LGKM(3);
       codes_landed(wn);
-      IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(xd, cd, 4); set_params(0, next_tile), p[0] = dqp(wn[0].x, 0, 0),
+      if constexpr (!GROUPED) {
+        if (last) {  // the parameter loads and everything older landed (4 DMA pieces issued since)
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          use_pc();
+        }
+      }
+      IWQ_PIN();
+      IWQ_GRP(8, 3, b1, IWQ_RD(12, a1), issue1(xd, cd, 4); set_params(0), p[0] = dqp(wn[0].x, 0, 0),
               p[1] = dqp(wn[0].x, 1, 0));
       IWQ_GRP(9, 3, b1, IWQ_RD(13, a1), issue1(xd, cd, 5), p[2] = dqp(wn[0].x, 2, 0), p[3] = dqp(wn[0].x, 3, 0));
-      IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(xd, cd, 6); set_params(1, next_tile), p[4] = dqp(wn[1].x, 0, 1),
+      IWQ_GRP(10, 3, b1, IWQ_RD(14, a1), issue1(xd, cd, 6); set_params(1), p[4] = dqp(wn[1].x, 0, 1),
               p[5] = dqp(wn[1].x, 1, 1));
       IWQ_GRP(11, 3, b1, IWQ_RD(15, a1), issue1(xd, cd, 7), p[6] = dqp(wn[1].x, 2, 1), p[7] = dqp(wn[1].x, 3, 1));
-      IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(xd, cd, 8); set_params(2, next_tile), p[8] = dqp(wn[2].x, 0, 2),
+      IWQ_GRP(12, 3, b1, IWQ_RD(0, na), issue1(xd, cd, 8); set_params(2), p[8] = dqp(wn[2].x, 0, 2),
               p[9] = dqp(wn[2].x, 1, 2));
       IWQ_GRP(13, 3, b1, IWQ_RD(1, na), issue1(xd, cd, 9), p[10] = dqp(wn[2].x, 2, 2), p[11] = dqp(wn[2].x, 3, 2));
-      IWQ_GRP(14, 3, b1, IWQ_RD(2, na), issue1(xd, cd, 10); set_params(3, next_tile), p[12] = dqp(wn[3].x, 0, 3),
+      IWQ_GRP(14, 3, b1, IWQ_RD(2, na), issue1(xd, cd, 10); set_params(3), p[12] = dqp(wn[3].x, 0, 3),
               p[13] = dqp(wn[3].x, 1, 3));
-      IWQ_GRP(15, 3, b1, IWQ_RD(3, na), issue1(xd, cd, 11); advance_issue(), p[14] = dqp(wn[3].x, 2, 3),
-              p[15] = dqp(wn[3].x, 3, 3));
+      IWQ_GRP(15, 3, b1, IWQ_RD(3, na), issue1(xd, cd, 11), p[14] = dqp(wn[3].x, 2, 3), p[15] = dqp(wn[3].x, 3, 3));
+      advance_issue();
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         b0[nt] = frag(p + 4 * nt);
         wc[nt] = wn[nt];
       }
+      sx = sxn;
+      sc = scn;
     }
-    // epilogue of tile j (its accumulators complete; the stream's next stages are in flight / landed)
+    // epilogue of tile j (the stream's next stages are in flight / landed meanwhile)
     const int col0 = n0 + wid * 64 + r16;
     float bc[4];
 #pragma unroll
