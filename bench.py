@@ -751,16 +751,22 @@ def fused_forward_section(rot_bytes=1 << 30):
             M = 8192
             x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
             y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+            nib = K.nib_codes(r.codes, N, Kd)
             t = _interleaved_ms({"fused": lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y),
+                                 "fused_nib": lambda: K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, out=y,
+                                                                   nib=True),
                                  "F.linear": lambda: F.linear(x, r.out)})
             tf = 2.0 * M * N * Kd / (t["fused"] / 1e3) / 1e12
+            tfn = 2.0 * M * N * Kd / (t["fused_nib"] / 1e3) / 1e12
             out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "mfma",
                         "fused_ms": round(t["fused"], 4), "F_linear_ms": round(t["F.linear"], 4),
                         "fused_TFLOPs": round(tf, 1), "frac_of_mfma_peak": round(tf / MFMA_PEAK_TFLOPS, 4),
                         "F_linear_TFLOPs": round(2.0 * M * N * Kd / (t["F.linear"] / 1e3) / 1e12, 1),
                         "fused_vs_F_linear": round(t["F.linear"] / t["fused"], 3),
+                        "fused_nib_ms": round(t["fused_nib"], 4), "fused_nib_TFLOPs": round(tfn, 1),
+                        "fused_nib_vs_F_linear": round(t["F.linear"] / t["fused_nib"], 3),
                         "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
-            del x, y
+            del x, y, nib
             # decode: M = 1, cold, codes in the decode tile layout (what QuantLinear "auto" keeps)
             M = 1
             x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
@@ -784,7 +790,9 @@ def fused_forward_section(rot_bytes=1 << 30):
         torch.cuda.empty_cache()
     return {"config": "BASELINE configs[2]: Llama-2-7B INT4 fused dequant+GEMM QuantLinear forward (packed codes) "
                       "vs F.linear on the dequantized fp16 weight, same run",
-            "kernels": "M=8192: k_w4a16_b32w (iwq_prefill.hip); M=1: k_w4a16_gemv(_ct) on tile-layout codes",
+            "kernels": "M=8192: row-major codes k_w4a16_b16w (per channel 151, grouped 150), NIB codes "
+                       "(QuantLinear nib_prefill) k_w4a16_b16p (persistent, 172) / b16w 152 (iwq_prefill16.hip); "
+                       "M=1: k_w4a16_gemv(_ct) on tile-layout codes",
             "mfma_peak_TFLOPs": MFMA_PEAK_TFLOPS, "rows": out}
 
 

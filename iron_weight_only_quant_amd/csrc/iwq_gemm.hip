@@ -1253,7 +1253,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
                           workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
   if (flags & IWQ_FLAG_NIB_CODES) {
     // NIB-layout codes (iwq_nib_codes): the prefill kernel only (the row-major default's NIB twin:
-    // 153 per channel, 152 grouped, and the split-K form), M >= 256; every other path reads the
+    // 172 per channel, 152 grouped, and the split-K form), M >= 256; every other path reads the
     // row-major layout
     if ((flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_FORCE_GENERIC)) || variant != 0 || M < 256 ||
         !prefill_b32_supported(M, N, K, a.gpr, a.group))

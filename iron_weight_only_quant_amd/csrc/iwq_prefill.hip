@@ -2953,11 +2953,12 @@ bool prefill_b32_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) 
 hipError_t prefill_b32_launch(const PrefillArgs& a, int variant, hipStream_t st, bool nib) {
   if (variant == 0) {
     // 74 on the 16x16x32 MFMA (iwq_prefill16.hip; NIB twins give the same bits): per channel with
-    // waves 4-7 staggered half a K-step (151 / 153; round 4: +6-11 % over 74 on q / gate / down at
-    // M = 8192, profiles/r04_ab_gemm_b16.jsonl), grouped on the 3-slot ring (150 / 152: +6-8 % over
-    // 74 at g128 on q / gate / down and 70B q / down, profiles/r04_ab_gemm_grouped16.jsonl)
+    // waves 4-7 staggered half a K-step (151; round 4: +6-11 % over 74 on q / gate / down at
+    // M = 8192, profiles/r04_ab_gemm_b16.jsonl) and, on NIB codes, the persistent one-wave-per-SIMD
+    // form (172: 1-4.5 % over 153, profiles/r04_ab_gemm_b16p_saddr.jsonl); grouped on the 3-slot
+    // ring (150 / 152: +6-8 % over 74 at g128, profiles/r04_ab_gemm_grouped16.jsonl)
     if (prefill16_supported(a.M, a.N, a.K, a.gpr, a.group))
-      return prefill16_launch(a, a.gpr == 1 ? (nib ? 153 : 151) : (nib ? 152 : 150), st);
+      return prefill16_launch(a, a.gpr == 1 ? (nib ? 172 : 151) : (nib ? 152 : 150), st);
     if (a.gpr == 1) return nib ? launch_w<true>(a, st) : launch_w<false>(a, st);
     return nib ? launch_w<true, true>(a, st) : launch_w<false, true>(a, st);
   }

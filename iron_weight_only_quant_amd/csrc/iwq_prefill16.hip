@@ -838,23 +838,28 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
 
   // ---- the DMA issue cursor: tile ij, K-step ikt (group ipg, ipr K-steps left in it), source pointers
   int ij = 0, ikt = 0, ipg = 0, ipr = ksg;
-  const _Float16* xsrc[8];
-  const uint8_t* csrc[2];
+  // X / code sources as a wave-uniform tile base (SGPRs) + 32-bit lane offsets: the DMA then takes
+  // the saddr form, no 64-bit address VALU per piece
+  const char* xb = nullptr;
+  const char* cb = nullptr;
+  uint32_t xo[8], co[2];
   const _Float16* psrc[2] = {nullptr, nullptr};
   const int64_t pstep = (GROUPED && a.pgm) ? a.N : 1;
   auto set_issue_tile = [&](int j) {
     const int64_t t = swizzled_block(b + (int64_t)j * G, ntiles);
     const int m0i = (int)(t / tiles_n) * TM, n0i = (int)(t % tiles_n) * TN;
+    xb = reinterpret_cast<const char*>(a.x + (int64_t)m0i * a.lda);
+    cb = reinterpret_cast<const char*>(a.codes + (int64_t)n0i * crow);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = (wid * 8 + i) * 8 + (lane >> 3);
-      const int gm = m0i + row < a.M ? m0i + row : a.M - 1;
-      xsrc[i] = a.x + (int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3);
+      const int gm = m0i + row < a.M ? row : a.M - 1 - m0i;
+      xo[i] = (uint32_t)(((int64_t)gm * a.lda + (((lane & 7) ^ xh(row)) << 3)) * 2);
     }
 #pragma unroll
     for (int j2 = 0; j2 < 2; ++j2) {
       const int ccol = wid * 64 + 32 * j2 + (lane >> 1);
-      csrc[j2] = a.codes + (int64_t)(n0i + ccol) * crow + (((lane & 1) ^ cswz(ccol)) << 4);
+      co[j2] = (uint32_t)((int64_t)ccol * crow + (((lane & 1) ^ cswz(ccol)) << 4));
     }
     if constexpr (GROUPED) {
       const int64_t c = n0i + wid * 64 + lane;
@@ -865,9 +870,9 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   };
   auto issue1 = [&](int xs, int cs, int i) {
     if (i < 8) {
-      glds16(xsrc[i] + ikt * TK, smem + xs * XS + (wid * 8 + i) * 1024);
+      glds16(xb + ikt * (TK * 2) + xo[i], smem + xs * XS + (wid * 8 + i) * 1024);
     } else if (i < 10) {
-      glds16(csrc[i - 8] + ikt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
+      glds16(cb + ikt * (TK / 2) + co[i - 8], smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
     } else if constexpr (GROUPED) {
       glds2(psrc[i - 10] + ipg * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
     }
@@ -1513,10 +1518,16 @@ bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st) {
   const int64_t blocks = ((int64_t)(a.M + TM - 1) / TM) * (a.N / TN);
   const dim3 grid((unsigned)blocks), blk(THR);
-  // the product forms: per channel 151 / 153 (staggered, 4-slot ring), grouped 150 / 152 (3-slot ring)
+  // the product forms: per channel 151 (staggered, 4-slot ring) / 172 (NIB codes, persistent one wave
+  // per SIMD), grouped 150 / 152 (3-slot ring)
   if (a.gpr == 1 && (variant == 151 || variant == 153)) {
     if (variant == 153) hipLaunchKernelGGL((k_w4a16_b16w<true, true>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((k_w4a16_b16w<true>), grid, blk, 0, st, a);
+    return hipGetLastError();
+  }
+  if (a.gpr == 1 && variant == 172) {  // NIB codes: the persistent form (same bits as 151 / 153)
+    const dim3 pg((unsigned)(blocks < persistent_cus() ? blocks : persistent_cus()));
+    hipLaunchKernelGGL((k_w4a16_b16p<true, false>), pg, dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (a.gpr != 1 && (variant == 150 || variant == 152)) {

@@ -409,6 +409,13 @@ FUSED_MAX_M = 2048
 NIB_MIN_M = 256
 
 
+# [N, K] weights on which the fused prefill beats hipBLASLt at large M (per channel, M = 8192, in-run
+# interleaved A/B): Llama-2-7B gate / up_proj, 1.14-1.18x (profiles/r04_ab_gemm_b16*.jsonl; the library
+# GEMM's 43 column tiles).  Everywhere else at large M the library GEMM on the resident fp16 weight
+# is 1.0-1.1x faster.
+LARGE_M_FUSED = frozenset({(11008, 4096)})
+
+
 def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     """QuantLinear(fused_forward="auto"): whether the packed-code kernels beat the reference forward
     F.linear(x, W_deq) (hipBLASLt on the resident fp16 weight) for an M-row batch on an [N, K] weight.
@@ -419,7 +426,7 @@ def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     M <= 32 (1.06-3.2x) and on down-like weights up to M = 512 (1.08-1.72x), but not on q_proj at
     M = 64 (0.86x) or gate_proj at 128-192 (0.92-0.94x)."""
     if group == -2:
-        return M <= 192 or (M <= 1024 and K >= 2 * N)
+        return M <= 192 or (M <= 1024 and K >= 2 * N) or (M >= 4096 and (N, K) in LARGE_M_FUSED)
     return M <= 32 or (M <= 512 and K >= 2 * N)
 
 
