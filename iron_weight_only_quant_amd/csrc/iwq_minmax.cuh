@@ -285,7 +285,7 @@ __device__ __forceinline__ void load_iter(const Iter& it, Vec8<DT> (&v)[UNROLL])
 // removed (the input is copied to the output) -- this kernel's own memory stream as a ceiling.
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
           bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
+__device__ __forceinline__ void k_group_body(const GroupArgs& a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
@@ -380,6 +380,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_
     }
   }
   flag_nan(a.nan_flag, any_nan);
+}
+
+template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
+          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
+  k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>(a);
+}
+// the same walk held to 64 VGPRs, i.e. 8 waves per SIMD (k_group needs 67-68 at fp16 g128: 7 waves)
+template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
+          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_group8(
+    GroupArgs a) {
+  k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>(a);
 }
 
 // =============================================================================================

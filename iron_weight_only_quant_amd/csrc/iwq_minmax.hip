@@ -220,8 +220,10 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
 // (contiguous UNROLL 4 + prefetch / grid-stride UNROLL 4), 3 / 4 contiguous UNROLL 2 / 1 + prefetch,
 // 5 / 6 grid-stride UNROLL 2 / 1, 7 / 8 contiguous UNROLL 4 / 2 + prefetch on half the resident waves,
 // 9 grid-stride + prefetch, 10 / 11 UNROLL 8 grid-stride / contiguous, 12 / 13 the walks of 1 / 2
-// without the arithmetic (roofline probes: wrong results)
+// without the arithmetic (roofline probes: wrong results), 14 / 15 the walks of 1 / 2 at 64 VGPRs
+// (8 waves per SIMD instead of 7)
 hipError_t launch_single_variant(int v, const GroupArgs& a, hipStream_t st) {
+  static int c14[64] = {0}, c15[64] = {0};
   switch (v) {
     case 1: return launch_variant_t<4, true, true, true, true, false, false, false>(a, st);
     case 2: return launch_variant_t<4, false, true, true, true, true, false, false>(a, st);
@@ -236,6 +238,9 @@ hipError_t launch_single_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 11: return launch_variant_t<8, true, true, true, true, false, false, false>(a, st);    // contiguous UNROLL 8
     case 12: return launch_variant_t<4, true, true, true, true, false, true, false>(a, st);     // 1's walk, no arithmetic
     case 13: return launch_variant_t<4, false, true, true, true, true, true, false>(a, st);     // 2's walk, no arithmetic
+    case 14: return launch_persistent(k_group8<DT_F16, 128, false, 0, false, 4, true, true>, c14, 4, a, st);
+    case 15: return launch_persistent(k_group8<DT_F16, 128, false, 0, false, 4, false, true, true, true, true>, c15, 4,
+                                      a, st);
   }
   return hipErrorInvalidValue;
 }

@@ -117,8 +117,17 @@ def _cases(AD):
     return out
 
 
-# + the double-approximate kernel's A/B forms: 2 (DPP / permlane exchange), 3 (the round-2 kernel)
-@pytest.mark.parametrize("flags", FLAG_SETS + (2 << 16, 3 << 16))
+def _ab_built():
+    try:
+        from iron_weight_only_quant_amd import _lib
+        return _lib.ab_built()
+    except OSError:
+        return False
+
+
+# + the double-approximate kernel's A/B forms (IWQ_AB library only): 2 (DPP / permlane exchange),
+# 3 (the round-2 kernel)
+@pytest.mark.parametrize("flags", FLAG_SETS + ((2 << 16, 3 << 16) if _ab_built() else ()))
 def test_approx_golden_kernel(K, AD, flags):
     x = dev16(AD["in/apx_a"])
     n = 0
