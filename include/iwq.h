@@ -81,7 +81,8 @@ enum iwq_status {
  * p of a code dword holds k = (0,2,4,6,1,3,5,7)[p].
  * The product library (libiwq.so) carries only the defaults and the variants the tests pin: 0;
  * iwq_w4a16_gemm 1 / 2 at M > 16 on row-major codes (the k_w4a16 / k_w4a16_big fallbacks);
- * per-tensor iwq_quantize_minmax 6 (the two-kernel form, the host's retry) and 9 (test-only abort).
+ * per-tensor iwq_quantize_minmax 6 (the two-kernel form, the host's retry) and 9 (test-only abort);
+ * iwq_quantize_minmax_batched(_ex) 100 / 101 / 102 / 118 (the roofline probes bench.py times).
  * Any other variant returns IWQ_ERR_ARG there; the A/B library (libiwq_ab.so, built with IWQ_AB=1)
  * has them all, and iwq_build_info() ends in "ab=1". */
 #define IWQ_FLAG_VARIANT(v) (((unsigned)(v) & 0xFFu) << 16)

@@ -146,7 +146,16 @@ __global__ __launch_bounds__(BLOCK) void k_probe(const iwq_batch_entry* entries,
   if (MODE == 3 && acc == 0x12345678u) sink[0] = acc;
 }
 
+// the roofline probes bench.py measures its ceiling with (CEILING_PROBES): in every library
+bool is_ceiling_probe(int v) { return v == 100 || v == 101 || v == 102 || v == 118; }
+
 hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
+  switch (v) {
+    case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
+    case 118: return launch_variant_t<4, false, true, true, true, false, true>(a, st);  // default walk, no arithmetic
+  }
 #if IWQ_AB
   switch (v) {
     case 1: return launch_variant_t<4, true, true, true>(a, st);
@@ -163,7 +172,6 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 12: return launch_variant_t<4, false, true, true>(a, st, 8);           // default kernel (same as 0)
     case 13: return launch_variant_t<4, false, true, false>(a, st);             // default walk, plain stores
     case 14: return launch_variant_t<4, false, false, false>(a, st);            // plain loads + plain stores
-    case 118: return launch_variant_t<4, false, true, true, true, false, true>(a, st);  // default walk, no arithmetic
     // memory-stream probes on the same skeleton (no arithmetic): which walk moves the bytes fastest
     case 119: return launch_variant_t<8, false, true, true, true, false, true>(a, st);     // 8 units in flight
     case 120: return launch_variant_t<2, false, true, true, true, false, true>(a, st);     // 2 units in flight
@@ -191,9 +199,6 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 139: return launch_variant_t<1, false, true, true, true, true, true>(a, st);      // skeleton, grid-stride, 1 unit
     case 140: return launch_variant_t<2, false, true, true, true, true, true>(a, st);      // skeleton, grid-stride, 2 units
     case 141: return launch_variant_t<1, false, true, true, true, true>(a, st, 4);         // grid-stride, 1 unit, 4 waves
-    case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
-    case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
-    case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 103: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 104: hipLaunchKernelGGL(k_probe<4>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 105: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 32)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
@@ -703,7 +708,7 @@ int iwq_quantize_minmax_batched(const iwq_batch_entry* d_entries, int32_t n_entr
   // states with IWQ_FLAG_BATCH_CODES that every entry carries out_codes.
   const int codes = (flags & IWQ_FLAG_BATCH_CODES) ? (n_bits <= 4 ? 4 : 8) : 0;
   const int variant = (int)((flags >> 16) & 0xFFu);
-  if (!IWQ_AB && variant != 0) return IWQ_ERR_ARG;  // A/B forms: IWQ_AB builds
+  if (!IWQ_AB && variant != 0 && !is_ceiling_probe(variant)) return IWQ_ERR_ARG;  // A/B forms: IWQ_AB builds
   if (variant != 0 && dtype == IWQ_F16 && group == 128 && !symmetric && codes == 0) {
     IWQ_HIP(launch_variant(variant, a, static_cast<hipStream_t>(stream)));
     return IWQ_OK;

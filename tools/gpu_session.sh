@@ -81,7 +81,7 @@ if [[ $WHAT == *dist2* ]]; then
 fi
 if [[ $WHAT == *pmc* ]]; then
   cd /tmp
-  B="python3 $ROOT/bench.py --no-cpu-baseline --no-ppl --no-shapes --ramp-seconds 0 --steps 3 --warmup 1"
+  B="python3 $ROOT/bench.py --no-cpu-baseline --no-ppl --no-shapes --no-sections --ramp-seconds 0 --steps 3 --warmup 1"
   step pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- $B
   step pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- $B
   step traffic 60 python3 "$ROOT/tools/pmc_traffic.py" "$OUT/pmc_fetch" "$OUT/pmc_write" --numel 6476005376 --kernel "k_group<0, 128, false, 0, true," -o "$OUT/traffic.json"
