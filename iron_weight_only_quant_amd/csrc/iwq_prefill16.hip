@@ -45,10 +45,17 @@ constexpr int PS = 2 * TN * 4;   // grouped: 256 scales + 256 zero points, one d
 __device__ __forceinline__ int xh(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) * 6); }
 __device__ __forceinline__ int cswz(int n) { return (n >> 3) & 1; }
 
+// row-major dequant (after a v_perm_b32): inline asm, the schedule measured best for 151
 __device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
   uint32_t r;
   asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "s"(mask_s), "v"(magic_v));
   return r;
+}
+// NIB dequant: the same instruction left to the compiler (it then tracks the hazard to the
+// following v_pk_add instead of padding every inline-asm result with s_nop: 172 -0.7...-1.5 %,
+// profiles/r04_ab_lib_and_or.jsonl)
+__device__ __forceinline__ uint32_t and_or_c(uint32_t x, uint32_t mask_s, uint32_t magic_v) {
+  return (x & mask_s) | magic_v;
 }
 
 __device__ __forceinline__ int64_t swizzled_block(int64_t bid, int64_t nblocks) {
@@ -216,7 +223,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     h2 d;
     if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or_c(t, m1_s, mg54)) - zh[nt] : as_h2(and_or_c(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
       d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
@@ -597,7 +604,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
       return as_h2(j & 1 ? w >> 1 : w);
     } else if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or_c(t, m1_s, mg54)) - zh[nt] : as_h2(and_or_c(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
       d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
@@ -981,7 +988,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
     h2 d;
     if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or_c(t, m1_s, mg54)) - zh[nt] : as_h2(and_or_c(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
       d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];
@@ -1314,7 +1321,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
     h2 d;
     if constexpr (NIB) {
       const uint32_t t = j >= 2 ? w >> 8 : w;
-      d = (j & 1) ? as_h2(and_or(t, m1_s, mg54)) - zh[nt] : as_h2(and_or(t, m0_s, mg64)) - zl[nt];
+      d = (j & 1) ? as_h2(and_or_c(t, m1_s, mg54)) - zh[nt] : as_h2(and_or_c(t, m0_s, mg64)) - zl[nt];
     } else {
       const uint32_t sel = j == 0 ? 0x0C000C00u : (j == 1 ? 0x0C010C01u : (j == 2 ? 0x0C020C02u : 0x0C030C03u));
       d = as_h2(and_or(__builtin_amdgcn_perm(w, w, sel), mask_s, magic_v)) - zz[nt];

@@ -40,7 +40,12 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--warm-seconds", type=float, default=2.0)
+    ap.add_argument("--lib", default=None, help="load this library build instead (A/B of two builds)")
+    ap.add_argument("--tag", default=None)
     a = ap.parse_args()
+    if a.lib:
+        from iron_weight_only_quant_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     from iron_weight_only_quant_amd import kernels
     xw = torch.randn(8192, 4096, device="cuda").half()
     ww = torch.randn(4096, 4096, device="cuda").half()
@@ -94,7 +99,7 @@ def main():
         for k in keys:
             ts = sorted(times[k])
             med = ts[len(ts) // 2]
-            print(json.dumps({"shape": name, "M": a.m, "N": N, "K": K, "group": a.group, "arm": k,
+            print(json.dumps({"shape": name, "M": a.m, "N": N, "K": K, "group": a.group, "arm": k, "tag": a.tag,
                               "ms": round(med, 4), "ms_min": round(ts[0], 4), "tflops": round(flops / med / 1e9, 1)}),
                   flush=True)
 
