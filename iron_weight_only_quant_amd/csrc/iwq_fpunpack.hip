@@ -63,28 +63,44 @@ __global__ __launch_bounds__(256) void k_dequant_fp_packed(UnpackArgs a) {
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   IWQ_GLOBAL h8* out = gp<h8>(a.out);
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  for (int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2048; base < a.total; base += nwaves * 2048) {
-    constexpr bool NIB = FMT == FMT_HW4 || FMT == FMT_TAB4;
+  constexpr bool NIB = FMT == FMT_HW4 || FMT == FMT_TAB4;
+  // one step = 2048 elements per wave: the codes AND the group parameters of the step are loaded
+  // together (no second dependent round trip for the scales), and the next step's loads are issued
+  // before this step's decode and stores (register double buffer)
+  struct Step {
     u32x2 w[4];
+    _Float16 sc[4], zv[4];
+  };
+  auto load_step = [&](int64_t base, Step& st) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t e = base + 512 * j + 8 * lane;
       const int64_t ee = e < a.total ? e : 0;
-      if constexpr (NIB) w[j] = u32x2{__builtin_nontemporal_load(gp<uint32_t>(a.codes) + ee / 8), 0u};
-      else w[j] = __builtin_nontemporal_load(gp<u32x2>(a.codes) + ee / 8);
+      if constexpr (NIB) st.w[j] = u32x2{__builtin_nontemporal_load(gp<uint32_t>(a.codes) + ee / 8), 0u};
+      else st.w[j] = __builtin_nontemporal_load(gp<u32x2>(a.codes) + ee / 8);
+      const int64_t gi = a.gshift >= 0 ? (ee >> a.gshift) : ee / a.group;
+      st.sc[j] = gp<_Float16>(a.scales)[gi];
+      if constexpr (ASYM) st.zv[j] = gp<_Float16>(a.zeros)[gi];
     }
+  };
+  int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2048;
+  if (base >= a.total) return;
+  Step nxt;
+  load_step(base, nxt);
+  while (true) {
+    const Step cur = nxt;
+    const int64_t b0 = base;
+    base += nwaves * 2048;
+    const bool more = base < a.total;
+    if (more) load_step(base, nxt);
+    const u32x2* w = cur.w;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int64_t e = base + 512 * j + 8 * lane;
+      const int64_t e = b0 + 512 * j + 8 * lane;
       if (e >= a.total) continue;
-      const int64_t gi = a.gshift >= 0 ? (e >> a.gshift) : e / a.group;
-      const _Float16 sc = gp<_Float16>(a.scales)[gi];
-      const h2 s2 = {sc, sc};
+      const h2 s2 = {cur.sc[j], cur.sc[j]};
       h2 z2 = {(_Float16)0.0f, (_Float16)0.0f};
-      if constexpr (ASYM) {
-        const _Float16 zv = gp<_Float16>(a.zeros)[gi];
-        z2 = h2{zv, zv};
-      }
+      if constexpr (ASYM) z2 = h2{cur.zv[j], cur.zv[j]};
       h2 d[4];
       if constexpr (FMT == FMT_HW4) {
         d[0] = __builtin_amdgcn_cvt_scalef32_pk_f16_fp4(w[j].x, 1.0f, 0);
@@ -137,6 +153,7 @@ __global__ __launch_bounds__(256) void k_dequant_fp_packed(UnpackArgs a) {
       }
       __builtin_nontemporal_store(o, out + e / 8);
     }
+    if (!more) break;
   }
 }
 
