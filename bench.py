@@ -752,10 +752,18 @@ def fused_forward_section(rot_bytes=1 << 30):
             x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
             y = torch.empty(M, N, dtype=torch.float16, device="cuda")
             nib = K.nib_codes(r.codes, N, Kd)
-            t = _interleaved_ms({"fused": lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y),
-                                 "fused_nib": lambda: K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, out=y,
-                                                                   nib=True),
-                                 "F.linear": lambda: F.linear(x, r.out)})
+            # QuantLinear(fused_forward=True)'s call: grouped weights also pass the group-major copies
+            # of their parameters (IWQ_FLAG_GROUP_MAJOR); "fused_ref_order" = the same kernel reading
+            # the reference's [N, K/g] parameter order
+            sgm, zgm = K.group_major_params(r.scales, r.zeros, N, Kd, group) if group != -2 else (None, None)
+            arms = {"fused": lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y,
+                                                  scales_gm=sgm, zeros_gm=zgm),
+                    "fused_nib": lambda: K.w4a16_gemm(x, nib, r.scales, r.zeros, 4, group, N, out=y, nib=True,
+                                                      scales_gm=sgm, zeros_gm=zgm),
+                    "F.linear": lambda: F.linear(x, r.out)}
+            if group != -2:
+                arms["fused_ref_order"] = lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y)
+            t = _interleaved_ms(arms)
             tf = 2.0 * M * N * Kd / (t["fused"] / 1e3) / 1e12
             tfn = 2.0 * M * N * Kd / (t["fused_nib"] / 1e3) / 1e12
             out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "mfma",
@@ -766,7 +774,10 @@ def fused_forward_section(rot_bytes=1 << 30):
                         "fused_nib_ms": round(t["fused_nib"], 4), "fused_nib_TFLOPs": round(tfn, 1),
                         "fused_nib_vs_F_linear": round(t["F.linear"] / t["fused_nib"], 3),
                         "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
-            del x, y, nib
+            if group != -2:
+                out[-1].update(fused_ref_order_ms=round(t["fused_ref_order"], 4),
+                               fused_ref_order_vs_F_linear=round(t["F.linear"] / t["fused_ref_order"], 3))
+            del x, y, nib, sgm, zgm
             # decode: M = 1, cold, codes in the decode tile layout (what QuantLinear "auto" keeps)
             M = 1
             x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
@@ -792,7 +803,8 @@ def fused_forward_section(rot_bytes=1 << 30):
                       "vs F.linear on the dequantized fp16 weight, same run",
             "kernels": "M=8192: row-major codes k_w4a16_b16w (per channel 151, grouped 150), NIB codes "
                        "(QuantLinear nib_prefill) k_w4a16_b16p (persistent, 172) / b16w 152 (iwq_prefill16.hip); "
-                       "M=1: k_w4a16_gemv(_ct) on tile-layout codes",
+                       "grouped: group-major parameter copies (IWQ_FLAG_GROUP_MAJOR, what QuantLinear keeps), "
+                       "fused_ref_order = the reference's parameter order; M=1: k_w4a16_gemv(_ct) on tile-layout codes",
             "mfma_peak_TFLOPs": MFMA_PEAK_TFLOPS, "rows": out}
 
 

@@ -73,6 +73,11 @@ enum iwq_status {
 #define IWQ_FLAG_NIB_CODES 0x400u    /* iwq_w4a16_gemm: codes are in the NIB layout (iwq_nib_codes);
                                         M >= 256 only (the prefill kernel and its split-K form);
                                         IWQ_ERR_ARG with a variant, TILED or FORCE_GENERIC        */
+#define IWQ_FLAG_GROUP_MAJOR 0x800u  /* iwq_w4a16_gemm: scales / zeros are group-major, [K/group, N]
+                                        (element g * N + n), grouped weights only; the unsplit
+                                        prefill kernel only: M >= 256, N % 256 == 0, K % 64 == 0,
+                                        group % 64 == 0 (IWQ_ERR_ARG otherwise, with a variant,
+                                        TILED or FORCE_GENERIC); combines with IWQ_FLAG_NIB_CODES  */
 /* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
  * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
  * (40-49 / 60-81 / 150-172 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first

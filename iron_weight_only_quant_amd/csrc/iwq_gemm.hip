@@ -1251,6 +1251,23 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
   const bool split_pref = !short_pref && variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
                           prefill_split_preferred(M, N, K, a.gpr, a.group) &&
                           workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
+  if (flags & IWQ_FLAG_GROUP_MAJOR) {
+    // group-major parameters ([K/group, N]: a transposed copy held next to the codes): the grouped
+    // 16x16x32 prefill kernel only (150 / 152 stage a K-step's 256 scales and zero points as contiguous
+    // 512-B pieces instead of 256 halves 2 K/group bytes apart), unsplit, M >= 256; row-major or
+    // (IWQ_FLAG_NIB_CODES) NIB codes, the same bits as with the reference's parameter order
+    if ((flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_FORCE_GENERIC)) || variant != 0 || M < 256 || a.gpr == 1 ||
+        !prefill16_supported(M, N, K, a.gpr, a.group))
+      return IWQ_ERR_ARG;
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    p.pgm = 1;
+    const hipError_t e = prefill_b32_launch(p, 0, st, (flags & IWQ_FLAG_NIB_CODES) != 0);
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
+  }
   if (flags & IWQ_FLAG_NIB_CODES) {
     // NIB-layout codes (iwq_nib_codes): the prefill kernel only (the row-major default's NIB twin:
     // 172 per channel, 152 grouped, and the split-K form), M >= 256; every other path reads the

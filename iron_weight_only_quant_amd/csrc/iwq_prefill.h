@@ -23,7 +23,7 @@ struct PrefillArgs {
   float* ws = nullptr;     // split-K: fp32 partial tiles (prefill_splitk_bytes), else unused
   int nsplit = 1;          // split-K: number of K ranges
   int kps = 0;             // split-K: 64-k steps per range
-  int pgm = 0;             // grouped, 16x16x32 forms: scales / zeros held group-major, [gpr, N] (A/B)
+  int pgm = 0;             // grouped, 16x16x32 forms: scales / zeros held group-major, [gpr, N] (IWQ_FLAG_GROUP_MAJOR)
 };
 
 // mid-size M (k_w4a16_mid): N % 64 == 0, K % 128 == 0, per-channel or group % 32 == 0; codes

@@ -98,6 +98,23 @@ __device__ __forceinline__ void landed(T& v) {
   asm volatile("" : "+v"(v));
 }
 
+// grouped parameters from their raw dwords (the halfword in bits 0-15): the value in both halves
+// (one v_perm), and the zero point's dequant offsets 1024 + z / 64 + z as packed fp16 adds (one
+// rounding, as the float sum's conversion) -- 5 VALU per column instead of a float round trip each
+__device__ __forceinline__ h2 bcast_lo(uint32_t v) { return as_h2(__builtin_amdgcn_perm(v, v, 0x01000100u)); }
+__device__ __forceinline__ void zero_offsets(h2 z2, h2& zz, h2& zl, h2& zh) {
+  zz = z2 + h2{(_Float16)1024.0f, (_Float16)64.0f};
+  zl = z2 + h2{(_Float16)1024.0f, (_Float16)1024.0f};
+  zh = z2 + h2{(_Float16)64.0f, (_Float16)64.0f};
+}
+// K-step -> its parameter group ((kt * TK) / group, group % TK == 0) by a multiply-high, not a
+// division per DMA issue (exact while kt * group / TK < 2^32)
+struct KStepGroup {
+  uint32_t d, mul;
+  __device__ explicit KStepGroup(int group) : d((uint32_t)group / TK), mul(0xFFFFFFFFu / ((uint32_t)group / TK) + 1u) {}
+  __device__ int operator()(int kt) const { return d == 1 ? kt : (int)__umulhi((uint32_t)kt, mul); }
+};
+
 #define IWQ_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #define IWQ_PIN() __builtin_amdgcn_sched_barrier(0)
 
@@ -157,11 +174,12 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
     psrc = arr + (a.pgm ? c : c * a.gpr);
   }
   const int64_t pstep = a.pgm ? a.N : 1;  // parameter stride between groups
+  const KStepGroup kgrp(GROUPED ? a.group : TK);
   auto issue1 = [&](int kt, int stg, int i) {
     uint8_t* base = smem + stg * STAGE;
     if (i < 4) glds16(xsrc[i] + kt * TK, base + (wid * 4 + i) * 1024);
     else if (i == 4) glds16(csrc + kt * (TK / 2), base + XS + wid * 1024);
-    else if constexpr (GROUPED) glds2(psrc + ((kt * TK) / a.group) * pstep, base + XS + CS + wid * 256);
+    else if constexpr (GROUPED) glds2(psrc + kgrp(kt) * pstep, base + XS + CS + wid * 256);
   };
   auto issue = [&](int kt, int stg) {
 #pragma unroll
@@ -172,6 +190,7 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
   const int col0 = n0 + wid * 32 + r16;
   float sfl[2] = {1.0f, 1.0f};
   h2 s2[2], zz[2], zl[2], zh[2];
+  const h2 zsym2 = {(_Float16)a.zsym, (_Float16)a.zsym};
   auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
@@ -210,9 +229,8 @@ __global__ __launch_bounds__(THR) void k_w4a16_b16w(PrefillArgs a) {
       landed(pzv);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)psv[nt]);
-        s2[nt] = h2{sc, sc};
-        set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pzv[nt]) : a.zsym);
+        s2[nt] = bcast_lo(psv[nt]);
+        zero_offsets(a.zeros ? bcast_lo(pzv[nt]) : zsym2, zz[nt], zl[nt], zh[nt]);
       }
     }
   };
@@ -507,6 +525,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   }
   const _Float16* psrc[2] = {nullptr, nullptr};
   int64_t pstep = 1;
+  const KStepGroup kgrp(GROUPED ? a.group : TK);
   if constexpr (GROUPED) {
     const int64_t c = n0 + wid * 64 + lane;
     const int64_t off = a.pgm ? c : c * a.gpr;
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
     } else if (i < 10) {
       glds16(csrc[i - 8] + kt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
     } else if constexpr (GROUPED) {
-      glds2(psrc[i - 10] + ((kt * TK) / a.group) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+      glds2(psrc[i - 10] + kgrp(kt) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
     }
   };
   auto issue = [&](int kt, int s) {
@@ -533,6 +552,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   const int col0 = n0 + wid * 64 + r16;
   float sfl[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   h2 s2[4], zz[4], zl[4], zh[4];
+  const h2 zsym2 = {(_Float16)a.zsym, (_Float16)a.zsym};
   auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
@@ -567,9 +587,8 @@ __global__ __launch_bounds__(256) void k_w4a16_b16q(PrefillArgs a) {
   u32x2 pv[4];  // grouped: raw parameter dwords (scales of tiles 0/1, 2/3; zero points of 0/1, 2/3)
   auto set_params = [&](int nt) {
     if constexpr (GROUPED) {
-      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
-      s2[nt] = h2{sc, sc};
-      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+      s2[nt] = bcast_lo(pv[nt >> 1][nt & 1]);
+      zero_offsets(a.zeros ? bcast_lo(pv[2 + (nt >> 1)][nt & 1]) : zsym2, zz[nt], zl[nt], zh[nt]);
     }
   };
   // the code (+ parameter) reads of code slot offset CO into W / pv, in this order
@@ -909,6 +928,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   };
   float sepi[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   h2 s2[4], zz[4], zl[4], zh[4];
+  const h2 zsym2 = {(_Float16)a.zsym, (_Float16)a.zsym};
   auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
@@ -955,9 +975,8 @@ __global__ __launch_bounds__(256) void k_w4a16_b16p(PrefillArgs a) {
   u32x2 pv[4];
   auto set_params = [&](int nt) {  // grouped: the stage's (s, z)
     if constexpr (GROUPED) {
-      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
-      s2[nt] = h2{sc, sc};
-      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+      s2[nt] = bcast_lo(pv[nt >> 1][nt & 1]);
+      zero_offsets(a.zeros ? bcast_lo(pv[2 + (nt >> 1)][nt & 1]) : zsym2, zz[nt], zl[nt], zh[nt]);
     }
   };
   auto read_codes = [&](u32x2* w, uint32_t co) {
@@ -1233,6 +1252,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
   }
   const _Float16* psrc[2] = {nullptr, nullptr};
   int64_t pstep = 1;
+  const KStepGroup kgrp(GROUPED ? a.group : TK);
   if constexpr (GROUPED) {
     const int64_t c = n0 + wid * 64 + lane;
     const int64_t off = a.pgm ? c : c * a.gpr;
@@ -1246,7 +1266,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
     } else if (i < 10) {
       glds16(csrc[i - 8] + kt * (TK / 2), smem + CBASE + cs * CST + (wid * 2 + i - 8) * 1024);
     } else if constexpr (GROUPED) {
-      glds2(psrc[i - 10] + ((kt * TK) / a.group) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
+      glds2(psrc[i - 10] + kgrp(kt) * pstep, smem + CBASE + cs * CST + CS + (i - 10) * 1024 + wid * 256);
     }
   };
   auto issue = [&](int kt, int s) {
@@ -1257,6 +1277,7 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
   const int col0 = n0 + wid * 64 + r16;
   float sfl[4] = {1.0f, 1.0f, 1.0f, 1.0f};
   h2 s2[4], zz[4], zl[4], zh[4];
+  const h2 zsym2 = {(_Float16)a.zsym, (_Float16)a.zsym};
   auto set_zero = [&](int nt, float zf) {
     zz[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
     zl[nt] = h2{(_Float16)(1024.0f + zf), (_Float16)(1024.0f + zf)};
@@ -1288,9 +1309,8 @@ __global__ __launch_bounds__(256) void k_w4a16_b16r(PrefillArgs a) {
   u32x2 pv[4];
   auto set_params = [&](int nt) {
     if constexpr (GROUPED) {
-      const _Float16 sc = __builtin_bit_cast(_Float16, (uint16_t)pv[nt >> 1][nt & 1]);
-      s2[nt] = h2{sc, sc};
-      set_zero(nt, a.zeros ? (float)__builtin_bit_cast(_Float16, (uint16_t)pv[2 + (nt >> 1)][nt & 1]) : a.zsym);
+      s2[nt] = bcast_lo(pv[nt >> 1][nt & 1]);
+      zero_offsets(a.zeros ? bcast_lo(pv[2 + (nt >> 1)][nt & 1]) : zsym2, zz[nt], zl[nt], zh[nt]);
     }
   };
   auto read_codes = [&](u32x2* w, uint32_t co) {

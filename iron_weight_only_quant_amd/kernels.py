@@ -486,12 +486,37 @@ def _check_packed(what, dev, codes, scales, zeros, n_bits, group, N, K, bias=Non
         chk("bias", bias, N, torch.float16)
 
 
+def group_major_params(scales: torch.Tensor, zeros: Optional[torch.Tensor], N: int, K: int, group: int):
+    """Grouped scales / zeros in the reference's order ([N, K/group]) -> group-major copies
+    ([K/group, N], element g * N + n) for w4a16_gemm(..., scales_gm=, zeros_gm=): the prefill kernel
+    then stages a K-step's 256 parameters as contiguous pieces (IWQ_FLAG_GROUP_MAJOR)."""
+    if group == -2:
+        raise ValueError("group_major_params: grouped weights only (per channel has one group per row)")
+    gpr = K // group
+
+    def t(v):
+        return None if v is None else v.reshape(N, gpr).t().contiguous().view(-1)
+    return t(scales), t(zeros)
+
+
+def gm_prefill_applies(M: int, N: int, K: int, group: int) -> bool:
+    """Shapes and row counts at which w4a16_gemm reads group-major parameters (IWQ_FLAG_GROUP_MAJOR:
+    the unsplit 16x16x32 prefill kernel, grouped, M >= NIB_MIN_M, no split-K needed)."""
+    if group == -2 or M < NIB_MIN_M or N % 256 or K % 64 or group % 64 or K % group:
+        return False
+    lib = L.load()
+    return int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) == 0
+
+
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
-               tiled: bool = False, out: Optional[torch.Tensor] = None, nib: bool = False) -> torch.Tensor:
+               tiled: bool = False, out: Optional[torch.Tensor] = None, nib: bool = False,
+               scales_gm: Optional[torch.Tensor] = None, zeros_gm: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA).
     tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only.
     nib: `codes` is in the NIB layout (nib_codes), M >= NIB_MIN_M only (the prefill kernel).
+    scales_gm / zeros_gm: optional group-major copies of the grouped parameters
+    (group_major_params), read where gm_prefill_applies (same bits; scales / zeros elsewhere).
     out: optional contiguous fp16 [M, N] destination (rows of x flattened)."""
     if tiled:
         flags |= L.IWQ_FLAG_TILED_CODES
@@ -527,6 +552,13 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
         if 110 <= v < 150 and N % 256 == 0:  # short-tile split (A/B): 128- / 64-row tiles, S ranges
             mtw, ns = (4, v - 108) if v < 130 else (2, v - 128)
             ws_bytes = max(ws_bytes, ((M + 32 * mtw - 1) // (32 * mtw)) * (N // 256) * ns * mtw * 8192 * 4)
+        if (scales_gm is not None and not tiled and v == 0 and not (flags & L.IWQ_FLAG_FORCE_GENERIC)
+                and ws_bytes == 0 and gm_prefill_applies(M, N, K, group)):
+            _check_packed("w4a16_gemm", x.device, codes, scales_gm, zeros_gm, n_bits, group, N, K, bias)
+            if (zeros_gm is None) != (zeros is None):
+                raise ValueError("w4a16_gemm: zeros_gm must accompany zeros (and only zeros)")
+            flags |= L.IWQ_FLAG_GROUP_MAJOR
+            scales, zeros = scales_gm, zeros_gm
         ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
         st = lib.iwq_w4a16_gemm_ws(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                    int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, L.ptr(ws), ws_bytes,

@@ -94,18 +94,18 @@ class QuantLinear(nn.Module):
         self._buffers.update(quantized=torch.tensor(False), scales=None, zeros=None, weight_fp4=None,
                              weight_fp6=None, weight_fp8=None, weight_bfp_mantissa=None,
                              weight_bfp_exponent=None, qweight=None, qweight_tiled=None,
-                             qweight_nib=None)
+                             qweight_nib=None, scales_gm=None, zeros_gm=None)
         # the packed codes are a derived cache of (weight, scales, zeros), not part of the reference's
         # state: kept out of state_dict (a strict load of a reference checkpoint must match), and
         # dropped whenever a state_dict is loaded so the forward never runs on stale codes
-        self._non_persistent_buffers_set.update(("qweight", "qweight_tiled", "qweight_nib"))
+        self._non_persistent_buffers_set.update(("qweight", "qweight_tiled", "qweight_nib", "scales_gm", "zeros_gm"))
         self.register_load_state_dict_post_hook(QuantLinear._drop_codes_after_load)
         if _init_weight:
             self.reset_parameters()
 
     @staticmethod
     def _drop_codes_after_load(module, incompatible_keys):
-        module._buffers.update(qweight=None, qweight_tiled=None, qweight_nib=None)
+        module._buffers.update(qweight=None, qweight_tiled=None, qweight_nib=None, scales_gm=None, zeros_gm=None)
 
     def reset_parameters(self):
         nn.init.kaiming_uniform_(self.weight, a=5 ** 0.5)
@@ -166,10 +166,19 @@ class QuantLinear(nn.Module):
             # VALU per 8 weights; +0.5-1.2 % per channel, +-0 g128 at M = 8192, for 0.5 B per
             # weight more device memory: DESIGN.md section 5)
             nib = kernels.nib_codes(codes, rows, cols)
+        sgm = zgm = None
+        if (self.fused_forward is True and codes is not None and self.quant_dim == 0
+                and 2 <= self.w_bit <= 4 and rows % 256 == 0 and cols % 64 == 0
+                and self.w_group_size > 0 and self.w_group_size % 64 == 0 and cols % self.w_group_size == 0):
+            # prefill batches read group-major copies of the grouped parameters (4 B per group and
+            # row; the kernel then stages a K-step's 256 of them as contiguous pieces, +1.5-5 % at
+            # g128, M = 8192: DESIGN.md section 5)
+            sgm, zgm = kernels.group_major_params(scales.reshape(-1), None if zeros is None else zeros.reshape(-1),
+                                                  rows, cols, self.w_group_size)
         # registered buffers (see __init__), written without nn.Module.__setattr__'s per-name checks
         self._buffers.update(scales=scales.view(-1, 1),
                              zeros=zeros.view(-1, 1) if zeros is not None else None,
-                             qweight=codes, qweight_tiled=tiled, qweight_nib=nib,
+                             qweight=codes, qweight_tiled=tiled, qweight_nib=nib, scales_gm=sgm, zeros_gm=zgm,
                              weight_fp4=None, weight_fp6=None, weight_fp8=None)
         self.quantized.fill_(True)
 
@@ -265,10 +274,12 @@ class QuantLinear(nn.Module):
                                               self.w_group_size)):
                 return kernels.w4a16_gemm(input, self.qweight_nib, self.scales.view(-1),
                                           None if self.zeros is None else self.zeros.view(-1), self.w_bit,
-                                          self.w_group_size, self.out_features, self.bias, nib=True)
+                                          self.w_group_size, self.out_features, self.bias, nib=True,
+                                          scales_gm=self.scales_gm, zeros_gm=self.zeros_gm)
             return kernels.w4a16_gemm(input, self.qweight, self.scales.view(-1),
                                       None if self.zeros is None else self.zeros.view(-1), self.w_bit,
-                                      self.w_group_size, self.out_features, self.bias)
+                                      self.w_group_size, self.out_features, self.bias,
+                                      scales_gm=self.scales_gm, zeros_gm=self.zeros_gm)
         original_input_shape = input.shape
         weight = self.weight.to(input.dtype)
         out = F.linear(input, weight, self.bias)

@@ -335,3 +335,19 @@ def test_auto_fused_policy():
     # Llama-2-7B gate / up, per channel)
     assert P(8192, 11008, 4096, -2) and not P(2048, 11008, 4096, -2) and not P(8192, 11008, 4096, 128)
     assert not P(8192, 4096, 11008, -2) and not P(8192, 28672, 8192, -2)
+
+
+def test_group_major_params_layout():
+    """kernels.group_major_params: [N, K/g] reference order -> [K/g, N] (element g * N + n) for
+    IWQ_FLAG_GROUP_MAJOR; zeros follow the scales, symmetric (None) stays None; per channel refused."""
+    from iron_weight_only_quant_amd import kernels as K
+    N, Kd, g = 256, 1024, 128
+    s = torch.arange(N * Kd // g, dtype=torch.float32).half()
+    z = (torch.arange(N * Kd // g) % 16).half()
+    sg, zg = K.group_major_params(s, z, N, Kd, g)
+    for n, gi in ((0, 0), (3, 5), (255, 7)):
+        assert sg[gi * N + n] == s[n * (Kd // g) + gi] and zg[gi * N + n] == z[n * (Kd // g) + gi]
+    assert sg.is_contiguous() and sg.numel() == s.numel()
+    assert K.group_major_params(s, None, N, Kd, g)[1] is None
+    with pytest.raises(ValueError):
+        K.group_major_params(s, z, N, Kd, -2)

@@ -1093,6 +1093,90 @@ def test_w4a16_nib_default(K, M, group):
         assert torch.equal(yl, y0)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256, 4096, 4096), (512, 512, 4608), (2304, 768, 2304)])
+@pytest.mark.parametrize("group,sym", [(128, False), (64, True), (256, False), (192, False)])
+def test_w4a16_group_major_params(K, M, N, Kd, group, sym):
+    """IWQ_FLAG_GROUP_MAJOR: the prefill kernel reading group-major copies of the parameters returns the
+    bits of the reference-order call on the same kernel, row-major and NIB codes; where it does not
+    apply (split-K wanted, M < 256, per channel, variants) the C-ABI refuses it and w4a16_gemm keeps the
+    reference-order parameters."""
+    if Kd % group:
+        pytest.skip("group must divide K")
+    torch.manual_seed(21)
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 97)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    sgm, zgm = K.group_major_params(r.scales, r.zeros, N, Kd, group)
+    gpr = Kd // group
+    assert torch.equal(sgm.view(gpr, N), r.scales.view(N, gpr).t())
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    nib = K.nib_codes(r.codes, N, Kd)
+    L = K.L
+    lib = L.load()
+
+    def raw(cd, sc, zr, fl, m=M):
+        y = torch.empty(m, N, dtype=torch.float16, device=DEV)
+        st = lib.iwq_w4a16_gemm(L.ptr(x), m, Kd, Kd, L.ptr(cd), L.ptr(sc), L.ptr(zr), 4, group, N, L.ptr(b),
+                                L.ptr(y), N, fl, L.stream_handle(x.device))
+        return st, y
+    # unsplit prefill kernel, reference order (NIB flag: the prefill kernel at any M >= 256) vs group-major
+    st0, y0 = raw(nib, r.scales, r.zeros, L.IWQ_FLAG_NIB_CODES)
+    st1, y1 = raw(nib, sgm, zgm, L.IWQ_FLAG_NIB_CODES | L.IWQ_FLAG_GROUP_MAJOR)
+    st2, y2 = raw(r.codes, sgm, zgm, L.IWQ_FLAG_GROUP_MAJOR)
+    assert (st0, st1, st2) == (0, 0, 0)
+    assert torch.equal(y0, y1) and torch.equal(y0, y2)
+    ref = x.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (x.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    assert bool(((y1.float() - ref).abs() <= tol).all())
+    # the Python face: group-major where gm_prefill_applies, else the reference order -- same bits either way
+    yk = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b, scales_gm=sgm, zeros_gm=zgm)
+    yd = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
+    assert torch.equal(yk, yd)
+    if K.gm_prefill_applies(M, N, Kd, group):
+        assert torch.equal(yk, y2)
+    # refusals
+    assert raw(r.codes, sgm, zgm, L.IWQ_FLAG_GROUP_MAJOR, m=255)[0] == L.IWQ_ERR_ARG
+    assert raw(r.codes, sgm, zgm, L.IWQ_FLAG_GROUP_MAJOR | L.IWQ_FLAG_FORCE_GENERIC)[0] == L.IWQ_ERR_ARG
+    assert raw(r.codes, sgm, zgm, L.IWQ_FLAG_GROUP_MAJOR | K.gemm_variant_flags(150))[0] == L.IWQ_ERR_ARG
+
+
+def test_w4a16_group_major_refuses_per_channel(K):
+    N, Kd, M = 512, 1024, 512
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 98)
+    r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+    x = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    y = torch.empty(M, N, dtype=torch.float16, device=DEV)
+    L = K.L
+    st = L.load().iwq_w4a16_gemm(L.ptr(x), M, Kd, Kd, L.ptr(r.codes), L.ptr(r.scales), L.ptr(r.zeros), 4, -2, N,
+                                 None, L.ptr(y), N, L.IWQ_FLAG_GROUP_MAJOR, L.stream_handle(x.device))
+    assert st == L.IWQ_ERR_ARG
+    with pytest.raises(ValueError):
+        K.group_major_params(r.scales, r.zeros, N, Kd, -2)
+
+
+@pytest.mark.parametrize("group", [128, -2])
+def test_quantlinear_group_major_params(K, group):
+    """fused_forward=True on grouped weights keeps group-major parameter copies (non-persistent, dropped
+    on load); the forward reads them at prefill sizes: the same bits as the reference-order call."""
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    lin = torch.nn.Linear(1024, 512, bias=True).half().to(DEV)
+    q = QuantLinear.from_linear(lin, w_bit=4, w_group_size=group, symmetric=False, fused_forward=True)
+    if group == -2:
+        assert q.scales_gm is None and q.zeros_gm is None
+        return
+    assert q.scales_gm is not None and "scales_gm" not in q.state_dict()
+    assert torch.equal(q.scales_gm.view(1024 // group, 512), q.scales.view(512, -1).t())
+    z = q.zeros.view(-1)
+    for shape in ((2, 300, 1024), (100, 1024), (1024, 1024)):
+        x = torch.randn(*shape, device=DEV).half()
+        ref = K.w4a16_gemm(x, q.qweight, q.scales.view(-1), z, 4, group, 512, q.bias)
+        assert torch.equal(q(x), ref), shape
+    q.load_state_dict(q.state_dict())
+    assert q.scales_gm is None and q.zeros_gm is None
+
+
 @pytest.mark.parametrize("M", [256, 384])
 @pytest.mark.parametrize("group", [-2, 128])
 def test_w4a16_nib_default_wide_unsplit(K, M, group):

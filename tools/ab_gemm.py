@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--warm-seconds", type=float, default=2.0)
     ap.add_argument("--lib", default=None, help="load this library build instead (A/B of two builds)")
     ap.add_argument("--tag", default=None)
+    ap.add_argument("--scales", default="data", choices=("data", "pow2", "ones"),
+                    help="DIAGNOSTIC: replace the scales by 2^round(log2 s) or 1 (low-entropy B operand; "
+                         "hipblaslt then runs on the matching dequantized weight)")
     a = ap.parse_args()
     if a.lib:
         from iron_weight_only_quant_amd import _lib
@@ -60,6 +63,11 @@ def main():
         w = torch.empty(N, K, dtype=torch.float16, device="cuda")
         kernels.fill_synthetic(w, 7)
         r = kernels.quantize_minmax(w, 4, a.group, False, 0, want_codes=True)
+        if a.scales != "data":
+            s = r.scales.float()
+            s = torch.ones_like(s) if a.scales == "ones" else torch.exp2(torch.round(torch.log2(s)))
+            r.scales.copy_(s.half())
+            kernels.dequant_packed(r.codes, r.scales, r.zeros, 4, a.group, N, K, out=r.out)
         x = (torch.randn(a.m, K, device="cuda") * 0.5).half()
         y = torch.empty(a.m, N, dtype=torch.float16, device="cuda")
         arms = {"hipblaslt": lambda: torch.nn.functional.linear(x, r.out)}
@@ -69,6 +77,17 @@ def main():
             toks.remove("nib")
             nc = kernels.nib_codes(r.codes, N, K)
             arms["nib"] = lambda nc=nc: kernels.w4a16_gemm(x, nc, r.scales, r.zeros, 4, a.group, N, out=y, nib=True)
+        if "gm" in toks or "nibgm" in toks:  # group-major parameter copies (IWQ_FLAG_GROUP_MAJOR), grouped only
+            sgm, zgm = kernels.group_major_params(r.scales, r.zeros, N, K, a.group)
+            if "gm" in toks:
+                toks.remove("gm")
+                arms["gm"] = lambda sgm=sgm, zgm=zgm: kernels.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, a.group, N,
+                                                                         out=y, scales_gm=sgm, zeros_gm=zgm)
+            if "nibgm" in toks:
+                toks.remove("nibgm")
+                ncg = kernels.nib_codes(r.codes, N, K)
+                arms["nibgm"] = lambda sgm=sgm, zgm=zgm, ncg=ncg: kernels.w4a16_gemm(
+                    x, ncg, r.scales, r.zeros, 4, a.group, N, out=y, nib=True, scales_gm=sgm, zeros_gm=zgm)
         for v in [int(t) for t in toks]:
             fl = kernels.gemm_variant_flags(v)
             cd = nib if v in NIB_VARIANTS else r.codes
