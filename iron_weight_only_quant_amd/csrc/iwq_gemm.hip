@@ -1256,12 +1256,14 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     // 16x16x32 prefill kernel only (150 / 152 stage a K-step's 256 scales and zero points as contiguous
     // 512-B pieces instead of 256 halves 2 K/group bytes apart), unsplit, M >= 256; row-major or
     // (IWQ_FLAG_NIB_CODES) NIB codes, the same bits as with the reference's parameter order
-    if ((flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_FORCE_GENERIC)) || variant != 0 || M < 256 || a.gpr == 1 ||
-        !prefill16_supported(M, N, K, a.gpr, a.group))
+    // (A/B builds: also the grouped 16x16x32 variants 150-172, codes in the variant's own layout)
+    const bool abv = IWQ_AB && variant >= 150 && variant <= 172 && !(flags & IWQ_FLAG_NIB_CODES);
+    if ((flags & (IWQ_FLAG_TILED_CODES | IWQ_FLAG_FORCE_GENERIC)) || (variant != 0 && !abv) || M < 256 ||
+        a.gpr == 1 || !prefill16_supported(M, N, K, a.gpr, a.group))
       return IWQ_ERR_ARG;
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
     p.pgm = 1;
-    const hipError_t e = prefill_b32_launch(p, 0, st, (flags & IWQ_FLAG_NIB_CODES) != 0);
+    const hipError_t e = prefill_b32_launch(p, (int)variant, st, (flags & IWQ_FLAG_NIB_CODES) != 0);
     if (e != hipSuccess) {
       iwq::last_hip_error() = (int)e;
       return IWQ_ERR_HIP;

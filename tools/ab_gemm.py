@@ -88,6 +88,14 @@ def main():
                 ncg = kernels.nib_codes(r.codes, N, K)
                 arms["nibgm"] = lambda sgm=sgm, zgm=zgm, ncg=ncg: kernels.w4a16_gemm(
                     x, ncg, r.scales, r.zeros, 4, a.group, N, out=y, nib=True, scales_gm=sgm, zeros_gm=zgm)
+        for t in [t for t in toks if t.startswith("gm")]:  # gmNNN: A/B variant NNN on group-major parameters
+            toks.remove(t)
+            v = int(t[2:])
+            sgm, zgm = kernels.group_major_params(r.scales, r.zeros, N, K, a.group)
+            cd = nib if v in NIB_VARIANTS else r.codes
+            fl = kernels.gemm_variant_flags(v) | kernels.L.IWQ_FLAG_GROUP_MAJOR
+            arms[t] = (lambda fl=fl, cd=cd, sgm=sgm, zgm=zgm: kernels.w4a16_gemm(x, cd, sgm, zgm, 4, a.group, N,
+                                                                                  flags=fl, out=y))
         for v in [int(t) for t in toks]:
             fl = kernels.gemm_variant_flags(v)
             cd = nib if v in NIB_VARIANTS else r.codes
