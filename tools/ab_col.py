@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--cols", type=int, default=4096)
     ap.add_argument("--copies", type=int, default=16)
     ap.add_argument("--group", type=int, default=128)
+    ap.add_argument("--variants", default="", help="comma list (default: every block shape of the group)")
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels as K
     ws = []
@@ -35,7 +36,8 @@ def main():
         for w, o in zip(ws, outs):
             K.quantize_minmax(w, 4, a.group, False, 1, out=o)
     torch.cuda.synchronize()
-    for v in ((0, 1, 2, 3, 4) if a.group in (32, 64) else (0, 1, 2, 3)):
+    vs = [int(t) for t in a.variants.split(",")] if a.variants else ((0, 1, 2, 3, 4) if a.group in (32, 64) else (0, 1, 2, 3))
+    for v in vs:
         flags = K.gemm_variant_flags(v)
         r = K.quantize_minmax(ws[0], 4, a.group, False, 1, flags=flags).out
         assert torch.equal(r.view(torch.int16), ref.view(torch.int16)), v
