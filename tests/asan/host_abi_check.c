@@ -143,6 +143,12 @@ static void check_gemm_validation(void) {
   /* NIB codes: M >= 256 only, no variant / tiled / generic */
   CHECK(iwq_w4a16_gemm(x, 128, 4096, 4096, c, s, NULL, 4, -2, 4096, NULL, y, 4096, IWQ_FLAG_NIB_CODES, NULL) == IWQ_ERR_ARG);
   CHECK(iwq_w4a16_gemm(x, 17, 4096, 4096, c, s, NULL, 4, -2, 4096, NULL, y, 4096, IWQ_FLAG_TILED_CODES, NULL) == IWQ_ERR_ARG);
+  /* group-major parameters: grouped weights, M >= 256, no variant / TILED / FORCE_GENERIC */
+  CHECK(iwq_w4a16_gemm(x, 512, 4096, 4096, c, s, NULL, 4, -2, 4096, NULL, y, 4096, IWQ_FLAG_GROUP_MAJOR, NULL) == IWQ_ERR_ARG);
+  CHECK(iwq_w4a16_gemm(x, 255, 4096, 4096, c, s, NULL, 4, 128, 4096, NULL, y, 4096, IWQ_FLAG_GROUP_MAJOR, NULL) == IWQ_ERR_ARG);
+  CHECK(iwq_w4a16_gemm(x, 512, 4096, 4096, c, s, NULL, 4, 128, 4096, NULL, y, 4096,
+                       IWQ_FLAG_GROUP_MAJOR | IWQ_FLAG_FORCE_GENERIC, NULL) == IWQ_ERR_ARG);
+  CHECK(iwq_w4a16_gemm(x, 512, 4096, 4096, c, s, NULL, 4, 32, 4096, NULL, y, 4096, IWQ_FLAG_GROUP_MAJOR, NULL) == IWQ_ERR_ARG);
   for (int64_t m = 1; m <= 8192; m *= 2) {
     CHECK(iwq_w4a16_gemm_workspace_bytes(m, 4096, 4096, -2) >= 0);
     CHECK(iwq_w4a16_gemm_workspace_bytes(m, 28672, 8192, 128) >= 0);
