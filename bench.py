@@ -38,6 +38,47 @@ MODEL_NAME = {"llama2-7b": "Llama-2-7B", "llama2-70b": "Llama-2-70B", "opt-125m"
 
 
 
+class Marks:
+    """--mark-file: the host-clock interval of every timed region (synchronized on both sides), so a
+    rocprofv3 --kernel-trace of the same run can be cut into the regions afterwards
+    (tools/trace_sections.py): per region, the kernels that ran in it and their average duration, to set
+    beside the number bench.py reports for it.  No-op (no extra synchronization) without the flag."""
+
+    def __init__(self):
+        self.rows = None
+
+    def enable(self):
+        self.rows = []
+
+    def region(self, name, **info):
+        import contextlib
+        if self.rows is None:
+            return contextlib.nullcontext({})
+
+        @contextlib.contextmanager
+        def cm():
+            rec = {"region": name, **info}
+            torch.cuda.synchronize()
+            rec["t0"] = {"boot": time.clock_gettime_ns(time.CLOCK_BOOTTIME), "mono": time.monotonic_ns(),
+                         "real": time.time_ns()}
+            yield rec
+            torch.cuda.synchronize()
+            rec["t1"] = {"boot": time.clock_gettime_ns(time.CLOCK_BOOTTIME), "mono": time.monotonic_ns(),
+                         "real": time.time_ns()}
+            self.rows.append(rec)
+        return cm()
+
+    def write(self, path, rank):
+        if self.rows is None or not path:
+            return
+        with open(path if rank == 0 else f"{path}.rank{rank}", "w") as f:
+            for r in self.rows:
+                f.write(json.dumps(r) + "\n")
+
+
+MARKS = Marks()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,7 +94,10 @@ def parse():
                     help="headline = weak scaling instead: every rank quantizes the full model")
     ap.add_argument("--no-weak", action="store_true", help="7B at N > 1: skip the secondary weak-scaling figure")
     ap.add_argument("--gather", action="store_true",
-                    help="also time the rooted gather of packed codes+scales to rank 0 (RCCL), reported separately")
+                    help="(default at N > 1, kept for old command lines) time the rooted gather of the packed "
+                         "codes + scales/zeros to rank 0 over RCCL, reported separately (never in value)")
+    ap.add_argument("--no-collectives", action="store_true",
+                    help="N > 1: skip the separately timed RCCL gather / scatter (gather_ms, scatter_ms)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank plumbing (spawn, shard plan, rooted gather) over gloo; "
                          "no GPU, no kernels, no timing")
@@ -64,6 +108,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ppl", action="store_true", help="skip the PPL-harness plumbing run (random-init OPT-125M)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--traffic-70b-file", default=os.path.join(ROOT, "profiles", "traffic_70b.json"))
     ap.add_argument("--variant", type=int, default=0, help="kernel tuning variant for the timed run")
     ap.add_argument("--variants", default="", help="A/B: comma list of variants timed in interleaved rounds")
     ap.add_argument("--rounds", type=int, default=5)
@@ -77,6 +122,9 @@ def parse():
     ap.add_argument("--no-sections", action="store_true",
                     help="skip the configs[2] fused-forward, configs[4] format and configs[3] 70B sections")
     ap.add_argument("--no-70b", action="store_true", help="skip the configs[3] Llama-2-70B section")
+    ap.add_argument("--mark-file", default="",
+                    help="write the host-clock interval of every timed region (JSONL) for tools/trace_sections.py "
+                         "(cuts a rocprofv3 kernel trace of this run into the bench's rows)")
     return ap.parse_args()
 
 
@@ -221,6 +269,10 @@ def scatter_weights(model, rank, world):
             sends.append(flat)
     else:
         recv = torch.empty(layouts[rank][1], dtype=torch.float16, device="cuda")
+    # warm: one small transfer per peer through the same path, so the timed scatter does not pay
+    # RCCL's lazy point-to-point connection setup
+    small = [torch.zeros(1 << 19, dtype=torch.float16, device="cuda") for _ in range(world)] if rank == 0 else None
+    shard.scatter_from_rank0(small, None if rank == 0 else torch.empty(1 << 19, dtype=torch.float16, device="cuda"))
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
@@ -232,7 +284,8 @@ def scatter_weights(model, rank, world):
         sends = [mine]  # drop the other ranks' copies on rank 0
     views = shard.views_of(mine, layouts[rank][0])
     names = [n for n, _, _ in layouts[rank][0]]
-    return [views[n] for n in names], names, shapes, round(ms, 3)
+    nbytes = 2 * sum(layouts[r][1] for r in range(1, world))  # fp16 bytes that left rank 0
+    return [views[n] for n in names], names, shapes, round(ms, 3), nbytes
 
 
 def ppl_plumbing(bits, group, symmetric, chunks=8, seqlen=2048):
@@ -341,6 +394,33 @@ def time_gather(plan, names, all_shapes, args, ws_n):
     return round(ms, 3), stats.get("recv_bytes", 0)
 
 
+def gather_section(plan, names, all_shapes, args, ws_n):
+    """N > 1, default: the packed results of this rank's bin (codes + scales/zeros, what a rank would
+    hand back) produced by one codes-writing launch over the same weights (outside the headline's
+    timed region), then the rooted gather to rank 0 timed alone (shard.gather_to_rank0: one
+    point-to-point send per rank, every receive posted together on rank 0)."""
+    from iron_weight_only_quant_amd import kernels
+    gplan = kernels.BatchPlan(plan.weights, args.bits, args.group, args.symmetric, outs=plan.outs, want_codes=True)
+    gplan.run()
+    torch.cuda.synchronize()
+    ms, nbytes = time_gather(gplan, names, all_shapes, args, ws_n)
+    del gplan
+    torch.cuda.empty_cache()
+    return {"gather_ms": ms, "gather_bytes_to_rank0": nbytes,
+            "gather_GBps": round(nbytes / ms / 1e6, 1) if ms else None}
+
+
+def scatter_section(model, rank, ws_n):
+    """N > 1, default (bounded): the whole model's fp16 weights from rank 0 to their owners
+    (shard.scatter_from_rank0 over RCCL, one send per destination, all in flight), timed alone after
+    a small warm-up transfer; the received buffers are dropped again."""
+    _, _, _, ms, nbytes = scatter_weights(model, rank, ws_n)
+    torch.cuda.empty_cache()
+    return {"scatter_ms": ms, "scatter_bytes_from_rank0": nbytes,
+            "scatter_GBps": round(nbytes / ms / 1e6, 1) if ms else None,
+            "scatter_model": MODEL_NAME[model]}
+
+
 def dry_run(args, ws_n, rank):
     """--dry-run: the multi-rank plumbing without a GPU (CPU tests): every rank builds zero-filled
     packed results of its bin's sizes, the rooted gather moves them to rank 0, and rank 0 prints the
@@ -361,22 +441,48 @@ def dry_run(args, ws_n, rank):
         zeros.append(None if args.symmetric else torch.zeros(G, dtype=torch.float16))
     res = shard.ShardResult(names, codes, scales, zeros)
     sent, recv, got = 0, 0, 0
-    if ws_n > 1:
+    coll = {}
+    if ws_n > 1 and not args.no_collectives:
         import torch.distributed as dist
         stats = {}
+        dist.barrier()
+        t0 = time.perf_counter()
         out = shard.gather_to_rank0(res, dict(shapes), [[shapes[i][0] for i in b] for b in bins], args.bits,
                                     args.group, args.symmetric, stats=stats)
+        dist.barrier()
+        gather_ms = max_over_ranks((time.perf_counter() - t0) * 1e3, ws_n)
         t = torch.tensor([stats["sent_bytes"], stats["recv_bytes"]], dtype=torch.int64)
         dist.all_reduce(t)
         sent, recv = int(t[0]), int(t[1])
         got = len(out) if out is not None else 0
+        # the scatter of the model's fp16 bins from rank 0 (CPU buffers over gloo; bin r filled with
+        # the value r + 1 so every receiver checks it got its own bin)
+        layouts = [shard.bin_layout(shapes, b) for b in bins]
+        sends = [torch.full((tot,), float(r + 1), dtype=torch.float16) for r, (_, tot) in enumerate(layouts)] \
+            if rank == 0 else None
+        rbuf = None if rank == 0 else torch.empty(layouts[rank][1], dtype=torch.float16)
+        dist.barrier()
+        t0 = time.perf_counter()
+        got_bin = shard.scatter_from_rank0(sends, rbuf)
+        dist.barrier()
+        scatter_ms = max_over_ranks((time.perf_counter() - t0) * 1e3, ws_n)
+        ok = torch.tensor([int(got_bin.numel() == layouts[rank][1] and bool((got_bin == rank + 1).all()))])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        sbytes = 2 * sum(tot for _, tot in layouts[1:])
+        coll = {"gather_ms": round(gather_ms, 3), "gather_bytes_to_rank0": recv,
+                "gather_GBps": round(recv / gather_ms / 1e6, 3),
+                "scatter_ms": round(scatter_ms, 3), "scatter_bytes_from_rank0": sbytes,
+                "scatter_GBps": round(sbytes / scatter_ms / 1e6, 3), "scatter_model": MODEL_NAME[args.model],
+                "scatter_verified": bool(ok.item())}
     # the record's multi-rank plumbing with stand-in timings (no GPU): per-rank statistics gathered
     # over gloo, the roofline over ranks, the CPU baseline on rank 0 (a small CPU sample)
     kernel_ms = 1.0 + 0.25 * rank  # stand-in: rank r "took" 1 + r/4 ms
     numel = sum(shapes[i][1][0] * shapes[i][1][1] for i in mine)
     alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
-    per_rank = gather_per_rank([kernel_ms, alg], ws_n)
-    roof = roofline_record(per_rank, "k_group<f16,128,asym,batched>", None, "dry run: no PMC")
+    ceil = 5000.0 - 100.0 * rank  # stand-in: each rank's own in-run copy ceiling
+    per_rank = gather_per_rank([kernel_ms, alg, ceil], ws_n)
+    roof = roofline_record(per_rank, "k_group<f16,128,asym,batched>", None, "dry run: no PMC",
+                           {"GBps": ceil, "forms": {"stand-in": ceil}})
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle.synth import synth
@@ -388,8 +494,9 @@ def dry_run(args, ws_n, rank):
             "dry_run": True, "world": ws_n, "model": args.model, "tensors": len(shapes),
             "tensors_at_rank0": got,
             "plan_packed_bytes_per_rank": [sum(nb(shapes[i][1]) for i in b) for b in bins],
-            "gather_sent_bytes": sent, "gather_recv_bytes": recv, "cpu_baseline": cpu})
-        rec["note"] = "dry run over gloo on the CPU: stand-in timings, no GPU"
+            "gather_sent_bytes": sent, "gather_recv_bytes": recv, "cpu_baseline": cpu, **coll})
+        rec["note"] = ("dry run over gloo on the CPU: stand-in kernel timings, no GPU; gather / scatter times are "
+                       "gloo over loopback")
         print(json.dumps(rec), flush=True)
 
 
@@ -405,20 +512,22 @@ def kernel_sources_sha():
     return h.hexdigest()[:16]
 
 
-def committed_traffic(path, numel, bits, group):
-    """HBM bytes per launch from the committed PMC record, if it was measured on this workload AND
-    on the current kernel sources; (bytes or None, reason)."""
+def committed_traffic(path, numel, bits, group, placement="out-of-place"):
+    """HBM bytes per launch from the committed PMC record, if it was measured on this workload (and
+    placement) AND on the current kernel sources; (bytes or None, reason)."""
+    rel = os.path.relpath(path, ROOT)
     if not os.path.exists(path):
-        return None, "no PMC record"
+        return None, f"no PMC record ({rel})"
     try:
         tf = json.load(open(path))
     except (OSError, ValueError):
-        return None, "unreadable PMC record"
-    if tf.get("workload_numel") != numel or tf.get("bits") != bits or tf.get("group") != group:
-        return None, "PMC record is for another workload"
+        return None, f"unreadable PMC record ({rel})"
+    if (tf.get("workload_numel") != numel or tf.get("bits") != bits or tf.get("group") != group
+            or tf.get("placement", "out-of-place") != placement):
+        return None, f"PMC record {rel} is for another workload"
     if tf.get("kernel_sources_sha") != kernel_sources_sha():
-        return None, "PMC record predates the current kernel sources"
-    return tf.get("hbm_bytes_per_launch"), "profiles/traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE, same sources)"
+        return None, f"PMC record {rel} predates the current kernel sources"
+    return tf.get("hbm_bytes_per_launch"), f"{rel} (rocprofv3 FETCH_SIZE/WRITE_SIZE, same sources)"
 
 
 def clock_ramp(plan, seconds):
@@ -495,14 +604,16 @@ def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
         torch.cuda.synchronize()
         st = torch.cuda.current_stream()
         ts = []
-        for _ in range(rounds):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            g.replay()
-            e1.record(st)
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) / len(idx) * 1e-3)
+        with MARKS.region(f"shapes/{shp[0]}x{shp[1]}", calls_per_replay=len(idx), replays=rounds) as mk:
+            for _ in range(rounds):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                g.replay()
+                e1.record(st)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / len(idx) * 1e-3)
         ts.sort()
+        mk["bench_us_per_call"] = round(ts[len(ts) // 2] * 1e6, 3)
         t = max_over_ranks(ts[len(ts) // 2], ws_n)
         n = shp[0] * shp[1]
         alg = n * 4 + (n // args.group) * 2 * (1 if args.symmetric else 2)
@@ -576,9 +687,13 @@ def ab_variants(plan, variants, args):
               file=sys.stderr, flush=True)
 
 
-def timed_steps(plan, args, ws_n, stream):
+def timed_steps(plan, args, ws_n, stream, region="headline"):
     """W untimed warmup steps, then EXACTLY K steps bracketed by barrier + synchronize on both sides.
     Returns (kernel ms per launch from HIP events on the launch stream, max-over-ranks wall ms per step)."""
+    return _timed_steps(plan, args, ws_n, stream, region)
+
+
+def _timed_steps(plan, args, ws_n, stream, region):
     for _ in range(args.warmup):
         plan.run(stream, variant=args.variant)
     torch.cuda.synchronize()
@@ -587,15 +702,17 @@ def timed_steps(plan, args, ws_n, stream):
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        plan.run(stream, variant=args.variant)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier(ws_n)
-    wall = time.perf_counter() - t0
+    with MARKS.region(region, launches=args.steps) as mk:  # exactly the K timed launches
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(args.steps):
+            plan.run(stream, variant=args.variant)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        barrier(ws_n)
+        wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    mk["bench_kernel_ms"] = round(kernel_ms, 5)
     return kernel_ms, max_over_ranks(wall, ws_n) / args.steps * 1e3
 
 
@@ -618,7 +735,7 @@ def weak_secondary(args, ws_n, rank):
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric)
     stream = torch.cuda.current_stream()
     clock_ramp(plan, 0.2)
-    kernel_ms, ms = timed_steps(plan, args, ws_n, stream)
+    kernel_ms, ms = timed_steps(plan, args, ws_n, stream, region="weak")
     total = all_ranks_sum(plan.numel, ws_n)
     shapes = None if args.no_shapes else per_shape(plan, names, ws_n, args)
     del plan, weights
@@ -627,6 +744,13 @@ def weak_secondary(args, ws_n, rank):
             "kernel_ms_rank0": round(kernel_ms, 4), "fp16_weights_total": total,
             "workload": f"every rank quantizes all {len(make_shapes(args.model))} Linear weights of "
                         f"{MODEL_NAME[args.model]}"}, shapes
+
+
+def shard_bin_elems(model, world):
+    """Elements of each rank's flat bin buffer (shard.bin_layout) for the model over `world` ranks."""
+    from iron_weight_only_quant_amd import shard
+    shapes = shard.model_linear_shapes(model)
+    return [shard.bin_layout(shapes, b)[1] for b in shard.plan_shards(shapes, world)]
 
 
 def make_shapes(model):
@@ -649,24 +773,40 @@ def gather_per_rank(vals, ws_n):
 
 
 def roofline_record(per_rank, kernel_name, traffic, traffic_src, ceiling=None, other=None):
-    """HBM roofline of the headline kernel over all ranks.  per_rank = [kernel_ms, alg_bytes] per rank
-    (HIP-event time of its launch on its stream; its algorithmic bytes per launch).  `achieved` is
-    per GPU: the mean algorithmic bytes per rank over the SLOWEST rank's kernel time (what the
-    max-over-ranks step time sees); `per_rank` gives each rank's own rate and fraction."""
-    kmax = max(k for k, _ in per_rank)
-    mean_bytes = sum(b for _, b in per_rank) / len(per_rank)
+    """HBM roofline of the headline kernel over all ranks.  per_rank = [kernel_ms, alg_bytes(,
+    ceiling_GBps)] per rank (HIP-event time of its launch on its stream; its algorithmic bytes per
+    launch; the in-run copy ceiling of its own GPU).  `achieved` is per GPU: the mean algorithmic
+    bytes per rank over the SLOWEST rank's kernel time (what the max-over-ranks step time sees);
+    `per_rank` gives each rank's own rate, fraction and kernel / ceiling ratio.  At N > 1 the top-level
+    `kernel_over_ceiling` is the lowest rank's ratio."""
+    kmax = max(p[0] for p in per_rank)
+    mean_bytes = sum(p[1] for p in per_rank) / len(per_rank)
     achieved = mean_bytes / (kmax / 1e3) / 1e9 if kmax > 0 else None
+    rows = []
+    for r, p in enumerate(per_rank):
+        k, b = p[0], p[1]
+        row = {"rank": r, "kernel_ms": round(k, 4), "alg_bytes": int(b),
+               "frac": (round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k > 0 else None)}
+        if len(p) > 2 and p[2] > 0 and k > 0:
+            row["ceiling_GBps"] = round(p[2], 1)
+            row["kernel_over_ceiling"] = round(b / (k / 1e3) / 1e9 / p[2], 4)
+        rows.append(row)
     rec = {"bound": "hbm", "achieved": None if achieved is None else round(achieved, 1), "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
            "traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_name,
            "kernel_ms": round(kmax, 4), "kernel_ms_basis": "max over ranks" if len(per_rank) > 1 else "rank 0",
            "alg_bytes_per_launch": int(round(mean_bytes)) if len(per_rank) > 1 else int(per_rank[0][1]),
-           "per_rank": [{"rank": r, "kernel_ms": round(k, 4), "alg_bytes": int(b),
-                         "frac": (round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k > 0 else None)}
-                        for r, (k, b) in enumerate(per_rank)]}
+           "per_rank": rows}
     if ceiling is not None:
-        rec["ceiling"] = ceiling
-        rec["kernel_over_ceiling"] = round(achieved / ceiling["GBps"], 4) if achieved else None
+        if len(per_rank) == 1:
+            rec["ceiling"] = ceiling
+            rec["kernel_over_ceiling"] = round(achieved / ceiling["GBps"], 4) if achieved else None
+        else:
+            ratios = [row["kernel_over_ceiling"] for row in rows if "kernel_over_ceiling" in row]
+            rec["ceiling"] = {"GBps": round(min(row.get("ceiling_GBps", 0) for row in rows), 1),
+                              "basis": "lowest rank's in-run ceiling (each rank's in per_rank)",
+                              "forms_rank0": ceiling.get("forms")}
+            rec["kernel_over_ceiling"] = min(ratios) if ratios else None
     if other is not None:
         rec["other_placement"] = other
     return rec
@@ -680,10 +820,11 @@ MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md chip table; ne
 FF_SHAPES = (("q_proj", 4096, 4096), ("gate_proj", 11008, 4096), ("down_proj", 4096, 11008))
 
 
-def _interleaved_ms(arms, reps=5, rounds=7):
+def _interleaved_ms(arms, reps=5, rounds=7, region=None):
     """Median ms per call of each arm: every round times each arm once (reps calls back to back, HIP
     events on the current stream -- the stream every arm launches on), arms in rotating order
-    (cdna_hip_programming.md §5.4 rule 24)."""
+    (cdna_hip_programming.md §5.4 rule 24).  With --mark-file each arm's timed calls are a region of
+    their own (`region`/<arm>), so the kernel trace can be cut per arm."""
     st = torch.cuda.current_stream()
     for f in arms.values():
         f()
@@ -692,17 +833,19 @@ def _interleaved_ms(arms, reps=5, rounds=7):
     times = {k: [] for k in keys}
     for rd in range(rounds):
         for k in keys[rd % len(keys):] + keys[:rd % len(keys)]:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(reps):
-                arms[k]()
-            e1.record(st)
-            torch.cuda.synchronize()
-            times[k].append(e0.elapsed_time(e1) / reps)
+            with MARKS.region(f"{region}/{k}", calls=reps, round=rd) as mk:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(reps):
+                    arms[k]()
+                e1.record(st)
+                torch.cuda.synchronize()
+                times[k].append(e0.elapsed_time(e1) / reps)
+            mk["bench_ms_per_call_this_round"] = round(times[k][-1], 5)
     return {k: sorted(v)[len(v) // 2] for k, v in times.items()}
 
 
-def _graph_ms(calls, rounds=5):
+def _graph_ms(calls, rounds=5, region=None):
     """Median device ms per call of `calls` captured in ONE hipGraph and replayed (no host launch cost
     in the time; the calls rotate over distinct resident buffers, so they run cold)."""
     s = torch.cuda.Stream()
@@ -719,14 +862,16 @@ def _graph_ms(calls, rounds=5):
     torch.cuda.synchronize()
     st = torch.cuda.current_stream()
     out = []
-    for _ in range(rounds):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        g.replay()
-        e1.record(st)
-        torch.cuda.synchronize()
-        out.append(e0.elapsed_time(e1) / len(calls))
+    with MARKS.region(region or "graph", calls_per_replay=len(calls), replays=rounds) as mk:
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            g.replay()
+            e1.record(st)
+            torch.cuda.synchronize()
+            out.append(e0.elapsed_time(e1) / len(calls))
     del g
+    mk["bench_ms_per_call"] = round(sorted(out)[len(out) // 2], 6)
     return sorted(out)[len(out) // 2]
 
 
@@ -763,7 +908,7 @@ def fused_forward_section(rot_bytes=1 << 30):
                     "F.linear": lambda: F.linear(x, r.out)}
             if group != -2:
                 arms["fused_ref_order"] = lambda: K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, out=y)
-            t = _interleaved_ms(arms)
+            t = _interleaved_ms(arms, region=f"fused_forward/{name}/{gname}/M{M}")
             tf = 2.0 * M * N * Kd / (t["fused"] / 1e3) / 1e12
             tfn = 2.0 * M * N * Kd / (t["fused_nib"] / 1e3) / 1e12
             out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "mfma",
@@ -787,9 +932,10 @@ def fused_forward_section(rot_bytes=1 << 30):
             copies = [tiled] + [tiled.clone() for _ in range(int(rot_bytes // cb))]
             wbytes = cb + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0)
             t_f = _graph_ms([(lambda c=c: K.w4a16_gemm(x, c, r.scales, r.zeros, 4, group, N, tiled=True, out=y))
-                             for c in copies])
+                             for c in copies], region=f"fused_forward/{name}/{gname}/M1/fused")
             refs = [r.out] + [r.out.clone() for _ in range(int(rot_bytes // (N * Kd * 2)))]
-            t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs])
+            t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs],
+                            region=f"fused_forward/{name}/{gname}/M1/F.linear")
             gbs = wbytes / (t_f / 1e3) / 1e9
             out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "hbm",
                         "fused_ms": round(t_f, 5), "F_linear_ms": round(t_r, 5),
@@ -841,7 +987,7 @@ def formats_section(rows=11008, cols=4096, copies=16):
                                             for p, o in zip(grids, outs)], 2 * n + n // 2 + 2 * G))
     res = []
     for name, calls, alg in paths:
-        t = _graph_ms(calls) / 1e3
+        t = _graph_ms(calls, region=f"formats/{name}") / 1e3
         res.append({"path": name, "us": round(t * 1e6, 2), "alg_bytes": int(alg),
                     "achieved_GBps": round(alg / t / 1e9, 1), "frac_of_hbm_peak": round(alg / t / 1e9 / HBM_PEAK_GBS, 4)})
     del ws, outs, grids
@@ -860,19 +1006,22 @@ def model70b_section(args, ws_n, rank, steps=5, warmup=2):
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric, outs=weights)
     stream = torch.cuda.current_stream()
     a = argparse.Namespace(warmup=warmup, steps=steps, variant=0)
-    kernel_ms, ms = timed_steps(plan, a, ws_n, stream)
+    kernel_ms, ms = timed_steps(plan, a, ws_n, stream, region="llama2_70b")
     numel = plan.numel
     alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
     per_rank = gather_per_rank([kernel_ms, alg], ws_n)
     total = all_ranks_sum(numel, ws_n)
+    if ws_n == 1:
+        traffic, src = committed_traffic(args.traffic_70b_file, numel, args.bits, args.group, "in-place")
+    else:
+        traffic, src = None, "the committed 70B PMC record is the 1-GPU launch's; at N > 1 each rank runs its own bin"
     del plan, weights
     torch.cuda.empty_cache()
     return {"config": f"BASELINE configs[3]: Llama-2-70B {len(shapes)} Linear weights bin-packed over {ws_n} GPU(s), "
                       f"INT{args.bits} g={args.group} {'sym' if args.symmetric else 'asym'}, in place",
             "value": round(total * 2 / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
             "steps": steps, "warmup": warmup, "fp16_weights_total": total, "scaling": "strong",
-            "roofline": roofline_record(per_rank, "k_group<f16,128,asym,batched> in place", None,
-                                        "no PMC record for this workload")}
+            "roofline": roofline_record(per_rank, "k_group<f16,128,asym,batched> in place", traffic, src)}
 
 
 def build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, roofline, extra):
@@ -903,6 +1052,8 @@ def build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, 
 
 def main():
     args = parse()
+    if args.mark_file:
+        MARKS.enable()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     ws_n, rank, _, n_dev = init_dist(args)
@@ -921,17 +1072,17 @@ def main():
     scatter_ms = None
     if args.scatter and ws_n > 1:
         weak = False
-        weights, names, all_shapes, scatter_ms = scatter_weights(args.model, rank, ws_n)
+        weights, names, all_shapes, scatter_ms, _ = scatter_weights(args.model, rank, ws_n)
     else:
         weights, names, all_shapes = make_weights(args.model, rank, ws_n, weak=weak)
     numel = sum(w.numel() for w in weights)
     plan = kernels.BatchPlan(weights, args.bits, args.group, args.symmetric,
-                             outs=weights if args.inplace else None, want_codes=args.gather)
+                             outs=weights if args.inplace else None)
     stream = torch.cuda.current_stream()
     if args.variants:
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
     clock_ramp(plan, args.ramp_seconds)
-    ceiling = copy_ceiling(plan) if ws_n == 1 else None
+    ceiling = copy_ceiling(plan)  # every rank: its own GPU's ceiling (roofline.per_rank)
     kernel_ms, ms_per_step = timed_steps(plan, args, ws_n, stream)
 
     other = None
@@ -942,29 +1093,41 @@ def main():
     if not args.no_shapes and ws_n == 1 and not args.inplace:
         shapes_rec = per_shape(plan, names, ws_n, args)
 
-    gather_ms, gather_bytes = None, None
-    if args.gather and ws_n > 1:
-        gather_ms, gather_bytes = time_gather(plan, names, all_shapes, args, ws_n)
+    coll = {"gather_ms": None, "gather_bytes_to_rank0": None, "scatter_ms": scatter_ms}
+    if ws_n > 1 and not args.no_collectives:
+        coll.update(gather_section(plan, names, all_shapes, args, ws_n))
 
     total_numel = all_ranks_sum(numel, ws_n)
     groups = numel // args.group
     alg_bytes = numel * 2 + numel * 2 + groups * 2 * (1 if args.symmetric else 2)  # read w, write deq, s(,z)
-    if args.gather:
-        alg_bytes += numel // 2 if args.bits <= 4 else numel  # packed codes written too
-    per_rank = gather_per_rank([kernel_ms, alg_bytes], ws_n)
+    per_rank = gather_per_rank([kernel_ms, alg_bytes, ceiling["GBps"]], ws_n)
     if ws_n == 1:
-        traffic, traffic_src = committed_traffic(args.traffic_file, numel, args.bits, args.group)
+        if args.model == "llama2-70b":
+            traffic, traffic_src = committed_traffic(args.traffic_70b_file, numel, args.bits, args.group, "in-place")
+        else:
+            traffic, traffic_src = committed_traffic(args.traffic_file, numel, args.bits, args.group,
+                                                     "in-place" if args.inplace else "out-of-place")
     else:
         traffic, traffic_src = None, ("the committed PMC record is the 1-GPU workload's; at N > 1 every rank runs "
                                       "a different bin (profiles/traffic.json: +0.07 % over algorithmic at N = 1)")
     roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched>", traffic, traffic_src, ceiling, other)
 
+    if ws_n > 1 and not args.no_collectives and not args.scatter:
+        # bounded: the headline model's fp16 weights scattered from rank 0 (its own buffers are freed
+        # first: rank 0 briefly holds every rank's bin)
+        del plan
+        plan = weights = None
+        torch.cuda.empty_cache()
+        coll.update(scatter_section(args.model, rank, ws_n))
+    elif args.scatter and scatter_ms is not None:
+        coll["scatter_bytes_from_rank0"] = 2 * sum(shard_bin_elems(args.model, ws_n)[1:])
+
     weak_rec = None
     if ws_n > 1 and not weak and args.model == "llama2-7b" and not args.no_weak and not args.scatter:
-        del plan
-        weights = None
+        plan = weights = None
         torch.cuda.empty_cache()
         weak_rec, shapes_rec = weak_secondary(args, ws_n, rank)
+    if weights is None:  # the CPU baseline samples this rank's bin
         weights, _, _ = make_weights(args.model, rank, ws_n) if (rank == 0 and not args.no_cpu_baseline) else (None, 0, 0)
 
     cpu = None
@@ -995,13 +1158,13 @@ def main():
             "cpu_baseline": cpu,
             "ppl_delta": None,
             "ppl_plumbing": ppl,
-            "gather_ms": gather_ms, "gather_bytes_to_rank0": gather_bytes,
-            "scatter_ms": scatter_ms,
+            **coll,
             "fused_forward": fused,
             "formats": formats,
             "llama2_70b": m70,
         })
         print(json.dumps(rec), flush=True)
+    MARKS.write(args.mark_file, rank)
     if ws_n > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

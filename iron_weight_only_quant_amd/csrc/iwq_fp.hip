@@ -933,8 +933,7 @@ hipError_t launch_apx_double_lut_t(const FpArgs& a, hipStream_t st) {
   if (a.variant == 2) return launch_apx_double_lut_v<G, 2>(a, st);
   if (a.variant == 3) return launch_apx_double_lut_v<G, 0>(a, st);
 #endif
-  if (a.variant != 0) return hipErrorInvalidValue;  // A/B forms: IWQ_AB builds
-  return launch_apx_double_lut_v<G, 4>(a, st);
+  return launch_apx_double_lut_v<G, 4>(a, st);  // variants were checked at the C-ABI entry
 }
 
 hipError_t launch_apx_double_lut(int64_t g, const FpArgs& a, hipStream_t st) {
@@ -1187,6 +1186,10 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
                                uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
   if (group <= 0) return IWQ_ERR_GROUP_MODE;  // approximate needs w_group_size > 0 (ValueError)
   if (!out_deq || !out_scales) return IWQ_ERR_ARG;
+  // A/B forms (variants 1..3 of the double-approximate decode) exist only in IWQ_AB builds; any other
+  // variant is refused here, before a launch, with IWQ_ERR_ARG like iwq_quantize_minmax does
+  const int variant = (int)((flags >> 16) & 0xFFu);
+  if (variant != 0 && (!IWQ_AB || !double_approx || variant > 3)) return IWQ_ERR_ARG;
   if (double_approx && (dtype == IWQ_BF16 || dtype == IWQ_F32))  // iwq_fpdt.hip
     return iwq::run_fp_dt(2, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
                           nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, stream, hi_align_start,

@@ -13,10 +13,12 @@ Differences by design (documented in DESIGN.md):
   * quantization runs in the gfx950 kernels (no CPU path);
   * `keep_codes=True` additionally keeps the packed integer codes (`qweight`, include/iwq.h layout)
     for the fused dequant->GEMM forward.
-FP4/FP6/FP8 (quant_linear.py:724-883) run the gfx950 FP codec (fp16 weights), with the formats set
-by the same module-level `configure_fp_formats` (:84-110).  The research formats run on the GPU too:
-`approximate=True` (+ `double_approximate`) = quantize_weight_approximate (:470-632, fp16 weights)
-and weight_format "bfp" = the block-floating-point branch (:648-723, fp16/bf16/fp32 weights).
+FP4/FP6/FP8 (quant_linear.py:724-883) run the gfx950 FP codec on fp16, bf16 and fp32 weights (every
+op in the weight's dtype, fp16 scales / zeros like the reference's .half() buffers), with the formats
+set by the same module-level `configure_fp_formats` (:84-110).  The research formats run on the GPU
+too, on fp16 / bf16 / fp32 weights: `approximate=True` (+ `double_approximate`) =
+quantize_weight_approximate (:470-632) and weight_format "bfp" = the block-floating-point branch
+(:648-723).
 """
 import torch
 import torch.nn as nn
@@ -139,9 +141,10 @@ class QuantLinear(nn.Module):
             res = kernels.quantize_minmax(w, self.w_bit, self.w_group_size, bool(self.symmetric), self.quant_dim,
                                           out=w if w.stride(1) == 1 and w.stride(0) >= w.shape[1] else None,
                                           want_codes=self.keep_codes and self.w_bit <= 8)
-            if res.retry is not None:
-                # per-tensor one-pass kernel: an aborted in-launch hand-off (another kernel holding
-                # CUs) wrote nothing; re-run on the two-kernel form (the reference never fails here)
+            if self.w_group_size == -1:
+                # per tensor (any dtype / quant_dim): an aborted one-pass hand-off (another kernel
+                # holding CUs) wrote nothing; settle() re-runs it on the two-kernel form (the reference
+                # never fails here) and raises if the outputs are still invalid
                 res.settle()
             if res.out is not w:
                 w.copy_(res.out)

@@ -175,6 +175,11 @@ static void check_fp_validation(void) {
   CHECK(iwq_approx_workspace_bytes(64, 128, 4, 3, 128, 0, 1) >= 0);
   CHECK(iwq_quantize_fp_approx(w, 64, 128, 128, IWQ_F16, 4, 3, -2, 0, 12, 15, 1, 0, out, 128, s, NULL, 0, flag, 0, NULL) ==
         IWQ_ERR_GROUP_MODE);
+  /* product library: an A/B variant of the double-approximate decode is refused before any launch */
+  CHECK(iwq_quantize_fp_approx(w, 64, 128, 128, IWQ_F16, 4, 3, 128, 0, 12, 15, 1, 1, out, 128, s, NULL, 0, flag,
+                               2u << 16, NULL) == IWQ_ERR_ARG);
+  CHECK(iwq_quantize_fp_approx(w, 64, 128, 128, IWQ_F16, 4, 3, 128, 0, 12, 15, 1, 0, out, 128, s, NULL, 0, flag,
+                               1u << 16, NULL) == IWQ_ERR_ARG);
 }
 
 int main(void) {

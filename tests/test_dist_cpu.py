@@ -228,6 +228,16 @@ def test_bench_gpus2_spawns_ranks_and_rooted_gather_moves_each_byte_once():
     assert roof["kernel_ms"] == 1.25 and roof["kernel_ms_basis"] == "max over ranks"
     assert [p["rank"] for p in roof["per_rank"]] == [0, 1]
     assert roof["per_rank"][0]["kernel_ms"] == 1.0 and roof["frac"] > 0
+    # every rank's own copy ceiling and kernel / ceiling ratio; the top level is the lowest rank's
+    assert [p["ceiling_GBps"] for p in roof["per_rank"]] == [5000.0, 4900.0]
+    assert roof["ceiling"]["GBps"] == 4900.0
+    assert roof["kernel_over_ceiling"] == min(p["kernel_over_ceiling"] for p in roof["per_rank"])
+    # the north star's collectives are in the DEFAULT N = 2 record (timed apart from value): the rooted
+    # gather of the packed results and the scatter of the model's fp16 bins from rank 0
+    assert rec["gather_ms"] > 0 and rec["gather_bytes_to_rank0"] == per_rank[1] and rec["gather_GBps"] > 0
+    lay = [shard.bin_layout(shapes, b)[1] for b in shard.plan_shards(shapes, 2)]
+    assert rec["scatter_ms"] > 0 and rec["scatter_bytes_from_rank0"] == 2 * lay[1]
+    assert rec["scatter_verified"] is True
     cpu = rec["cpu_baseline"]
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port" and "OPT-125M" in cpu["sample"]
 

@@ -886,6 +886,39 @@ def test_per_tensor_onepass_timeout_retry(K):
     assert bits_equal(to_np(q.scales.view(-1)), exp.scales.reshape(-1))
 
 
+def test_per_tensor_onepass_timeout_retry_quant_dim1(K):
+    """The same abort at quant_dim 1 (the C side takes the one-pass kernel for every fp16 per-tensor
+    call: the group is the whole tensor, so the walk does not depend on quant_dim): the retry is set
+    up there too, out of place and in place, and QuantLinear(quant_dim=1) settles it."""
+    x = synth(57, (1536, 2048), "float16")
+    exp = O.quantlinear_int(x, 4, -1, False, 1, "float16")
+    r = K.quantize_minmax(to_dev(x, "float16"), 4, -1, False, 1, want_codes=True, flags=K.gemm_variant_flags(9))
+    assert r.retry is not None
+    assert int(r.nan_flag.item()) & 2
+    assert not r.has_nan() and r.retried
+    assert bits_equal(to_np(r.out), exp.dequant)
+    assert bits_equal(to_np(r.scales), exp.scales.reshape(-1))
+    assert bits_equal(to_np(r.zeros), exp.zeros.reshape(-1))
+    assert np.array_equal(r.codes.cpu().numpy().reshape(-1), O.pack_codes(exp.codes, 4).reshape(-1))
+    xi = to_dev(x, "float16")
+    r = K.quantize_minmax(xi, 4, -1, False, 1, out=xi, flags=K.gemm_variant_flags(9))
+    torch.cuda.synchronize()
+    assert bits_equal(to_np(xi), x), "aborted one-pass launch wrote into the weight"
+    assert not r.has_nan() and r.retried
+    assert bits_equal(to_np(xi), exp.dequant)
+    from iron_weight_only_quant_amd.quant_linear import QuantLinear
+    lin = torch.nn.Linear(2048, 1536, bias=False).half().cuda()
+    lin.weight.data.copy_(to_dev(x, "float16"))
+    orig = K.quantize_minmax
+    K.quantize_minmax = lambda *a, **kw: orig(*a, **{**kw, "flags": K.gemm_variant_flags(9)})
+    try:
+        q = QuantLinear.from_linear(lin, w_bit=4, w_group_size=-1, symmetric=False, quant_dim=1)
+    finally:
+        K.quantize_minmax = orig
+    assert bits_equal(to_np(q.weight.data), exp.dequant)
+    assert bits_equal(to_np(q.scales.view(-1)), exp.scales.reshape(-1))
+
+
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
 def test_quant_dim1_register_kernel(K, dtype):
     """quant_dim 1 with groups of 32/64/128/256 rows (the register-resident column kernel; cols not a

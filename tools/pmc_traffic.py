@@ -35,13 +35,14 @@ def main():
     ap.add_argument("--bits", type=int, default=4)
     ap.add_argument("--group", type=int, default=128)
     ap.add_argument("--kernel", default="k_group")
+    ap.add_argument("--placement", default="out-of-place", choices=["out-of-place", "in-place"])
     ap.add_argument("-o", "--out", default="profiles/traffic.json")
     a = ap.parse_args()
     fetch_kib, nf = counter(a.fetch_dir, "FETCH_SIZE", a.kernel)
     write_kib, nw = counter(a.write_dir, "WRITE_SIZE", a.kernel)
     read_bytes = fetch_kib * 1024 * 2
     write_bytes = write_kib * 1024
-    rec = {"workload_numel": a.numel, "bits": a.bits, "group": a.group, "kernel": a.kernel,
+    rec = {"workload_numel": a.numel, "bits": a.bits, "group": a.group, "kernel": a.kernel, "placement": a.placement,
            "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "dispatches": [nf, nw],
            "read_bytes_per_launch": read_bytes, "write_bytes_per_launch": write_bytes,
            "hbm_bytes_per_launch": read_bytes + write_bytes,
