@@ -572,6 +572,17 @@ def copy_ceiling(plan, steps=5, rounds=3):
     return {"GBps": max(forms.values()), "forms": forms}
 
 
+def launch_floor_us(reps=32):
+    """Per-call device time of the smallest kernel of this library (iwq_fill_synthetic on 16
+    elements: one wave, no memory traffic to speak of) in the same hipGraph replay form as the cold
+    single calls: the per-kernel floor of a dependent launch on this box (dispatch, end-of-kernel
+    release, next dispatch; profiles/r05_launch_floor.jsonl: 1.6 us).  Reported beside every
+    per-call figure so the kernel's own share can be read off (never subtracted from `value`)."""
+    from iron_weight_only_quant_amd import kernels as K
+    t = torch.empty(16, dtype=torch.float16, device="cuda")
+    return _graph_ms([(lambda: K.fill_synthetic(t, 1))] * reps, region="launch_floor") * 1e3
+
+
 def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
     """Single-tensor drop-in calls (kernels.quantize_minmax == pseudo_quantize_tensor's device path)
     per Llama weight shape, COLD: `reps` consecutive calls on distinct resident instances of the
@@ -579,6 +590,7 @@ def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
     replayed; device time per call = event time / reps (includes the inter-kernel boundary).
     value per shape = all ranks' fp16 input bytes / max-over-ranks time."""
     from iron_weight_only_quant_amd import kernels as K
+    floor = launch_floor_us()
     by_shape = {}
     for i, w in enumerate(plan.weights):
         by_shape.setdefault(tuple(w.shape), []).append(i)
@@ -617,10 +629,12 @@ def per_shape(plan, names, ws_n, args, reps=32, rounds=5):
         t = max_over_ranks(ts[len(ts) // 2], ws_n)
         n = shp[0] * shp[1]
         alg = n * 4 + (n // args.group) * 2 * (1 if args.symmetric else 2)
+        kt = t - floor * 1e-6
         out[f"{shp[0]}x{shp[1]}"] = {
             "us_per_call": round(t * 1e6, 2), "weights_GBps": round(ws_n * n * 2 / t / 1e9, 1),
             "achieved_GBps_per_gpu": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-            "calls": len(idx), "cold": True}
+            "calls": len(idx), "cold": True, "launch_floor_us": round(floor, 3),
+            "frac_beyond_launch_floor": round(alg / kt / 1e9 / HBM_PEAK_GBS, 4) if kt > 0 else None}
         del g
     return out
 
@@ -887,6 +901,7 @@ def fused_forward_section(rot_bytes=1 << 30):
     F = torch.nn.functional
     out = []
     gen = torch.Generator(device="cuda").manual_seed(1234)
+    floor = launch_floor_us()
     for name, N, Kd in FF_SHAPES:
         w = torch.empty(N, Kd, dtype=torch.float16, device="cuda")
         K.fill_synthetic(w, 7)
@@ -937,9 +952,12 @@ def fused_forward_section(rot_bytes=1 << 30):
             t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs],
                             region=f"fused_forward/{name}/{gname}/M1/F.linear")
             gbs = wbytes / (t_f / 1e3) / 1e9
+            kt = t_f - floor / 1e3
             out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "hbm",
                         "fused_ms": round(t_f, 5), "F_linear_ms": round(t_r, 5),
                         "packed_weight_GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+                        "launch_floor_us": round(floor, 3),
+                        "frac_beyond_launch_floor": round(wbytes / (kt / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if kt > 0 else None,
                         "fused_vs_F_linear": round(t_r / t_f, 3), "cold_copies": len(copies),
                         "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
             del x, y, tiled, copies, refs, r
