@@ -80,6 +80,10 @@ struct FpArgs {
 // sign-only code decodes to -0); the grid keeps the sign of t always (rint(-0) = -0).
 // ---------------------------------------------------------------------------------------------
 constexpr int LUT_BLOCK = 512;
+// k_fp_group_lut's workgroup.  Round 5 A/B (profiles/r05_ab_fp_lut_block.jsonl): 1024 threads held to
+// 64 VGPRs (two 48 KB tables per CU = 8 waves per SIMD instead of 6) spilled ~300 B per lane and ran
+// 15-35 % SLOWER on every pack path; the 512-thread form stays
+constexpr int LUT_QBLOCK = 512;
 constexpr int LUT_MAX = 32768;
 
 __host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
@@ -432,14 +436,14 @@ __device__ __forceinline__ FpParams bcast_fp_params(const FpParams& p, int k) {
 // Group parameters are computed once per iteration of 4 units (g >= 32: lane l computes unit l % 4
 // of its group) and DPP-broadcast, as in k_group; GS = grid-stride walk (large single tensors).
 template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0>
-__global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
+__global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
   __shared__ uint16_t tab_buf[120];
-  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_BLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
+  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_QBLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
   const Log2Tabs tabs = stage_log2_tables(tab_buf);  // its barrier also publishes the table
   lds_char* lut = (lds_char*)lut_dyn;
-  constexpr int WPBL = LUT_BLOCK / WAVE;
+  constexpr int WPBL = LUT_QBLOCK / WAVE;
   constexpr int UNROLL = 4;
   constexpr int LPG = G / 8;
   constexpr bool RED_SYM = SYM || CODEC != CODEC_FP;
@@ -457,8 +461,8 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
     u0 = wave * per;
     cend = min(u0 + per, a.total_units);
   }
-  const _Float16 bnd = __builtin_bit_cast(_Float16, (uint16_t)lut_bound_bits(CODEC, a.f));
-  const h2 bound2 = {bnd, bnd};
+  const uint16_t bnd2 = (uint16_t)(lut_bound_bits(CODEC, a.f) << 1);  // the clamp bound as a table offset
+  const u16x2 bound2x = {bnd2, bnd2};
   const _Float16 rb16 = (_Float16)__builtin_ldexpf(1.0f, a.f.bias - 15);
   const h2 rebias = {rb16, rb16};
   bool any_nan = false;
@@ -486,38 +490,71 @@ __global__ __launch_bounds__(LUT_BLOCK) void k_fp_group_lut(FpArgs a) {
       }
     }
   };
+  auto store_params = [&](int64_t e0, const FpParams& p) {
+    if ((lane % LPG) == 0) {
+      if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
+      if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);
+    }
+  };
   auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
     Vec8<DT_F16> o;
-    bool nan8 = false;
-    uint32_t c[8];
-    uint32_t cp[4];  // table path: the codes of elements 2j, 2j+1 in the 16-bit halves of cp[j]
     if (table) {  // finite group (grid: S > 0): table path, no NaN possible
+      // in three phases so that the unit's eight table reads are in flight together (one LDS wait per
+      // unit instead of one per pair, round 5): quotients + table indices, reads, then sign / dequant /
+      // codes.  Same bits as fp_pair_lut.
+      const h2 s16 = h2{(_Float16)p.s, (_Float16)p.s};
+      const h2 z16 = h2{(_Float16)p.z, (_Float16)p.z};
+      uint32_t tb[4], a2[4], r[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint32_t q;
-        o.u[j] = fp_pair_lut<CODEC, SYM>(vk.u[j], p, bound2, lut, CODES ? &q : nullptr);
-        if constexpr (CODES != 0) cp[j] = codes_of_values(q, a.f, rebias);
+        h2 d = as_h2(vk.u[j]);
+        if constexpr (!SYM) d = d - z16;                                   // RN16(w - z)
+        tb[j] = as_u32(__builtin_convertvector(pk_div_f16vals(__builtin_convertvector(d, f2), p.rs, p.s), h2));
+        // 2|t| clamped to 2*bound: positive fp16 bit patterns order like their values and t is finite
+        // (or +-inf) on a table group, so the clamp of t and the table byte offset are two packed ops
+        a2[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, tb[j]) << (u16x2)1,
+                                                                       bound2x));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const h2 rv = {*(lds_h*)(lut + (a2[j] & 0xFFFFu)), *(lds_h*)(lut + (a2[j] >> 16))};
+        r[j] = as_u32(rv);
+      }
+      uint32_t cp[4];  // the codes of elements 2j, 2j+1 in the 16-bit halves of cp[j]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t rb = r[j];
+        if constexpr (CODEC == CODEC_GRID) {
+          rb |= tb[j] & 0x80008000u;
+        } else {  // sign where |t| != 0: bit 15 of (tb + 0x7FFF) is clear exactly for negative nonzero t
+          const uint32_t sum = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, tb[j]) + (u16x2)0x7FFF);
+          rb |= tb[j] & ~sum & 0x80008000u;
+        }
+        h2 y = as_h2(rb) * s16;                                             // RN16(exact product)
+        if constexpr (!SYM) y = y + z16;                                    // RN16(exact sum)
+        o.u[j] = as_u32(y);
+        if constexpr (CODES != 0) cp[j] = codes_of_values(rb, a.f, rebias);
+      }
+      if (e0 < tnumel) {
+        if (tout) o.store(tout + e0 * F::BYTES);
+        // the pairs' halves straight into bytes / nibbles (two v_perm for bytes, the INT packing)
+        if constexpr (CODES != 0) store_codes8<CODES>(a.codes, e0, cp);
+        store_params(e0, p);
       }
     } else {
+      bool nan8 = false;
+      uint32_t c[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float y = fp_elem<CODEC, SYM, CODES != 0>(F::to_f(vk.get(i)), p, a.f, c[i], tabs);
         nan8 |= (y != y);
         o.set(i, F::from_f(y));
       }
-    }
-    if (e0 < tnumel) {
-      any_nan |= nan8;
-      if (tout) o.store(tout + e0 * F::BYTES);
-      if constexpr (CODES != 0) {
-        // table path: the pairs' halves straight into bytes / nibbles (two v_perm for bytes, the INT
-        // packing) instead of splitting them into eight words first (~14 VALU per unit)
-        if (table) store_codes8<CODES>(a.codes, e0, cp);
-        else store_fp_codes8<CODES>(a.codes, e0, c);
-      }
-      if ((lane % LPG) == 0) {
-        if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
-        if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);
+      if (e0 < tnumel) {
+        any_nan |= nan8;
+        if (tout) o.store(tout + e0 * F::BYTES);
+        if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
+        store_params(e0, p);
       }
     }
   };
@@ -852,15 +889,15 @@ hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
   auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true, false, CODES>;
   const size_t lds = (size_t)a.lut_n8 * 2;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
-  constexpr int WPBL = LUT_BLOCK / WAVE;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_QBLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
+  constexpr int WPBL = LUT_QBLOCK / WAVE;
   int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
   const int64_t cap = (int64_t)cu_count() * occ;
   const bool gs = a.total_units >= 2 * cap * WPBL * 4;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
-  else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
+  else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   return hipGetLastError();
 }
 
@@ -869,13 +906,13 @@ hipError_t launch_fp_lut_batched_t(const FpArgs& a, hipStream_t st) {
   auto kern = k_fp_group_lut<CODEC, G, SYM, false, true>;
   const size_t lds = (size_t)a.lut_n8 * 2;
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_BLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
-  constexpr int WPBL = LUT_BLOCK / WAVE;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_QBLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
+  constexpr int WPBL = LUT_QBLOCK / WAVE;
   int64_t blocks = (a.total_units + 4 * WPBL - 1) / (4 * WPBL);
   const int64_t cap = (int64_t)cu_count() * occ;
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_BLOCK), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   return hipGetLastError();
 }
 
