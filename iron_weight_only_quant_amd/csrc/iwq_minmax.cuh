@@ -880,13 +880,18 @@ constexpr uint32_t OP_SPIN_LIMIT = 1u << 22;
 constexpr int OP_NT = 2;  // buffer-instruction cache bits: non-temporal (streamed once)
 constexpr unsigned long long OP_GO = 1, OP_ABORT = 2;
 
-// Workgroup b owns the contiguous vectors [b * nvt * 512, (b + 1) * nvt * 512) (16-B vectors of 8
-// elements; nvt <= NV vectors per thread, chosen so the chunks spread over every CU); vector i of
-// thread t is b * nvt * 512 + i * 512 + t: every load / store instruction covers 8 KiB contiguous per
-// workgroup.  The loads go through a buffer descriptor over the workgroup's chunk (one 32-bit per-lane
-// offset for all vectors; the range check zero-fills loads beyond the chunk -- i >= nvt, or the last
-// chunk's tail -- without touching memory, and the key fold masks them).  A granule counts once its
-// tag equals 1 (granules[gridDim.x] is the consensus word; all zeroed by the per-launch memset).
+// Workgroup b owns the contiguous vectors [b * nvt * 512, (b + 1) * nvt * 512) (vectors of 8
+// elements: 16 B for fp16 / bf16, 32 B for fp32; nvt <= NV vectors per thread, chosen so the chunks
+// spread over every CU); vector i of thread t is b * nvt * 512 + i * 512 + t: every load / store
+// instruction covers 8 KiB contiguous per workgroup (fp32: two instructions over 16 KiB).  The loads
+// go through a buffer descriptor over the workgroup's chunk (one 32-bit per-lane offset for all
+// vectors; the range check zero-fills loads beyond the chunk -- i >= nvt, or the last chunk's tail --
+// without touching memory, and the key fold masks them).  A granule counts once its tag equals 1.
+// Keys: 16-bit dtypes publish (min, max) as packed int16 in ONE granule per workgroup; fp32 (round 5)
+// publishes two granules, {tag, min key} and {tag, max key} (granules[2b], granules[2b + 1]); the
+// consensus word follows the last granule.  All granules are zeroed by the per-launch memset.
+// Elementwise: fp16 takes the packed fast path, bf16 / fp32 (round 5) a Markstein-division fast path
+// on the register-held vectors; non-finite or extreme ranges re-read the input for the literal chain.
 template <int DT, bool SYM, int CODES, int NV>
 __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* out, uint8_t* codes, void* scales,
                                                            void* zeros, int64_t nvec, int nvt,
@@ -894,7 +899,10 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
                                                            uint32_t* nan_flag, uint32_t spin_limit) {
   constexpr uint32_t tag = 1;
   using F = Fmt<DT>;
-  static_assert(DT == DT_F16, "one-pass per-tensor: fp16 (keys packed in one dword, packed fast path)");
+  constexpr bool K32 = F::NB == 32;       // 32-bit order keys: two granules per workgroup
+  constexpr int KG = K32 ? 2 : 1;         // granules per workgroup
+  constexpr int VB = F::BYTES * 8;        // bytes per 8-element vector
+  constexpr int32_t KMIN = K32 ? (int32_t)0x80000000 : -0x8000, KMAX = K32 ? 0x7FFFFFFF : 0x7FFF;
   typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
   __shared__ int32_t smn[OP_THR / 64], smx[OP_THR / 64];
   __shared__ int32_t fin[3];
@@ -903,26 +911,48 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   const int64_t chunk = (int64_t)nvt * OP_THR;                    // vectors per workgroup
   const int64_t v0 = (int64_t)blockIdx.x * chunk;                 // this workgroup's first vector
   const int64_t nv_here = nvec - v0 < chunk ? nvec - v0 : chunk;  // > 0: one workgroup per non-empty chunk
-  const int nbytes = (int)(nv_here * 16);
-  const char* wb = static_cast<const char*>(rflp(static_cast<const void*>(w + v0 * 16)));
+  const int nbytes = (int)(nv_here * VB);
+  const char* wb = static_cast<const char*>(rflp(static_cast<const void*>(w + v0 * VB)));
   const auto rin = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wb), 0, nbytes, 0x00020000);
+  // fp32: the two 16-B halves of a thread's vector i are chunks 2i and 2i + 1 of 512 x 16 B each
+  // (chunk c of thread t at byte (c * 512 + t) * 16 of the workgroup's range), so every load / store
+  // instruction still covers 8 KiB contiguous; elementwise work does not care which 8 elements share
+  // a register vector.  16-bit dtypes: one chunk per vector.
   const int voff = threadIdx.x * 16;
+  const int64_t nch = nv_here * (VB / 16);  // valid 16-B chunks of this workgroup
   Vec8<DT> v[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const u32x4v x = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, i * OP_THR * 16, OP_NT);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[i].u[j] = x[j];
+    for (int h = 0; h < VB / 16; ++h) {
+      const u32x4v x = __builtin_amdgcn_raw_buffer_load_b128(rin, voff, (i * (VB / 16) + h) * OP_THR * 16, OP_NT);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i].u[4 * h + j] = x[j];
+    }
   }
-  int32_t mn = 0x7FFF, mx = -0x8000;  // int16 identities (every 16-bit order key lies in between)
+  int32_t mn = KMAX, mx = KMIN;  // identities (every order key lies in between)
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     if (i < nvt) {  // uniform (a branch, not a break: the loop must stay fully unrolled)
-      int32_t a, b;
-      minmax8<DT, SYM>(v[i], a, b);
-      if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
-        mn = min(mn, a);
-        mx = max(mx, b);
+      if constexpr (K32) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if ((int64_t)(2 * i + h) * OP_THR + threadIdx.x < nch) {
+#pragma unroll
+            for (int e = 4 * h; e < 4 * h + 4; ++e) {
+              const int32_t kk = SYM ? mag_key<DT>(v[i].get(e)) : key_of<DT>(v[i].get(e));
+              mn = min(mn, SYM ? 0 : kk);
+              mx = max(mx, kk);
+            }
+          }
+        }
+      } else {
+        int32_t a, b;
+        minmax8<DT, SYM>(v[i], a, b);
+        if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+          mn = min(mn, a);
+          mx = max(mx, b);
+        }
       }
     }
   }
@@ -932,19 +962,67 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int i = 1; i < OP_THR / 64; ++i) { mn = min(mn, smn[i]); mx = max(mx, smx[i]); }
-    const uint32_t keys = (uint32_t)(uint16_t)(int16_t)mn | ((uint32_t)(uint16_t)(int16_t)mx << 16);
-    __hip_atomic_store(granules + blockIdx.x, ((unsigned long long)tag << 32) | keys, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (K32) {
+      __hip_atomic_store(granules + 2 * blockIdx.x, ((unsigned long long)tag << 32) | (uint32_t)mn,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(granules + 2 * blockIdx.x + 1, ((unsigned long long)tag << 32) | (uint32_t)mx,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint32_t keys = (uint32_t)(uint16_t)(int16_t)mn | ((uint32_t)(uint16_t)(int16_t)mx << 16);
+      __hip_atomic_store(granules + blockIdx.x, ((unsigned long long)tag << 32) | keys, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (wv == 0) {
-    // sweep every workgroup's granule until all carry the tag (relaxed agent-scope loads bypass L1)
-    const int ng = (int)gridDim.x;
+    // sweep every workgroup's granule(s) until all carry the tag (relaxed agent-scope loads bypass L1)
+    const int ng = (int)gridDim.x * KG;
     int32_t gmn, gmx;
+    auto fold = [&](unsigned long long x, int g) {
+      if constexpr (K32) {
+        if (g & 1) gmx = max(gmx, (int32_t)(uint32_t)x);
+        else gmn = min(gmn, (int32_t)(uint32_t)x);
+      } else {
+        gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
+        gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
+      }
+    };
+    // round 5: every granule a lane still waits for is loaded in the same spin iteration (up to 8 x 64
+    // granules: one relaxed agent-scope round trip per iteration instead of one per 64 granules in
+    // sequence -- four on a 256-CU chip, eight with fp32's two granules per workgroup)
+    constexpr int SWK = 8;
     auto sweep = [&](uint32_t limit) -> bool {  // true: gave up before seeing every granule
-      gmn = 0x7FFF;
-      gmx = -0x8000;
+      gmn = KMAX;
+      gmx = KMIN;
       bool gave_up = false;
-      for (int g0 = 0; g0 < ng; g0 += 64) {
+      if (ng <= 64 * SWK) {
+        const int nk = (ng + 63) / 64;
+        uint32_t have = 0;  // bit k: granule 64 k + lane seen with the tag (or beyond ng)
+#pragma unroll
+        for (int k = 0; k < SWK; ++k)
+          if (k >= nk || 64 * k + lane >= ng) have |= 1u << k;
+        uint32_t spins = 0;
+        while (true) {
+          unsigned long long xv[SWK];
+#pragma unroll
+          for (int k = 0; k < SWK; ++k)
+            if (!((have >> k) & 1u)) xv[k] = __hip_atomic_load(granules + 64 * k + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int k = 0; k < SWK; ++k) {
+            if (!((have >> k) & 1u) && (uint32_t)(xv[k] >> 32) == tag) {
+              have |= 1u << k;
+              fold(xv[k], 64 * k + lane);
+            }
+          }
+          if (__all(have == (1u << SWK) - 1u)) break;
+          if (++spins > limit) {
+            gave_up = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        return gave_up;
+      }
+      for (int g0 = 0; g0 < ng; g0 += 64) {  // (more workgroups than 8 x 64 granules: chunk by chunk)
         const int g = g0 + lane;
         uint32_t spins = 0;
         unsigned long long x = 0;
@@ -958,10 +1036,7 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
           }
           __builtin_amdgcn_s_sleep(1);
         }
-        if (g < ng && (uint32_t)(x >> 32) == tag) {
-          gmn = min(gmn, (int32_t)(int16_t)(uint16_t)(x & 0xFFFFu));
-          gmx = max(gmx, (int32_t)(int16_t)(uint16_t)((x >> 16) & 0xFFFFu));
-        }
+        if (g < ng && (uint32_t)(x >> 32) == tag) fold(x, g);
       }
       return gave_up;
     };
@@ -1005,39 +1080,101 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   // SGPR soffset needs before a VALU overwrites its data registers (the first dword of the stored
   // vector was clobbered -- caught by the bit-exact tests), so the output leaves through 64-bit
   // addresses with the range check done by hand
-  char* ob = out ? out + v0 * 16 + threadIdx.x * 16 : nullptr;
+  char* ob = out ? out + v0 * VB + threadIdx.x * 16 : nullptr;
   bool any_nan = false;
-  if (p.fast) {  // the packed fp16 path on the register-held vectors (uniform: one group)
-    const FastPk k = fast_pk<SYM>(p, n_bits);
+  if constexpr (DT == DT_F16) {
+    if (p.fast) {  // the packed fp16 path on the register-held vectors (uniform: one group)
+      const FastPk k = fast_pk<SYM>(p, n_bits);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      if (i < nvt) {  // uniform
-        u32x4v o;
-        uint32_t c[4];
+      for (int i = 0; i < NV; ++i) {
+        if (i < nvt) {  // uniform
+          u32x4v o;
+          uint32_t c[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t cp;
-          o[j] = quant2_fast<SYM>(v[i].u[j], p, k, cp);
-          c[j] = codes2_fast(cp, k);
+          for (int j = 0; j < 4; ++j) {
+            uint32_t cp;
+            o[j] = quant2_fast<SYM>(v[i].u[j], p, k, cp);
+            c[j] = codes2_fast(cp, k);
+          }
+          if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+            if (ob) __builtin_nontemporal_store(o, gp<u32x4v>(static_cast<void*>(ob + (int64_t)i * OP_THR * 16)));
+            if constexpr (CODES != 0) store_codes8<CODES>(codes, (v0 + (int64_t)i * OP_THR + threadIdx.x) * 8, c);
+          }
         }
-        if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
-          if (ob) __builtin_nontemporal_store(o, gp<u32x4v>(static_cast<void*>(ob + (int64_t)i * OP_THR * 16)));
-          if constexpr (CODES != 0) store_codes8<CODES>(codes, (v0 + (int64_t)i * OP_THR + threadIdx.x) * 8, c);
+      }
+    } else {
+      // non-finite range / zero scale (never on real weights): the exact chain, each thread re-reading
+      // its own vectors (nothing else writes them, so this is right in place too)
+      for (int i = 0; i < nvt; ++i) {
+        const int64_t u = v0 + (int64_t)i * OP_THR + threadIdx.x;
+        if (u < v0 + nv_here) {
+          Vec8<DT> x, o;
+          x.template load<true>(w + u * 8 * F::BYTES);
+          uint32_t c[4];
+          any_nan |= quant8<DT, SYM>(x, p, n_bits, o, c);
+          if (out) o.template store<true>(out + u * 8 * F::BYTES);
+          if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
         }
       }
     }
   } else {
-    // non-finite range / zero scale (never on real weights): the exact chain, each thread re-reading
-    // its own vectors (nothing else writes them, so this is right in place too)
-    for (int i = 0; i < nvt; ++i) {
-      const int64_t u = v0 + (int64_t)i * OP_THR + threadIdx.x;
-      if (u < v0 + nv_here) {
-        Vec8<DT> x, o;
-        x.template load<true>(w + u * 8 * F::BYTES);
-        uint32_t c[4];
-        any_nan |= quant8<DT, SYM>(x, p, n_bits, o, c);
-        if (out) o.template store<true>(out + u * 8 * F::BYTES);
-        if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+    // bf16 / fp32 (round 5).  Fast path (one group, so a uniform branch): the quotient as Markstein's
+    // corrected product, q = RN32(w / s) from rs = RN32(1 / s) (exact IEEE reciprocal, once); then one
+    // rounding to the storage dtype, rint, the bound clamp and RN((c - z) * s) -- bit-identical to the
+    // literal chain quant_exact (iwq_common.cuh) whenever tensor_fast_dt holds: s normal and
+    // >= 2^-40 (the reference clamps the range at 1e-5 first, so s >= 1.5e-10 for <= 16 bits), and
+    // max |w| * rs < 2^100 (no overflow in q0 or the residual).  A quotient that matters (|w / s| >=
+    // 0.5) then has |w| >= s / 2, a normal number whose residual w - q0 s cannot underflow, so the
+    // correction is exact (the fp16 selftest checks the same construction exhaustively); smaller
+    // quotients round to 0 whatever their last bits.  r + z needs no rounding: exact below 2^8 (bf16)
+    // / 2^24 (fp32), and beyond that the clamp to [lo, hi] gives the same bound; (c - z) * s is the
+    // reference's product: fp32-rounded, then (bf16) rounded to the storage dtype.
+    const float mxa = fmaxf(fabsf(F::to_f(bits_of_key<DT>(fin[0]))), fabsf(F::to_f(bits_of_key<DT>(fin[1]))));
+    // (bf16 represents every integer only up to 2^8: above 8 bits the reference's R(r + z) can move
+    // an in-range integer, so wider bf16 codes take the literal chain)
+    const bool fastdt = p.s >= 0x1p-40f && p.s <= 0x1p100f && mxa * p.rs < 0x1p100f &&
+                        n_bits <= (F::NB == 16 ? 8 : 16);
+    if (fastdt) {
+      const float rs = p.rs, sc = p.s, zz = p.z, lo = p.lo, hi = p.hi;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        if (i < nvt) {  // uniform
+          Vec8<DT> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = F::to_f(v[i].get(e));
+            const float q0 = x * rs;
+            const float q = opaque(__builtin_fmaf(__builtin_fmaf(-q0, sc, x), rs, q0));  // RN32(x / s)
+            const float t = F::R(q);
+            const float c = __builtin_amdgcn_fmed3f(__builtin_rintf(t) + zz, lo, hi);
+            o.set(e, F::from_f(SYM ? c * sc : (c - zz) * sc));
+          }
+          if (ob) {
+            if constexpr (K32) {
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                if ((int64_t)(2 * i + h) * OP_THR + threadIdx.x < nch)
+                  __builtin_nontemporal_store((u32x4v){o.u[4 * h], o.u[4 * h + 1], o.u[4 * h + 2], o.u[4 * h + 3]},
+                                              gp<u32x4v>(static_cast<void*>(ob + (int64_t)(2 * i + h) * OP_THR * 16)));
+            } else if ((int64_t)i * OP_THR + threadIdx.x < nv_here) {
+              o.template store<true>(ob + (int64_t)i * OP_THR * VB);
+            }
+          }
+        }
+      }
+    } else {
+      // non-finite / extreme ranges: the literal op chain, each thread re-reading its own vectors
+      // (nothing else writes them, so this is right in place too)
+      for (int i = 0; i < nvt; ++i) {
+        const int64_t u = v0 + (int64_t)i * OP_THR + threadIdx.x;
+        if (u < v0 + nv_here) {
+          Vec8<DT> x, o;
+          x.template load<true>(w + u * 8 * F::BYTES);
+          uint32_t c[4];
+          any_nan |= quant8<DT, SYM>(x, p, n_bits, o, c);
+          if (out) o.template store<true>(out + u * 8 * F::BYTES);
+          if constexpr (CODES != 0) store_codes8<CODES>(codes, u * 8, c);
+        }
       }
     }
   }

@@ -428,8 +428,9 @@ hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void*
   const int64_t chunk = (int64_t)nvt * OP_THR;
   const int64_t nblk = (nvec + chunk - 1) / chunk;
   if (nvt < 1 || nvt > NV || nblk < 1 || nblk > cus) return hipErrorInvalidValue;
-  // the granules and the consensus word after them: zeroed before the launch
-  const size_t gbytes = ((size_t)(nblk + 1) * 8 + 15) / 16 * 16;
+  // the granules (two per workgroup for fp32's 32-bit keys) and the consensus word after them: zeroed
+  // before the launch
+  const size_t gbytes = ((size_t)(nblk * (DT == DT_F32 ? 2 : 1) + 1) * 8 + 15) / 16 * 16;
   hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_tensor_onepass<DT, SYM, CODES, NV>), dim3((unsigned)nblk), dim3(OP_THR), 0, st,
@@ -437,23 +438,33 @@ hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void*
                      nvec, nvt, reinterpret_cast<unsigned long long*>(ws), n_bits, nan_flag, spin_limit);
   return hipGetLastError();
 }
+// fp16: every codes width; bf16 / fp32 (round 5): the fake-quant output only (CODES 0) -- with packed
+// codes they take the pair.  Register budget: NV vectors of 8 elements per thread, up to 48 x 16 B
+// (16-bit dtypes) or 24 x 32 B (fp32) = 192 VGPRs of data: ~100 MB of weights on 256 CUs either way.
 template <int DT, bool SYM, int CODES>
 bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err,
                            bool fixed_nv, uint32_t spin_limit) {
-  if constexpr (DT != DT_F16) {
+  if constexpr (DT != DT_F16 && CODES != 0) {
     return false;
   } else {
     if (nan_flag == nullptr) return false;  // an aborted hand-off must be reportable (bit 1)
     const int cus = device_cu_count();
-    if ((int64_t)cus + 1 > (int64_t)TENSOR_PARTS_MAX) return false;  // granules beyond the workspace
+    // granules (two per workgroup for fp32) + the consensus word must fit the workspace
+    if ((int64_t)cus * (DT == DT_F32 ? 2 : 1) + 1 > (int64_t)TENSOR_PARTS_MAX) return false;
     const int64_t nvec = numel / 8;
     const int64_t per = (nvec + (int64_t)cus * OP_THR - 1) / ((int64_t)cus * OP_THR);
     // nvt = per spreads the chunks over every CU; fixed_nv (A/B) uses the template's NV instead
-    if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-    else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-    else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-    else return false;
+    if constexpr (DT == DT_F32) {
+      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      else if (per <= 24) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 24>(w, out, codes, scales, zeros, nvec, fixed_nv ? 24 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      else return false;
+    } else {
+      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      else return false;
+    }
     return true;
   }
 }

@@ -161,9 +161,10 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
         wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         st = call(ws, wsb)
-        # where the C side can take the one-pass kernel (iwq_minmax.hip: per tensor, fp16, any quant_dim --
-        # a per-tensor group is the whole tensor, so quant_dim does not change the walk)
-        if group == -1 and w.dtype == torch.float16:
+        # where the C side can take the one-pass kernel (iwq_minmax.hip: per tensor, any quant_dim -- a
+        # per-tensor group is the whole tensor, so quant_dim does not change the walk; fp16, and bf16 /
+        # fp32 without packed codes)
+        if group == -1:
             def retry():  # the one-pass hand-off aborted (QuantResult.settle): same call on the pair
                 flag2 = torch.zeros(1, dtype=torch.int32, device=dev)
                 with L.on_device(dev):

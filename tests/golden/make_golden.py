@@ -12,6 +12,7 @@ Produces (committed, data only):
   tests/golden/int_large_70b.json  the same at the four Llama-2-70B Linear shapes (configs[3])
                                    (`--only 70b` regenerates just this file)
   tests/golden/int_large_pt.json   per-tensor (-1) at the 7B shapes (`--only pt`)
+  tests/golden/int_large_pt_dt.json  per-tensor (-1) on bf16 (7B shapes) and fp32 (4096^2) (`--only pt_dt`)
   tests/golden/int_batched.json    quantize_model's batched group modes on a 4-tensor set, fp16 and
                                    bf16, SHA-256 of every layer's outputs (`--only batched`)
 
@@ -246,6 +247,30 @@ def large_pt_cases():
     return res
 
 
+def large_pt_dt_cases():
+    """Per-tensor (-1) on bf16 and fp32 weights (round 5: the one-pass kernel also holds bf16 / fp32
+    weights in registers, keys in two dwords for fp32): bf16 at the three Llama-2-7B shapes, fp32 at
+    4096 x 4096 (the larger fp32 shapes exceed the register capacity and take the two-kernel pair)."""
+    res = {"generator": "oracle/synth.py (seed, shape, dtype)", "cases": []}
+    for dtype, names in (("bfloat16", ("q_proj", "gate_proj", "down_proj")), ("float32", ("q_proj",))):
+        for name, shp, seed in LARGE:
+            if name not in names:
+                continue
+            x = synth(seed, shp, dtype)
+            base = {"dtype": dtype, "name": name, "shape": list(shp), "seed": seed}
+            res["cases"].append({**base, "kind": "input", "sha_input": sha(x)})
+            for bits, zp in ((4, True), (8, False)):
+                out = ref_qf(x, dtype, n_bits=bits, zero_point=zp, q_group_size=-1, per_tensor=True)
+                res["cases"].append({**base, "kind": "qf_pt", "n_bits": bits, "zero_point": zp, "sha_deq": sha(out)})
+            for bits, sym in ((4, False), (4, True)):
+                deq, s, z, _ = ref_ql(x, dtype, w_bit=bits, w_group_size=-1, symmetric=sym)
+                res["cases"].append({**base, "kind": "ql", "w_bit": bits, "symmetric": sym, "w_group_size": -1,
+                                     "sha_deq": sha(deq), "sha_scales": sha(s),
+                                     "sha_zeros": None if z is None else sha(z)})
+            print("large_pt_dt", dtype, name, flush=True)
+    return res
+
+
 # quantize_model's batched launches in every non-headline group mode (per-channel, per-tensor,
 # quant_dim 1, long and non-power-of-two groups) on multi-tensor sets, fp16 AND bf16 (round 4:
 # the batched bf16 modes were compared with the per-layer path only)
@@ -288,6 +313,11 @@ if __name__ == "__main__":
         with open(os.path.join(HERE, "int_batched.json"), "w") as f:
             json.dump(batched_cases(), f, indent=1)
         print("batched done", flush=True)
+        sys.exit(0)
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pt_dt":
+        with open(os.path.join(HERE, "int_large_pt_dt.json"), "w") as f:
+            json.dump(large_pt_dt_cases(), f, indent=1)
+        print("large_pt_dt done", flush=True)
         sys.exit(0)
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "pt":
         with open(os.path.join(HERE, "int_large_pt.json"), "w") as f:

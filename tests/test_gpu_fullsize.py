@@ -33,7 +33,10 @@ def K():
 
 
 def _np(t):
-    return t.detach().contiguous().cpu().numpy()
+    t = t.detach().contiguous().cpu()
+    if t.dtype == torch.bfloat16:  # the bit patterns, as the golden generator hashes them
+        return t.view(torch.int16).numpy().view(np.uint16)
+    return t.numpy()
 
 
 def _cases(fname):
@@ -234,6 +237,79 @@ def test_per_tensor_one_pass_full_size(K, name):
             ri = K.quantize_minmax(y, c["w_bit"], -1, c["symmetric"], 0, out=y)
             assert torch.equal(y.view(torch.int16), r.out.view(torch.int16))
             assert int(ri.nan_flag.item()) == 0
+
+
+@pytest.mark.parametrize("case", [("bfloat16", "q_proj"), ("bfloat16", "gate_proj"), ("bfloat16", "down_proj"),
+                                  ("float32", "q_proj")])
+def test_per_tensor_one_pass_dtypes_full_size(K, case):
+    """Round 5: per tensor on bf16 / fp32 weights takes the one-pass kernel too (keys in two dwords for
+    fp32; the literal op chain on the register-held vectors): equal to the reference's SHA-256s
+    (tests/golden/int_large_pt_dt.json: pseudo_quantize_tensor(per_tensor=True) and QuantLinear
+    w_group_size=-1 on bf16 / fp32 weights), to the two-kernel pair (variant 6), and in place."""
+    dtype, name = case
+    td = getattr(torch, dtype)
+    cases = [c for c in _cases("int_large_pt_dt.json") if c["name"] == name and c["dtype"] == dtype]
+    inp = cases[0]
+    x = torch.empty(tuple(inp["shape"]), dtype=td, device=DEV)
+    K.fill_synthetic(x, inp["seed"])
+    bits_of = (lambda t: t.view(torch.int16)) if td != torch.float32 else (lambda t: t.view(torch.int32))
+    assert sha(_np(x)) == inp["sha_input"]
+    for c in cases[1:]:
+        if c["kind"] == "qf_pt":
+            r = K.quantize_minmax(x, c["n_bits"], -1, not c["zero_point"], 0)
+            assert int(r.nan_flag.item()) == 0
+            assert sha(_np(r.out)) == c["sha_deq"], c
+        else:
+            r = K.quantize_minmax(x, c["w_bit"], -1, c["symmetric"], 0)
+            assert int(r.nan_flag.item()) == 0
+            assert sha(_np(r.out)) == c["sha_deq"], c
+            assert sha(_np(r.scales).reshape(-1, 1)) == c["sha_scales"], c
+            if c["sha_zeros"] is not None:
+                assert sha(_np(r.zeros).reshape(-1, 1)) == c["sha_zeros"], c
+            r6 = K.quantize_minmax(x, c["w_bit"], -1, c["symmetric"], 0, flags=K.gemm_variant_flags(6))
+            assert torch.equal(bits_of(r6.out), bits_of(r.out))
+            y = x.clone()
+            ri = K.quantize_minmax(y, c["w_bit"], -1, c["symmetric"], 0, out=y)
+            assert torch.equal(bits_of(y), bits_of(r.out))
+            assert int(ri.nan_flag.item()) == 0
+            # the one-pass hand-off aborted on purpose (test-only variant 9): the retry on the pair
+            ra = K.quantize_minmax(x, c["w_bit"], -1, c["symmetric"], 0, flags=K.gemm_variant_flags(9))
+            assert int(ra.nan_flag.item()) & 2
+            assert not ra.has_nan() and ra.retried
+            assert torch.equal(bits_of(ra.out), bits_of(r.out))
+
+
+@pytest.mark.parametrize("shape", [(1, 8), (3, 40), (48, 256), (1000, 1000), (2048, 3000)])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_per_tensor_one_pass_ragged_dtypes(K, shape, dtype):
+    """Small / ragged per-tensor sizes on bf16 / fp32 weights (one workgroup, partial chunks, the
+    buffer range check at a 32-B vector for fp32): equal to the oracle and the pair, sym and asym."""
+    from oracle.synth import synth as _synth
+    x_np = _synth(91 + shape[0], shape, dtype)
+    x = torch.empty(shape, dtype=getattr(torch, dtype), device=DEV)
+    K.fill_synthetic(x, 91 + shape[0])
+    # 4 / 8 bits: the Markstein fast path; 12 bits: bf16 leaves it (integers above 2^8), fp32 keeps it
+    for bits, sym in ((4, False), (4, True), (8, False), (8, True), (12, False)):
+        ref = O.quantlinear_int(x_np, w_bit=bits, w_group_size=-1, symmetric=sym, dtype=dtype)
+        r = K.quantize_minmax(x, bits, -1, sym, 0)
+        got = _np(r.out)
+        assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(ref.dequant).view(np.uint8)), (shape, bits, sym)
+        r6 = K.quantize_minmax(x, bits, -1, sym, 0, flags=K.gemm_variant_flags(6))
+        assert np.array_equal(_np(r6.out).view(np.uint8), got.view(np.uint8))
+        assert int(r.nan_flag.item()) == 0
+    # a constant huge tensor (range clamped to 1e-5: max|w| / s ~ 1e36 > 2^100) takes the literal
+    # chain: same bits as the oracle
+    big = np.full(shape, 1e30, dtype=np.float32)
+    big_np = big if dtype == "float32" else O.f32_to_bf16_bits(big)
+    ref = O.quantlinear_int(big_np, w_bit=4, w_group_size=-1, symmetric=False, dtype=dtype)
+    xb = torch.from_numpy(np.ascontiguousarray(big_np).view(np.int32 if dtype == "float32" else np.int16))
+    xb = xb.to(DEV).view(getattr(torch, dtype))
+    rb = K.quantize_minmax(xb, 4, -1, False, 0)
+    assert np.array_equal(_np(rb.out).view(np.uint8), np.ascontiguousarray(ref.dequant).view(np.uint8))
+    # non-finite values take the literal chain (the fast path's preconditions fail): NaN poisons all
+    y = x.clone()
+    y.view(-1)[len(y.view(-1)) // 2] = float("nan")
+    assert K.quantize_minmax(y, 4, -1, False, 0).has_nan()
 
 
 @pytest.mark.parametrize("shape", [(1, 8), (3, 40), (48, 256), (1000, 1000), (2048, 3000)])

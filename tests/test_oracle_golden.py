@@ -134,6 +134,28 @@ def test_large_llama_shapes_sha(case_idx):
             assert sha(r.zeros) == c["sha_zeros"], c
 
 
+def test_large_per_tensor_bf16_sha():
+    """Per-tensor (-1) on a full 4096 x 4096 bf16 weight through the oracle vs the reference's SHA-256s
+    (tests/golden/int_large_pt_dt.json, round 5: the fixtures the GPU one-pass bf16 / fp32 kernel is
+    checked against)."""
+    spec = json.load(open(os.path.join(GOLD, "int_large_pt_dt.json")))
+    mine = [c for c in spec["cases"] if c["name"] == "q_proj" and c["dtype"] == "bfloat16"]
+    inp = mine[0]
+    x = synth(inp["seed"], tuple(inp["shape"]), "bfloat16")
+    assert sha(x) == inp["sha_input"]
+    for c in mine[1:]:
+        if c["kind"] == "qf_pt":
+            r = O.pseudo_quantize_tensor(x, n_bits=c["n_bits"], zero_point=c["zero_point"], q_group_size=-1,
+                                         per_tensor=True, dtype="bfloat16")
+            assert sha(r.dequant) == c["sha_deq"], c
+        else:
+            r = O.quantlinear_int(x, w_bit=c["w_bit"], w_group_size=-1, symmetric=c["symmetric"], dtype="bfloat16")
+            assert sha(r.dequant) == c["sha_deq"], c
+            assert sha(r.scales) == c["sha_scales"], c
+            if c["sha_zeros"] is not None:
+                assert sha(r.zeros) == c["sha_zeros"], c
+
+
 def test_torch_restatement_matches_golden():
     """bench.py's CPU baseline (oracle/torch_ref.py) is pinned to the reference's outputs too."""
     import torch
