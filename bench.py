@@ -832,6 +832,8 @@ def roofline_record(per_rank, kernel_name, traffic, traffic_src, ceiling=None, o
 # ---------------------------------------------------------------------------------------------
 MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA (MI355X_MICROARCH.md chip table; never the sparse figure)
 FF_SHAPES = (("q_proj", 4096, 4096), ("gate_proj", 11008, 4096), ("down_proj", 4096, 11008))
+# fused_proj.fuse_projections' row concatenations of one layer's siblings: q/k/v and gate/up
+DECODE_FUSED_SHAPES = (("qkv_fused", 3 * 4096, 4096), ("gate_up_fused", 2 * 11008, 4096))
 
 
 def _interleaved_ms(arms, reps=5, rounds=7, region=None):
@@ -902,6 +904,33 @@ def fused_forward_section(rot_bytes=1 << 30):
     out = []
     gen = torch.Generator(device="cuda").manual_seed(1234)
     floor = launch_floor_us()
+
+    def decode_row(name, N, Kd, r, group, gname, M=1):
+        """M = 1, cold (each call reads a different resident copy, >= rot_bytes per replay, hipGraph),
+        codes in the decode tile layout (what QuantLinear "auto" keeps) vs F.linear on rotated fp16."""
+        x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
+        y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+        tiled = K.tile_codes(r.codes, N, Kd)
+        cb = r.codes.numel()
+        copies = [tiled] + [tiled.clone() for _ in range(int(rot_bytes // cb))]
+        wbytes = cb + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0)
+        t_f = _graph_ms([(lambda c=c: K.w4a16_gemm(x, c, r.scales, r.zeros, 4, group, N, tiled=True, out=y))
+                         for c in copies], region=f"fused_forward/{name}/{gname}/M1/fused")
+        refs = [r.out] + [r.out.clone() for _ in range(int(rot_bytes // (N * Kd * 2)))]
+        t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs],
+                        region=f"fused_forward/{name}/{gname}/M1/F.linear")
+        gbs = wbytes / (t_f / 1e3) / 1e9
+        kt = t_f - floor / 1e3
+        row = {"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "hbm",
+               "fused_ms": round(t_f, 5), "F_linear_ms": round(t_r, 5),
+               "packed_weight_GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+               "launch_floor_us": round(floor, 3),
+               "frac_beyond_launch_floor": round(wbytes / (kt / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if kt > 0 else None,
+               "fused_vs_F_linear": round(t_r / t_f, 3), "cold_copies": len(copies),
+               "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"}
+        del x, y, tiled, copies, refs
+        torch.cuda.empty_cache()
+        return row
     for name, N, Kd in FF_SHAPES:
         w = torch.empty(N, Kd, dtype=torch.float16, device="cuda")
         K.fill_synthetic(w, 7)
@@ -938,38 +967,27 @@ def fused_forward_section(rot_bytes=1 << 30):
                 out[-1].update(fused_ref_order_ms=round(t["fused_ref_order"], 4),
                                fused_ref_order_vs_F_linear=round(t["F.linear"] / t["fused_ref_order"], 3))
             del x, y, nib, sgm, zgm
-            # decode: M = 1, cold, codes in the decode tile layout (what QuantLinear "auto" keeps)
-            M = 1
-            x = (torch.randn(M, Kd, device="cuda", generator=gen) * 0.5).half()
-            y = torch.empty(M, N, dtype=torch.float16, device="cuda")
-            tiled = K.tile_codes(r.codes, N, Kd)
-            cb = r.codes.numel()
-            copies = [tiled] + [tiled.clone() for _ in range(int(rot_bytes // cb))]
-            wbytes = cb + r.scales.numel() * 2 + (r.zeros.numel() * 2 if r.zeros is not None else 0)
-            t_f = _graph_ms([(lambda c=c: K.w4a16_gemm(x, c, r.scales, r.zeros, 4, group, N, tiled=True, out=y))
-                             for c in copies], region=f"fused_forward/{name}/{gname}/M1/fused")
-            refs = [r.out] + [r.out.clone() for _ in range(int(rot_bytes // (N * Kd * 2)))]
-            t_r = _graph_ms([(lambda wt=wt: F.linear(x, wt)) for wt in refs],
-                            region=f"fused_forward/{name}/{gname}/M1/F.linear")
-            gbs = wbytes / (t_f / 1e3) / 1e9
-            kt = t_f - floor / 1e3
-            out.append({"shape": name, "N": N, "K": Kd, "weights": gname, "M": M, "bound": "hbm",
-                        "fused_ms": round(t_f, 5), "F_linear_ms": round(t_r, 5),
-                        "packed_weight_GBps": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
-                        "launch_floor_us": round(floor, 3),
-                        "frac_beyond_launch_floor": round(wbytes / (kt / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if kt > 0 else None,
-                        "fused_vs_F_linear": round(t_r / t_f, 3), "cold_copies": len(copies),
-                        "auto": "fused" if K.auto_fused_preferred(M, N, Kd, group) else "F.linear"})
-            del x, y, tiled, copies, refs, r
+            out.append(decode_row(name, N, Kd, r, group, gname))
+            del r
         del w
+        torch.cuda.empty_cache()
+    # the decode GEMV as QuantLinear "auto" runs it after fused_proj.fuse_projections: ONE launch over
+    # the row-concatenated q/k/v (and gate/up) codes of a layer, which amortises the per-launch floor
+    for name, N, Kd in DECODE_FUSED_SHAPES:
+        w = torch.empty(N, Kd, dtype=torch.float16, device="cuda")
+        K.fill_synthetic(w, 7)
+        r = K.quantize_minmax(w, 4, -2, False, 0, want_codes=True)
+        out.append(decode_row(name, N, Kd, r, -2, "per-channel"))
+        del r, w
         torch.cuda.empty_cache()
     return {"config": "BASELINE configs[2]: Llama-2-7B INT4 fused dequant+GEMM QuantLinear forward (packed codes) "
                       "vs F.linear on the dequantized fp16 weight, same run",
             "kernels": "M=8192: row-major codes k_w4a16_b16w (per channel 151, grouped 150), NIB codes "
                        "(QuantLinear nib_prefill) k_w4a16_b16p (persistent, 172) / b16w 152 (iwq_prefill16.hip); "
                        "grouped: group-major parameter copies (IWQ_FLAG_GROUP_MAJOR, what QuantLinear keeps), "
-                       "fused_ref_order = the reference's parameter order; M=1: k_w4a16_gemv(_ct) on tile-layout codes",
-            "mfma_peak_TFLOPs": MFMA_PEAK_TFLOPS, "rows": out}
+                       "fused_ref_order = the reference's parameter order; M=1: k_w4a16_gemv(_ct) on tile-layout codes "
+                       "(qkv_fused / gate_up_fused: the fused_proj concatenations, one launch per layer input)",
+            "mfma_peak_TFLOPs": MFMA_PEAK_TFLOPS, "launch_floor_us": round(floor, 3), "rows": out}
 
 
 def formats_section(rows=11008, cols=4096, copies=16):

@@ -351,3 +351,49 @@ def test_group_major_params_layout():
     assert K.group_major_params(s, None, N, Kd, g)[1] is None
     with pytest.raises(ValueError):
         K.group_major_params(s, z, N, Kd, -2)
+
+
+def test_trace_sections_cuts_a_kernel_trace_into_bench_regions(tmp_path):
+    """tools/trace_sections.py (round 5): dispatches are assigned to bench.py --mark-file regions by the
+    host clock that makes every region non-empty, same-name regions (the rounds of one interleaved arm)
+    merge, and the dominant kernel's average is set beside bench.py's own per-call figure."""
+    import csv
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import trace_sections as TS
+    d = tmp_path / "prof"
+    d.mkdir()
+    rows = []
+    # region A: 4 launches of 10 us at t = 1000.., region B (two rounds): 2 x 3 launches of 5 us + a small
+    # kernel, a dispatch outside every region
+    for i in range(4):
+        rows.append(("k_big", 1_000_000 + i * 11_000, 1_000_000 + i * 11_000 + 10_000))
+    for base in (2_000_000, 3_000_000):
+        for i in range(3):
+            rows.append(("k_mid", base + i * 6_000, base + i * 6_000 + 5_000))
+        rows.append(("k_tiny", base + 20_000, base + 20_500))
+    rows.append(("k_outside", 5_000_000, 5_001_000))
+    with open(d / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for n, s, e in rows:
+            w.writerow([n, s, e])
+    off = 777  # the "mono" clock is shifted: only "boot" puts every dispatch inside its region
+    marks = [{"region": "A", "t0": {"boot": 990_000, "mono": 990_000 + off, "real": 0},
+              "t1": {"boot": 1_050_000, "mono": 1_050_000 + off, "real": 1}, "bench_kernel_ms": 0.0100},
+             {"region": "B", "t0": {"boot": 1_990_000, "mono": 9e18, "real": 0},
+              "t1": {"boot": 2_030_000, "mono": 9e18, "real": 1}, "bench_ms_per_call_this_round": 0.0050},
+             {"region": "B", "t0": {"boot": 2_990_000, "mono": 9e18, "real": 0},
+              "t1": {"boot": 3_030_000, "mono": 9e18, "real": 1}, "bench_ms_per_call_this_round": 0.0052}]
+    (tmp_path / "marks.jsonl").write_text("".join(json.dumps(m) + "\n" for m in marks))
+    res = TS.summarize(TS.load_trace(str(d)), TS.load_marks(str(tmp_path / "marks.jsonl")))
+    assert res["clock"] == "boot" and res["regions_with_dispatches"] == 3
+    a, b = res["rows"]
+    assert a["region"] == "A" and [k["kernel"] for k in a["kernels"]] == ["k_big"]
+    assert a["kernels"][0]["dispatches"] == 4 and a["kernels"][0]["avg_us"] == 10.0
+    assert a["kernels"][0]["median_gap_us"] == 1.0 and a["dominant_avg_over_bench"] == 1.0
+    assert b["region"] == "B" and b["kernels"][0]["kernel"] == "k_mid" and b["kernels"][0]["dispatches"] == 6
+    assert b["kernels"][1]["kernel"] == "k_tiny" and b["kernels"][1]["dispatches"] == 2
+    assert b["bench"]["bench_ms_per_call_this_round"] == 0.0051  # median over the merged rounds
+    assert abs(b["dominant_avg_over_bench"] - 5.0 / 5.1) < 1e-3
