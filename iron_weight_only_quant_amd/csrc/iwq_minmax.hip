@@ -327,7 +327,8 @@ hipError_t launch_row(int dt, bool sym, int codes, const RowArgs& a, hipStream_t
 }
 
 // Block = TX column chunks (8 columns, 16 B each) x TY row slices.  Default 32 x 8 (512-B row
-// segments; 16 x 16 at g = 256 to bound registers), picked by tools/ab_col.py (profiles/r01_ab_col.jsonl:
+// segments) for g = 64, 16 x 16 at g = 128 (round 5, below) and g = 256 (to bound registers), picked
+// by tools/ab_col.py (profiles/r01_ab_col.jsonl:
 // 11008x4096 g=128 39.1 us vs 41.2 for the r1 8 x 32 shape, g=32 45.3 vs 67.7).  flags variant
 // 1 = 8 x 32, 2 = 32 x 8, 3 = 16 x 16.
 template <int DT, bool SYM, int CODES, int TX, int TY>
@@ -362,7 +363,10 @@ hipError_t launch_col_v(int variant, const ColArgs& a, hipStream_t st) {
   if (variant == 1) return launch_col_t<DT, SYM, CODES, 8, 32>(a, st);
   if (variant == 2) return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
 #endif
-  if (variant == 3 || a.g == 256) return launch_col_t<DT, SYM, CODES, 16, 16>(a, st);  // 16 rows/thread at g=256
+  // 16 x 16 at g = 128 (round 5: 37.8-37.9 vs 38.2-39.5 us for 32 x 8 on 11008 x 4096, two rounds of
+  // the same box, profiles/r05_ab_col.jsonl; 512-thread 32 x 16 / 64 x 8 / 16 x 32 blocks 38.8-40.4)
+  // and at g = 256 (16 rows per thread)
+  if (variant == 3 || a.g == 256 || (variant == 0 && a.g == 128)) return launch_col_t<DT, SYM, CODES, 16, 16>(a, st);
   return launch_col_t<DT, SYM, CODES, 32, 8>(a, st);
 }
 template <int DT, bool SYM>
