@@ -1223,10 +1223,11 @@ int iwq_quantize_fp_approx_lut(const void* w, int64_t rows, int64_t cols, int64_
                                uint32_t* nan_flag, unsigned flags, void* stream, const void* lut) {
   if (group <= 0) return IWQ_ERR_GROUP_MODE;  // approximate needs w_group_size > 0 (ValueError)
   if (!out_deq || !out_scales) return IWQ_ERR_ARG;
-  // A/B forms (variants 1..3 of the double-approximate decode) exist only in IWQ_AB builds; any other
+  // A/B forms (variants 1..3 of the double-approximate decode; the single-aligned decode has none and
+  // ignores them, so one flag set drives both in the A/B tests) exist only in IWQ_AB builds; any other
   // variant is refused here, before a launch, with IWQ_ERR_ARG like iwq_quantize_minmax does
   const int variant = (int)((flags >> 16) & 0xFFu);
-  if (variant != 0 && (!IWQ_AB || !double_approx || variant > 3)) return IWQ_ERR_ARG;
+  if (variant != 0 && (!IWQ_AB || variant > 3)) return IWQ_ERR_ARG;
   if (double_approx && (dtype == IWQ_BF16 || dtype == IWQ_F32))  // iwq_fpdt.hip
     return iwq::run_fp_dt(2, w, rows, cols, ld_w, dtype, exp_bits, mant_bits, group, 1, quant_dim, out_deq, ld_out,
                           nullptr, out_scales, nullptr, workspace, workspace_bytes, nan_flag, stream, hi_align_start,
