@@ -78,6 +78,14 @@ enum iwq_status {
                                         prefill kernel only: M >= 256, N % 256 == 0, K % 64 == 0,
                                         group % 64 == 0 (IWQ_ERR_ARG otherwise, with a variant,
                                         TILED or FORCE_GENERIC); combines with IWQ_FLAG_NIB_CODES  */
+#define IWQ_FLAG_WS_ZEROED 0x1000u   /* iwq_quantize_minmax, per tensor (group -1): the FIRST HALF of the
+                                        workspace (iwq_workspace_bytes / 2 bytes) is zero on entry (e.g.
+                                        a workspace kept per stream, zeroed once, used only by such
+                                        calls): no zeroing launch before the one-pass kernel.  Every
+                                        path leaves that half zero on exit (the one-pass kernel's last
+                                        workgroup clears its hand-off words; the two-kernel and
+                                        universal forms use only the second half, which needs no
+                                        zeroing).  Ignored by other calls.                           */
 /* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
  * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
  * (40-49 / 60-81 / 150-172 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first
@@ -86,7 +94,8 @@ enum iwq_status {
  * p of a code dword holds k = (0,2,4,6,1,3,5,7)[p].
  * The product library (libiwq.so) carries only the defaults and the variants the tests pin: 0;
  * iwq_w4a16_gemm 1 / 2 at M > 16 on row-major codes (the k_w4a16 / k_w4a16_big fallbacks);
- * per-tensor iwq_quantize_minmax 6 (the two-kernel form, the host's retry) and 9 (test-only abort);
+ * per-tensor iwq_quantize_minmax 6 (the two-kernel form, the host's retry), 8 (the one-pass kernel
+ * at any size; the default takes it from 32 MiB, 16 MiB for bf16) and 9 (test-only abort);
  * iwq_quantize_minmax_batched(_ex) 100 / 101 / 102 / 118 (the roofline probes bench.py times).
  * Any other variant returns IWQ_ERR_ARG there; the A/B library (libiwq_ab.so, built with IWQ_AB=1)
  * has them all, and iwq_build_info() ends in "ab=1". */

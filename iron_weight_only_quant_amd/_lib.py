@@ -28,6 +28,7 @@ IWQ_FLAG_BATCH_CODES = 0x100
 IWQ_FLAG_TILED_CODES = 0x200
 IWQ_FLAG_NIB_CODES = 0x400
 IWQ_FLAG_GROUP_MAJOR = 0x800
+IWQ_FLAG_WS_ZEROED = 0x1000
 
 EXPORTS = (
     "iwq_workspace_bytes", "iwq_quantize_minmax", "iwq_batch_plan", "iwq_quantize_minmax_batched",

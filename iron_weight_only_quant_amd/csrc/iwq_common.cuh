@@ -26,6 +26,36 @@ namespace iwq {
 // last HIP error of this host thread, shared by every translation unit (iwq_last_hip_error)
 int& last_hip_error();
 
+// Zeroing without hipMemsetAsync (round 5): a memset captured into a hipGraph comes back right on the
+// graph's FIRST replay only -- from the second on it leaves ~60 % of the bytes non-zero (every size
+// tried, 16 B to 8 KiB; tools/diag_graph_memset.py, profiles/r05_diag_graph_memset.log; eager memsets
+// are fine).  Every zeroing a caller may capture therefore goes through this kernel: 16-B vector
+// stores for the aligned body, byte stores for the head and tail.
+namespace {
+__global__ __launch_bounds__(256) void k_zero_bytes(unsigned char* p, uint64_t n, uint64_t head, uint64_t body16) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * 256;
+  if (t < head) p[t] = 0;
+  uint4* b = reinterpret_cast<uint4*>(p + head);
+  for (uint64_t i = t; i < body16; i += nt) b[i] = make_uint4(0u, 0u, 0u, 0u);
+  const uint64_t tail0 = head + body16 * 16;
+  if (tail0 + t < n) p[tail0 + t] = 0;  // < 16 tail bytes
+}
+}  // namespace
+
+inline hipError_t zero_async(void* p, uint64_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  unsigned char* c = static_cast<unsigned char*>(p);
+  uint64_t head = (16 - (reinterpret_cast<uintptr_t>(c) & 15)) & 15;
+  if (head > n) head = n;
+  const uint64_t body16 = (n - head) / 16;
+  uint64_t blocks = (body16 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_zero_bytes, dim3((unsigned)blocks), dim3(256), 0, st, c, n, head, body16);
+  return hipGetLastError();
+}
+
 
 enum : int { DT_F16 = 0, DT_BF16 = 1, DT_F32 = 2 };
 

@@ -1117,7 +1117,7 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
   }
   const int64_t need = ((8 * G + 255) / 256) * 256;
   if (!ws || ws_bytes < need || !aligned16p(ws)) return IWQ_ERR_WORKSPACE;
-  if (codes == 4) IWQ_HIP_FP(hipMemsetAsync(codes_out, 0, (size_t)(rows * (cols / 2)), s));
+  if (codes == 4) IWQ_HIP_FP(zero_async(codes_out, (uint64_t)(rows * (cols / 2)), s));
   SegArgs a{};
   a.w = static_cast<const char*>(w);
   a.out = static_cast<char*>(out);

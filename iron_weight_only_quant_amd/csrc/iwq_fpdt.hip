@@ -365,7 +365,7 @@ int run_fp_dt(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w
   if (!ws || ws_bytes < fp_dt_workspace_bytes(rows, cols, G, dbl) || (reinterpret_cast<uintptr_t>(ws) & 15))
     return IWQ_ERR_WORKSPACE;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (codes == 4) IWQ_HIP_DT(hipMemsetAsync(codes_out, 0, (size_t)(rows * (cols / 2)), s));
+  if (codes == 4) IWQ_HIP_DT(zero_async(codes_out, (uint64_t)(rows * (cols / 2)), s));
   auto r256 = [](int64_t b) { return (b + 255) / 256 * 256; };
   uint8_t* wsb = static_cast<uint8_t*>(ws);
   DtArgs d{};

@@ -862,7 +862,8 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
 // every workgroup sweeps all granules (relaxed agent-scope atomic loads, bounded spin) until every
 // tag is 1, folds them, and the workgroup quantizes its registers and stores -- 4 B per element of
 // HBM traffic instead of the two-kernel pair's 6.  The granules (8 B x CU count, at the workspace's
-// start) and the CONSENSUS word after them are zeroed by a hipMemsetAsync before every launch.
+// start), the CONSENSUS word and the done counter after them are zero before every launch (a zeroing
+// kernel, or IWQ_FLAG_WS_ZEROED: the kernel's last workgroup leaves them zero).
 //
 // Fail-safe hand-off (round 4): the hand-off needs every workgroup resident at once; when another
 // kernel holds CUs a sweep can give up.  Every workgroup stores NOTHING until the launch has agreed
@@ -889,7 +890,8 @@ constexpr unsigned long long OP_GO = 1, OP_ABORT = 2;
 // without touching memory, and the key fold masks them).  A granule counts once its tag equals 1.
 // Keys: 16-bit dtypes publish (min, max) as packed int16 in ONE granule per workgroup; fp32 (round 5)
 // publishes two granules, {tag, min key} and {tag, max key} (granules[2b], granules[2b + 1]); the
-// consensus word follows the last granule.  All granules are zeroed by the per-launch memset.
+// consensus word and a done counter follow the last granule.  All are zero on entry (the per-launch
+// memset, or IWQ_FLAG_WS_ZEROED) and the last workgroup to finish its hand-off zeroes them again.
 // Elementwise: fp16 takes the packed fast path, bf16 / fp32 (round 5) a Markstein-division fast path
 // on the register-held vectors; non-finite or extreme ranges re-read the input for the literal chain.
 template <int DT, bool SYM, int CODES, int NV>
@@ -1070,7 +1072,34 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
     }
   }
   __syncthreads();
-  if (fin[2] == 0) return;  // ABORT: no output byte is written (the input is untouched)
+  // round 5: past the barrier no wave of this workgroup reads a granule any more -- count the
+  // workgroup done; the LAST one zeroes the granules, the consensus word and the counter, so the next
+  // launch on the same workspace needs no memset (IWQ_FLAG_WS_ZEROED).  A relaxed increment is
+  // enough: wave 0's granule store, sweep loads and CAS all completed before the barrier (the loads
+  // and the CAS returned values that decided fin[]; the vector memory counter retires in order, so
+  // the earlier store was acknowledged too; the barrier's workgroup fences keep the compiler from
+  // hoisting the increment), and the last workgroup issues its clearing stores only after its
+  // increment returned the final count -- agent-scope atomics at the coherence point, so no clearing
+  // store overtakes a publish or a sweep.  The increment is issued here and its value used only at
+  // the end (clear_if_last), so its round trip overlaps this workgroup's output stores.
+  unsigned long long done = 0;
+  if (threadIdx.x == 0)
+    done = __hip_atomic_fetch_add(granules + (int)gridDim.x * KG + 1, 1ull, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  auto clear_if_last = [&]() {
+    if (threadIdx.x < 64) {
+      done = (unsigned long long)__shfl((long long)done, 0);
+      if (done == (unsigned long long)gridDim.x - 1) {
+        const int ng = (int)gridDim.x * KG;
+        for (int g = threadIdx.x; g < ng + 2; g += 64)
+          __hip_atomic_store(granules + g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if (fin[2] == 0) {  // ABORT: no output byte is written (the input is untouched)
+    clear_if_last();
+    return;
+  }
   const GroupParams p = params_from_keys<DT, SYM>(fin[0], fin[1], n_bits, rmax_for(n_bits, SYM));
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (scales) store_param<DT>(scales, 0, p.s);
@@ -1179,6 +1208,7 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
     }
   }
   flag_nan(nan_flag, any_nan);
+  clear_if_last();
 }
 
 template <int DT, bool SYM>

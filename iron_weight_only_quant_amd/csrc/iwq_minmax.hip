@@ -404,6 +404,12 @@ hipError_t launch_seg(int dt, bool sym, const SegArgs& a, hipStream_t st) {
 
 
 constexpr int TENSOR_PARTS_MAX = 4096;
+// A per-tensor workspace holds two regions of TENSOR_PARTS_MAX 8-byte words: the one-pass kernel's
+// granules, consensus word and done counter in the first (zeroed before its launch, or kept zero by
+// the caller and the kernel -- IWQ_FLAG_WS_ZEROED), the pair's / universal path's partial keys in the
+// second (fully written before they are read: never needs zeroing), so the pair leaves the first
+// region zero without a clearing launch.
+constexpr int TENSOR_SCRATCH_WORDS32 = TENSOR_PARTS_MAX * 2;  // the second region, in int32 units
 
 // Per-tensor variants (flags bits 16..23; profiles/r01_ab_tensor.jsonl):
 //   0/2: temporal loads in both passes (default: cold 11008x4096 51.1 -> 49.0 us, 4096^2 22.6 -> 20.0 us)
@@ -427,16 +433,19 @@ void launch_tensor_pair(const void* w, void* out, void* codes, void* scales, voi
 template <int DT, bool SYM, int CODES, int NV>
 hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t nvec,
                                     int nvt, int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int cus,
-                                    uint32_t spin_limit) {
+                                    uint32_t spin_limit, bool wsz) {
   // one workgroup per nvt * 512 vectors (<= the CU count: every chunk is non-empty and all are resident)
   const int64_t chunk = (int64_t)nvt * OP_THR;
   const int64_t nblk = (nvec + chunk - 1) / chunk;
   if (nvt < 1 || nvt > NV || nblk < 1 || nblk > cus) return hipErrorInvalidValue;
-  // the granules (two per workgroup for fp32's 32-bit keys) and the consensus word after them: zeroed
-  // before the launch
-  const size_t gbytes = ((size_t)(nblk * (DT == DT_F32 ? 2 : 1) + 1) * 8 + 15) / 16 * 16;
-  hipError_t e = hipMemsetAsync(ws, 0, gbytes, st);
-  if (e != hipSuccess) return e;
+  // the granules (two per workgroup for fp32's 32-bit keys), the consensus word and the done counter
+  // after them: zeroed before the launch unless the caller states they are (IWQ_FLAG_WS_ZEROED: the
+  // kernel's last workgroup leaves them zero, so a workspace kept per stream needs no memset launch)
+  if (!wsz) {
+    const size_t gbytes = ((size_t)(nblk * (DT == DT_F32 ? 2 : 1) + 2) * 8 + 15) / 16 * 16;
+    hipError_t e = zero_async(ws, gbytes, st);  // (not hipMemsetAsync: iwq_common.cuh)
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL((k_tensor_onepass<DT, SYM, CODES, NV>), dim3((unsigned)nblk), dim3(OP_THR), 0, st,
                      static_cast<const char*>(w), static_cast<char*>(out), static_cast<uint8_t*>(codes), scales, zeros,
                      nvec, nvt, reinterpret_cast<unsigned long long*>(ws), n_bits, nan_flag, spin_limit);
@@ -448,45 +457,61 @@ hipError_t launch_tensor_onepass_nv(const void* w, void* out, void* codes, void*
 template <int DT, bool SYM, int CODES>
 bool launch_tensor_onepass(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, hipError_t* err,
-                           bool fixed_nv, uint32_t spin_limit) {
+                           bool fixed_nv, uint32_t spin_limit, bool wsz) {
   if constexpr (DT != DT_F16 && CODES != 0) {
     return false;
   } else {
     if (nan_flag == nullptr) return false;  // an aborted hand-off must be reportable (bit 1)
     const int cus = device_cu_count();
-    // granules (two per workgroup for fp32) + the consensus word must fit the workspace
-    if ((int64_t)cus * (DT == DT_F32 ? 2 : 1) + 1 > (int64_t)TENSOR_PARTS_MAX) return false;
+    // granules (two per workgroup for fp32) + the consensus word + the done counter must fit the workspace
+    if ((int64_t)cus * (DT == DT_F32 ? 2 : 1) + 2 > (int64_t)TENSOR_PARTS_MAX) return false;
     const int64_t nvec = numel / 8;
     const int64_t per = (nvec + (int64_t)cus * OP_THR - 1) / ((int64_t)cus * OP_THR);
     // nvt = per spreads the chunks over every CU; fixed_nv (A/B) uses the template's NV instead
     if constexpr (DT == DT_F32) {
-      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-      else if (per <= 24) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 24>(w, out, codes, scales, zeros, nvec, fixed_nv ? 24 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit, wsz);
+      else if (per <= 24) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 24>(w, out, codes, scales, zeros, nvec, fixed_nv ? 24 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit, wsz);
       else return false;
     } else {
-      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-      else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
-      else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit);
+      if (per <= 16) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 16>(w, out, codes, scales, zeros, nvec, fixed_nv ? 16 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit, wsz);
+      else if (per <= 32) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 32>(w, out, codes, scales, zeros, nvec, fixed_nv ? 32 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit, wsz);
+      else if (per <= 48) *err = launch_tensor_onepass_nv<DT, SYM, CODES, 48>(w, out, codes, scales, zeros, nvec, fixed_nv ? 48 : (int)per, ws, n_bits, nan_flag, st, cus, spin_limit, wsz);
       else return false;
     }
     return true;
   }
 }
 
-// variants: 0 = one pass where the tensor fits the registers (fp16, n_bits <= 8), else the pair below;
-// 6 = the pair (round-2 default) forced; 7 = one pass with NV vectors per thread (the first form:
-// fewer, fuller chunks, some CUs idle);
+// variants: 0 = one pass where it pays (tensor_onepass_pays) and the tensor fits the registers, else
+// the pair below; 6 = the pair (round-2 default) forced; 7 = one pass with NV vectors per thread (the
+// first form: fewer, fuller chunks, some CUs idle); 8 = one pass wherever it fits (any size);
 // 9 = TEST ONLY: one pass whose every sweep gives up at once (spin limit 0), so the launch ABORTs:
 // nothing is written, nan_flag bit 1 is set, and the host's retry on the pair can be exercised
+// variant bit 8 (set by iwq_quantize_minmax from IWQ_FLAG_WS_ZEROED): the first workspace region is
+// zero on entry and must be zero on exit -- the one-pass kernel cleans up after itself, the pair never
+// touches it
+// Round 5 (profiles/r05_tensor_dt_sizes.jsonl, cold calls, zeroed workspace): the one pass pays from
+// 32 MiB of fp16 / fp32 and 16 MiB of bf16 (ties there); below, the hand-off's fixed cost (publish,
+// sweep and consensus round trips, ~4-5 us) exceeds the pair's second read, which mostly hits the
+// MALL at these sizes (8 MiB fp16: 14.7 us one pass vs 10.1 us pair; 48 MiB: 27.5 vs 30.5).
+template <int DT>
+bool tensor_onepass_pays(int64_t numel) {
+  const int64_t bytes = numel * (DT == DT_F32 ? 4 : 2);
+  return bytes >= (DT == DT_BF16 ? (16ll << 20) : (32ll << 20));
+}
+
 template <int DT, bool SYM, int CODES>
 hipError_t launch_tensor_t(const void* w, void* out, void* codes, void* scales, void* zeros, int64_t numel,
                            int32_t* ws, int n_bits, uint32_t* nan_flag, hipStream_t st, int variant) {
-  if (variant == 0 || variant == 7 || variant == 9) {
+  const bool wsz = (variant & 0x100) != 0;
+  variant &= 0xFF;
+  if ((variant == 0 && tensor_onepass_pays<DT>(numel)) || variant == 7 || variant == 8 || variant == 9) {
     hipError_t e = hipSuccess;
     if (launch_tensor_onepass<DT, SYM, CODES>(w, out, codes, scales, zeros, numel, ws, n_bits, nan_flag, st, &e,
-                                              IWQ_AB && variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT))
+                                              IWQ_AB && variant == 7, variant == 9 ? 0u : OP_SPIN_LIMIT, wsz))
       return e;
   }
+  ws += TENSOR_SCRATCH_WORDS32;  // the pair's partial keys: the second region
   const int64_t nunits = numel / 8;
   int64_t blocks = (int64_t)device_cu_count() * 8;
   const int64_t need = (nunits + BLOCK - 1) / BLOCK;
@@ -558,7 +583,7 @@ int64_t iwq_workspace_bytes(int64_t rows, int64_t cols, int64_t group, int quant
   int64_t L = 0, G = 0;
   if (rows <= 0 || cols <= 0) return 0;
   if (group_geometry(rows, cols, group, quant_dim, L, G) != IWQ_OK) return 0;
-  if (group == IWQ_GROUP_PER_TENSOR) return (int64_t)TENSOR_PARTS_MAX * 8;  // per-workgroup partial keys
+  if (group == IWQ_GROUP_PER_TENSOR) return (int64_t)TENSOR_PARTS_MAX * 16;  // the two regions above
   return ((8 * G + 255) / 256) * 256;
 }
 
@@ -588,10 +613,12 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
   const bool al = aligned16(w) && (!out_deq || aligned16(out_deq)) && (ld_w * eb) % 16 == 0 &&
                   (!out_deq || (ld_out * eb) % 16 == 0) && (!out_codes || aligned16(out_codes));
   const bool fastbits = n_bits <= 8;
-  // product library: the default, and per tensor the pair forced (6: the host's retry) and the
-  // test-only abort (9); every other variant is an A/B form (IWQ_AB builds)
+  // product library: the default, and per tensor the pair forced (6: the host's retry), the one pass
+  // forced (8) and the test-only abort (9); every other variant is an A/B form (IWQ_AB builds)
   const int variant = (int)((flags >> 16) & 0xFFu);
-  if (!IWQ_AB && variant != 0 && !(group == IWQ_GROUP_PER_TENSOR && (variant == 6 || variant == 9))) return IWQ_ERR_ARG;
+  if (!IWQ_AB && variant != 0 &&
+      !(group == IWQ_GROUP_PER_TENSOR && (variant == 6 || variant == 8 || variant == 9)))
+    return IWQ_ERR_ARG;
 
   if (!generic && quant_dim == 0 && group > 0 && group >= 8 && group <= 512 && is_pow2(group) && al &&
       fastbits && ld_w == cols && (!out_deq || ld_out == cols)) {
@@ -615,7 +642,8 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
     const int64_t need = iwq_workspace_bytes(rows, cols, group, quant_dim);
     if (!workspace || workspace_bytes < need || !aligned16(workspace)) return IWQ_ERR_WORKSPACE;
     IWQ_HIP(launch_tensor(dtype, sym, codes, w, out_deq, out_codes, out_scales, sym ? nullptr : out_zeros,
-                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s, variant));
+                          rows * cols, static_cast<int32_t*>(workspace), n_bits, nan_flag, s,
+                          variant | ((flags & IWQ_FLAG_WS_ZEROED) ? 0x100 : 0)));
     return IWQ_OK;
   }
   if (!generic && quant_dim == 0 && group != IWQ_GROUP_PER_TENSOR && L % 8 == 0 && L <= ROW_MAX_L && al && fastbits) {
@@ -659,7 +687,7 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
   if (codes == 4) {
     const int64_t nbytes = rows * (cols / 2);
     if ((reinterpret_cast<uintptr_t>(out_codes) & 3u) != 0) return IWQ_ERR_ARG;
-    IWQ_HIP(hipMemsetAsync(out_codes, 0, (size_t)nbytes, s));
+    IWQ_HIP(zero_async(out_codes, (uint64_t)nbytes, s));
   }
   SegArgs a{};
   a.w = static_cast<const char*>(w);
@@ -667,7 +695,8 @@ int iwq_quantize_minmax(const void* w, int64_t rows, int64_t cols, int64_t ld_w,
   a.codes = static_cast<uint8_t*>(out_codes);
   a.scales = out_scales;
   a.zeros = sym ? nullptr : out_zeros;
-  a.keys = static_cast<int32_t*>(workspace);
+  // per tensor: the second region (the first stays zero for IWQ_FLAG_WS_ZEROED callers)
+  a.keys = static_cast<int32_t*>(workspace) + (group == IWQ_GROUP_PER_TENSOR ? TENSOR_SCRATCH_WORDS32 : 0);
   a.rows = rows;
   a.cols = cols;
   a.ld_w = ld_w;

@@ -85,6 +85,32 @@ class _FlagPool:
 _flags = _FlagPool()
 
 
+class _TensorWsCache:
+    """Per (device, stream) workspace for per-tensor calls (include/iwq.h IWQ_FLAG_WS_ZEROED, round 5):
+    zeroed once, and every per-tensor call leaves its first half zero again (the one-pass kernel's
+    hand-off words; the pair's partial keys live in the second half), so the one-pass kernel runs without
+    a zeroing launch before it (one launch floor, ~1.6-1.9 us, per call).  Calls on one stream are
+    ordered, so one workspace per stream never serves two launches at once.  Not used while a graph is
+    captured (a replay may run on another stream): those calls get a fresh workspace and the memset."""
+
+    def __init__(self):
+        self.bufs = {}
+
+    def get(self, dev, stream_key, nbytes):
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), stream_key)
+        b = self.bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.zeros(max(nbytes, 256), dtype=torch.uint8, device=dev)
+            self.bufs[key] = b
+        return b
+
+    def drop(self, dev, stream_key):
+        self.bufs.pop((dev.index if dev.index is not None else torch.cuda.current_device(), stream_key), None)
+
+
+_tws = _TensorWsCache()
+
+
 def group_geometry(rows, cols, group, quant_dim):
     """(L, G) of the grouped view, or raise like the reference (quant_linear.py:896-906)."""
     vr, vc = (cols, rows) if quant_dim == 1 else (rows, cols)
@@ -114,12 +140,16 @@ def _raise_for(status, what):
 
 def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, quant_dim: int = 0,
                     out: Optional[torch.Tensor] = None, want_deq: bool = True, want_codes: bool = False,
-                    want_scales: bool = True, flags: int = 0) -> QuantResult:
+                    want_scales: bool = True, flags: int = 0,
+                    zeroed_workspace: Optional[torch.Tensor] = None) -> QuantResult:
     """Min-max fake-quantize a 2-D weight on the GPU.
 
     w       [rows, cols] fp16/bf16/fp32 CUDA tensor with unit column stride (any row stride).
     out     destination for the dequantized weight (may be `w` itself for in-place), else a new
             contiguous tensor is allocated when want_deq.
+    zeroed_workspace  per tensor only: a uint8 device tensor of >= iwq_workspace_bytes whose first
+            half is zero, and which the call leaves so (IWQ_FLAG_WS_ZEROED) -- for graph capture, where
+            the per-stream cache is not used; eager calls get the stream's cached one without asking.
     """
     L.require_device(w)
     if w.dim() != 2:
@@ -159,8 +189,22 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
     retry = None
     if st == L.IWQ_ERR_WORKSPACE:
         wsb = int(lib.iwq_workspace_bytes(rows, cols, group, quant_dim))
-        ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
+        skey = torch.cuda.current_stream(dev).cuda_stream if group == -1 else None
+        if group == -1 and zeroed_workspace is not None:
+            if zeroed_workspace.dtype != torch.uint8 or zeroed_workspace.numel() < wsb \
+                    or zeroed_workspace.device != dev:
+                raise ValueError(f"zeroed_workspace must be >= {wsb} uint8 bytes on {dev}")
+            ws, skey = zeroed_workspace, None
+            flags = int(flags) | L.IWQ_FLAG_WS_ZEROED
+        elif group == -1 and not torch.cuda.is_current_stream_capturing():
+            # the stream's zeroed workspace: no zeroing launch before the one-pass kernel
+            ws = _tws.get(dev, skey, wsb)
+            flags = int(flags) | L.IWQ_FLAG_WS_ZEROED
+        else:
+            ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=dev)
         st = call(ws, wsb)
+        if st != L.IWQ_OK and skey is not None and (int(flags) & L.IWQ_FLAG_WS_ZEROED):
+            _tws.drop(dev, skey)  # a failed launch may have left it dirty: zero a new one next time
         # where the C side can take the one-pass kernel (iwq_minmax.hip: per tensor, any quant_dim -- a
         # per-tensor group is the whole tensor, so quant_dim does not change the walk; fp16, and bf16 /
         # fp32 without packed codes)

@@ -46,7 +46,7 @@ def test_batch_entry_layout():
 
 def test_workspace_bytes(lib):
     assert lib.iwq_workspace_bytes(4096, 4096, 128, 0) == 8 * 4096 * 32
-    assert lib.iwq_workspace_bytes(4096, 4096, -1, 0) == 4096 * 8  # per-workgroup partial keys
+    assert lib.iwq_workspace_bytes(4096, 4096, -1, 0) == 4096 * 16  # one-pass hand-off words + partial keys
     assert lib.iwq_workspace_bytes(100, 64, -2, 1) == 512
     assert lib.iwq_workspace_bytes(4096, 100, 128, 0) == 0  # invalid geometry
 

@@ -296,7 +296,9 @@ def test_per_tensor_one_pass_ragged_dtypes(K, shape, dtype):
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(ref.dequant).view(np.uint8)), (shape, bits, sym)
         r6 = K.quantize_minmax(x, bits, -1, sym, 0, flags=K.gemm_variant_flags(6))
         assert np.array_equal(_np(r6.out).view(np.uint8), got.view(np.uint8))
-        assert int(r.nan_flag.item()) == 0
+        r8 = K.quantize_minmax(x, bits, -1, sym, 0, flags=K.gemm_variant_flags(8))  # the one pass forced
+        assert np.array_equal(_np(r8.out).view(np.uint8), got.view(np.uint8))
+        assert int(r.nan_flag.item()) == 0 and int(r8.nan_flag.item()) == 0
     # a constant huge tensor (range clamped to 1e-5: max|w| / s ~ 1e36 > 2^100) takes the literal
     # chain: same bits as the oracle
     big = np.full(shape, 1e30, dtype=np.float32)
@@ -304,19 +306,22 @@ def test_per_tensor_one_pass_ragged_dtypes(K, shape, dtype):
     ref = O.quantlinear_int(big_np, w_bit=4, w_group_size=-1, symmetric=False, dtype=dtype)
     xb = torch.from_numpy(np.ascontiguousarray(big_np).view(np.int32 if dtype == "float32" else np.int16))
     xb = xb.to(DEV).view(getattr(torch, dtype))
-    rb = K.quantize_minmax(xb, 4, -1, False, 0)
-    assert np.array_equal(_np(rb.out).view(np.uint8), np.ascontiguousarray(ref.dequant).view(np.uint8))
+    for fl in (0, K.gemm_variant_flags(8)):
+        rb = K.quantize_minmax(xb, 4, -1, False, 0, flags=fl)
+        assert np.array_equal(_np(rb.out).view(np.uint8), np.ascontiguousarray(ref.dequant).view(np.uint8))
     # non-finite values take the literal chain (the fast path's preconditions fail): NaN poisons all
     y = x.clone()
     y.view(-1)[len(y.view(-1)) // 2] = float("nan")
     assert K.quantize_minmax(y, 4, -1, False, 0).has_nan()
+    assert K.quantize_minmax(y, 4, -1, False, 0, flags=K.gemm_variant_flags(8)).has_nan()
 
 
 @pytest.mark.parametrize("shape", [(1, 8), (3, 40), (48, 256), (1000, 1000), (2048, 3000)])
 @pytest.mark.parametrize("sym", [False, True])
 def test_per_tensor_one_pass_ragged(K, shape, sym):
     """Small / ragged per-tensor sizes (one workgroup, partial chunks, a last chunk's out-of-range
-    buffer loads): equal to the oracle and to the two-kernel pair."""
+    buffer loads): the default (the pair below 32 MiB), the one pass forced (variant 8) and the pair
+    forced (6) equal to the oracle."""
     from oracle.synth import synth as _synth
     x_np = _synth(77 + shape[0], shape, "float16")
     x = torch.from_numpy(x_np).to(DEV)
@@ -326,4 +331,8 @@ def test_per_tensor_one_pass_ragged(K, shape, sym):
     assert np.array_equal(_np(r.scales).view(np.uint16), ref.scales.reshape(-1).view(np.uint16))
     r6 = K.quantize_minmax(x, 4, -1, sym, 0, flags=K.gemm_variant_flags(6))
     assert torch.equal(r6.out.view(torch.int16), r.out.view(torch.int16))
-    assert int(r.nan_flag.item()) == 0
+    r8 = K.quantize_minmax(x, 4, -1, sym, 0, want_codes=shape[1] % 2 == 0, flags=K.gemm_variant_flags(8))
+    assert torch.equal(r8.out.view(torch.int16), r.out.view(torch.int16))
+    if r.codes is not None:
+        assert torch.equal(r8.codes, r.codes)
+    assert int(r.nan_flag.item()) == 0 and int(r8.nan_flag.item()) == 0

@@ -817,8 +817,9 @@ def test_quantlinear_fused_forward_auto(K, monkeypatch):
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
 def test_per_tensor_fast_path(K, dtype):
     """group -1 (per-tensor) on a tensor big enough for many partial-key workgroups, quant_dim 0 and 1,
-    sym / asym, with codes: the default path (fp16 quant_dim 0: the one-pass kernel; else the
-    two-kernel reduce + apply) and the pair's variants vs the oracle, bit-exact."""
+    sym / asym, with codes: the default path (at 6 MB the two-kernel reduce + apply: the one pass pays
+    from 32 MiB), the one pass forced (variant 8; fp16, and bf16 / fp32 without codes) and the
+    pair's variants vs the oracle, bit-exact."""
     x = synth(55, (1536, 2048), dtype)
     big = np.float32(-3.25)  # a single outlier decides the scale
     x.reshape(-1)[123457] = O.f32_to_bf16_bits(big).reshape(-1)[0] if dtype == "bfloat16" else big
@@ -826,8 +827,8 @@ def test_per_tensor_fast_path(K, dtype):
     for bits, sym, qd in ((4, False, 0), (8, True, 0), (3, False, 1), (4, True, 1)):
         exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
         # + pair variants 1 (non-temporal), 3 (apply walks backwards), 4 / 5 (apply unrolled), 6 (the
-        # pair forced), one-pass variant 7 (NV vectors per thread)
-        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (6,) + abv(1, 3, 4, 5, 7)]:
+        # pair forced), one-pass variants 7 (NV vectors per thread) and 8 (the one pass at any size)
+        for flags in FLAG_SETS + [K.gemm_variant_flags(v) for v in (6, 8) + abv(1, 3, 4, 5, 7)]:
             r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=True, flags=flags)
             assert bits_equal(to_np(r.out), exp.dequant), (bits, sym, qd, flags)
             assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (bits, sym, qd)
@@ -887,8 +888,8 @@ def test_per_tensor_onepass_timeout_retry(K):
 
 
 def test_per_tensor_onepass_timeout_retry_quant_dim1(K):
-    """The same abort at quant_dim 1 (the C side takes the one-pass kernel for every fp16 per-tensor
-    call: the group is the whole tensor, so the walk does not depend on quant_dim): the retry is set
+    """The same abort at quant_dim 1 (the C side takes the one-pass kernel for per-tensor calls at any
+    quant_dim: the group is the whole tensor, so the walk does not depend on it): the retry is set
     up there too, out of place and in place, and QuantLinear(quant_dim=1) settles it."""
     x = synth(57, (1536, 2048), "float16")
     exp = O.quantlinear_int(x, 4, -1, False, 1, "float16")
@@ -917,6 +918,95 @@ def test_per_tensor_onepass_timeout_retry_quant_dim1(K):
         K.quantize_minmax = orig
     assert bits_equal(to_np(q.weight.data), exp.dequant)
     assert bits_equal(to_np(q.scales.view(-1)), exp.scales.reshape(-1))
+
+
+def _stream_ws(K):
+    dev = torch.device("cuda", torch.cuda.current_device())
+    return K._tws.bufs.get((dev.index, torch.cuda.current_stream(dev).cuda_stream))
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_per_tensor_workspace_left_zero(K, dtype):
+    """Per tensor, eager calls use the stream's cached workspace with IWQ_FLAG_WS_ZEROED (no zeroing
+    launch): every path must leave its first half zero -- the one-pass kernel (its last workgroup
+    clears the granules, the consensus word and the done counter; variant 8 forces it at these
+    sizes), the pair (the default here, variant 6, the bf16 / fp32 codes path: partial keys in the
+    second half), the aborted one-pass + retry (variant 9), the universal path (FORCE_GENERIC, a
+    ragged numel).  Tensors of different sizes and ranges back to back, each bit-exact vs the oracle
+    (a stale granule or consensus word would hand the next launch a wrong range or outcome)."""
+    cases = []
+    for i, (shape, scale) in enumerate((((1536, 2048), 1.0), ((64, 4096), 300.0), ((4096, 1024), 0.01),
+                                        ((7, 9), 2.0), ((2048, 2048), 1.0))):
+        x = synth(70 + i, shape, "float32") * np.float32(scale)
+        cases.append(x.astype(np.float32) if dtype == "float32" else
+                     (O.f32_to_bf16_bits(x) if dtype == "bfloat16" else x.astype(np.float16)))
+    runs = 0
+    for x in cases:
+        xd = to_dev(x, dtype)
+        for bits, sym, qd, codes in ((4, False, 0, False), (8, True, 1, False), (4, False, 0, True)):
+            exp = O.quantlinear_int(x, bits, -1, sym, qd, dtype)
+            for flags in (0, 1, K.gemm_variant_flags(6), K.gemm_variant_flags(8), K.gemm_variant_flags(9)):
+                if codes and x.shape[1] % 2:
+                    continue
+                r = K.quantize_minmax(xd, bits, -1, sym, qd, want_codes=codes, flags=flags)
+                assert not r.has_nan()
+                assert bits_equal(to_np(r.out), exp.dequant), (x.shape, bits, sym, qd, codes, flags)
+                assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (x.shape, bits, flags)
+                if codes:
+                    assert np.array_equal(r.codes.cpu().numpy().reshape(-1),
+                                          O.pack_codes(exp.codes, bits).reshape(-1)), (x.shape, bits, flags)
+                ws = _stream_ws(K)
+                assert ws is not None
+                torch.cuda.synchronize()
+                half = int(K.L.load().iwq_workspace_bytes(*x.shape, -1, qd)) // 2
+                assert int(ws[:half].count_nonzero()) == 0, ("workspace left dirty", x.shape, bits, qd, codes, flags)
+                runs += 1
+    assert runs >= 70
+
+
+def test_per_tensor_zeroed_workspace_graph(K):
+    """zeroed_workspace= under hipGraph capture (where the per-stream cache is not used): per-tensor
+    calls captured on one caller-zeroed workspace (the pair, the one pass forced), and one-pass calls
+    on fresh workspaces zeroed by the captured memset, replayed twice on new inputs: bit-exact vs the
+    oracle, the zeroed half of the workspace zero after each replay; a workspace too small is
+    refused."""
+    n = 5
+    xs = [synth(80 + i, (1024, 2048), "float16") for i in range(n)]
+    dev = [to_dev(x, "float16") for x in xs]
+    wsb = int(K.L.load().iwq_workspace_bytes(1024, 2048, -1, 0))
+    zw = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        K.quantize_minmax(dev[0], 4, -1, False, 0, zeroed_workspace=zw[:wsb - 16])
+    outs = [torch.empty_like(d) for d in dev]
+    # calls 0-2 on the zeroed workspace (default = the pair at 4 MB, then the one pass forced twice);
+    # calls 3-4 the one pass on captured-memset workspaces
+    kws = [dict(zeroed_workspace=zw), dict(zeroed_workspace=zw, flags=K.gemm_variant_flags(8)),
+           dict(zeroed_workspace=zw, flags=K.gemm_variant_flags(8)), dict(flags=K.gemm_variant_flags(8)),
+           dict(flags=K.gemm_variant_flags(8))]
+    res = []
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        for d, o, kw in zip(dev, outs, kws):  # warm-up outside the capture (lazy allocations)
+            K.quantize_minmax(d, 4, -1, False, 0, out=o, **kw)
+        with torch.cuda.graph(g, stream=s):
+            for d, o, kw in zip(dev, outs, kws):
+                res.append(K.quantize_minmax(d, 4, -1, False, 0, out=o, **kw))
+    torch.cuda.current_stream().wait_stream(s)
+    for rnd in range(2):
+        xs = [synth(90 + n * rnd + i, (1024, 2048), "float16") * np.float16(1 + 5 * i) for i in range(n)]
+        for d, x in zip(dev, xs):
+            d.copy_(to_dev(x, "float16"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(zw[:wsb // 2].count_nonzero()) == 0
+        for i, (x, o, r) in enumerate(zip(xs, outs, res)):
+            exp = O.quantlinear_int(x, 4, -1, False, 0, "float16")
+            assert not (int(r.nan_flag.item()) & 6)
+            assert bits_equal(to_np(o), exp.dequant), (rnd, i)
+            assert bits_equal(to_np(r.scales), exp.scales.reshape(-1)), (rnd, i)
+    del g
 
 
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])

@@ -1,5 +1,8 @@
 """Per-tensor (w_group_size = -1) quantization by storage dtype, cold single calls: the one-pass
-kernel (default where it applies) against the reduce + apply pair (variant 6), fp16 / bf16 / fp32.
+kernel (variant 8, forced; the default takes it from 32 MiB, 16 MiB for bf16) against the reduce +
+apply pair (variant 6), fp16 / bf16 / fp32;
+arms "0z" / "8z": on a caller-zeroed workspace (IWQ_FLAG_WS_ZEROED: no zeroing launch,
+what eager calls get from the per-stream cache).
 Per call device time from a hipGraph over distinct resident copies (>= 1 GiB per replay), median of 5
 replays; algorithmic bytes = read + write of the weight (+ the scale / zero).  One JSON line per arm.
 
@@ -20,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="4096x4096,11008x4096")
     ap.add_argument("--dtypes", default="float16,bfloat16,float32")
-    ap.add_argument("--variants", default="0,6")
+    ap.add_argument("--variants", default="0,0z,8z,6")
     ap.add_argument("--bits", type=int, default=4)
     a = ap.parse_args()
     from iron_weight_only_quant_amd import kernels as K
@@ -34,9 +37,12 @@ def main():
             for i, w in enumerate(ws):
                 K.fill_synthetic(w, 300 + i)
             outs = [torch.empty_like(w) for w in ws]
-            for v in (int(x) for x in a.variants.split(",")):
-                fl = K.gemm_variant_flags(v)
-                calls = [(lambda i=i: K.quantize_minmax(ws[i], a.bits, -1, False, 0, out=outs[i], flags=fl))
+            wsb = int(K.L.load().iwq_workspace_bytes(rows, cols, -1, 0))
+            zw = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+            for v in a.variants.split(","):
+                fl = K.gemm_variant_flags(int(v.rstrip("z")))
+                kw = {"zeroed_workspace": zw} if v.endswith("z") else {}
+                calls = [(lambda i=i: K.quantize_minmax(ws[i], a.bits, -1, False, 0, out=outs[i], flags=fl, **kw))
                          for i in range(n)]
                 us = graph_us(calls)
                 alg = rows * cols * eb * 2 + 2 * eb
