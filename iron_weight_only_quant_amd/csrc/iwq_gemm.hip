@@ -322,6 +322,41 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
 //     column tile are summed through LDS in k-split order (deterministic).
 // ---------------------------------------------------------------------------------------------
 constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X image (2+ workgroups per CU)
+// grouped decode (round 5): the (s, z) rows of np / gpr consecutive columns starting at parameter
+// index pbase, staged as one dword per group (s | z << 16), rows padded to gpr + 1 dwords.  The first
+// PRE chunks per thread are loaded by pst_preload (issued together with the X image's loads) and
+// written by pst_store, which also walks any longer rows.
+constexpr int PST_LDS_MAX = 80 * 1024;  // X image + staged parameters per workgroup (2 per CU)
+template <int PRE>
+__device__ __forceinline__ void pst_preload(const GemmArgs& a, int64_t pbase, int np, int nthr, uint32_t (&ps)[PRE],
+                                            uint32_t (&pz)[PRE]) {
+  const uint32_t zs = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a.zsym);
+#pragma unroll
+  for (int r = 0; r < PRE; ++r) {
+    const int i = (int)threadIdx.x + r * nthr;
+    ps[r] = i < np ? (uint32_t)gp<uint16_t>(a.scales)[pbase + i] : 0u;
+    pz[r] = i < np && a.zeros ? (uint32_t)gp<uint16_t>(a.zeros)[pbase + i] : zs;
+  }
+}
+template <int PRE>
+__device__ __forceinline__ void pst_store(const GemmArgs& a, uint32_t* pst, int64_t pbase, int np, int nthr,
+                                          const uint32_t (&ps)[PRE], const uint32_t (&pz)[PRE]) {
+#pragma unroll
+  for (int r = 0; r < PRE; ++r) {
+    const int i = (int)threadIdx.x + r * nthr;
+    if (i < np) {
+      const int c = i / a.gpr, g = i - c * a.gpr;
+      pst[c * (a.gpr + 1) + g] = ps[r] | (pz[r] << 16);
+    }
+  }
+  const uint32_t zs = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a.zsym);
+  for (int i = (int)threadIdx.x + PRE * nthr; i < np; i += nthr) {  // rows longer than PRE chunks
+    const int c = i / a.gpr, g = i - c * a.gpr;
+    const uint32_t sv16 = gp<uint16_t>(a.scales)[pbase + i];
+    const uint32_t zv16 = a.zeros ? (uint32_t)gp<uint16_t>(a.zeros)[pbase + i] : zs;
+    pst[c * (a.gpr + 1) + g] = sv16 | (zv16 << 16);
+  }
+}
 
 // TILED: codes in the decode tile layout (iwq_tile_codes): the 1 KiB a wave loads for one 128-k
 // step of its 16 columns is contiguous (lane l = 16 q + r at byte 16 l), instead of 16 column rows x
@@ -329,8 +364,19 @@ constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X imag
 // PC (per channel, a.gpr == 1): B = (q - z) exactly and the fp32 result is scaled once in the
 // epilogue, y = RN16(s * sum x (q - z) + b), as the prefill kernels' FACTOR path (4 fewer VALU per
 // 8 weights; A = I still gives W_deq exactly: s (q - z) is exact in fp32)
-template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false, bool PC = false>
+// PST (grouped, round 5): the workgroup's parameter rows -- its 16 T columns of the reference's
+// [N, K/g] scales and zero points, one contiguous run each -- are staged into LDS beside the X image
+// by coalesced loads, (s, z) interleaved in one dword and the rows padded to gpr + 1 dwords (the 16
+// columns a step reads land in distinct banks); a step then takes its (s, z) with one ds_read_b32
+// instead of two 2-byte global gathers over 16 rows on the in-order vmcnt behind its code loads.
+// GF (grouped, round 5): the scale FACTORED per k-step (group % 128 == 0: a step lies in one group):
+// B = (q - z) exactly as PC, the step's four MFMAs into a fresh accumulator, then
+// acc += s_g * step -- the PC numerics per group, y = RN16(sum_g s_g sum_{k in g} x (q - z) + b)
+// (A = I still gives W_deq exactly), 16 fewer VALU per k-step than RN16((q - z) s) per weight.
+template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false, bool PC = false, bool PST = false,
+          bool GF = false>
 __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
+  static_assert(!PST || !PC, "staged parameters: grouped weights only");
   constexpr int WPB = S * T;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63;
@@ -364,7 +410,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   auto load = [&](int j, int u) {
     const int kt = ks + j * S;
     bc[u] = __builtin_nontemporal_load(gp<u32x4>(cbase + kt * kstride));
-    if (!perch) {
+    if (!perch && !PST) {
       const int kk = kt * BK + 32 * q;
       const int64_t gi = (int64_t)n * a.gpr + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group);
       sv[u] = gp<_Float16>(a.scales)[gi];
@@ -375,36 +421,80 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
       for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
     }
   };
+  // the code prefetch first (DRAM: the longest latency); then the X image (XLDS) and the staged
+  // parameters (PST), their first XPRE / PRE chunks loaded into registers together before any is
+  // written, so their latencies overlap.  (Issuing X before the codes, so that its wait does not
+  // include them in vmcnt order, measured 4-7 % SLOWER on every shape: the codes' DRAM latency is
+  // the critical path, profiles/r05_gemv_grouped.jsonl.)
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (u < nj) load(u, u);
-
+  constexpr int XPRE = 4, PRE = 4;
+  const int cpr = a.K / 8;                   // 16-B chunks per X row
+  const int nxc = XLDS ? a.M * cpr : 0;      // chunks of the X image
+  u32x4 xpre[XPRE];
+  // PST: after the X image (or at the start without one)
+  uint32_t* pst = reinterpret_cast<uint32_t*>(dsm + (XLDS ? (a.M * xpitch + 15) / 16 * 16 : 0));
+  const int np = PST ? T * 16 * a.gpr : 0;
+  const int64_t pbase = (int64_t)blockIdx.x * np;
+  uint32_t pre_s[PRE], pre_z[PRE];
   if constexpr (XLDS) {
-    // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c
-    const int cpr = a.K / 8;
-    for (int m = 0; m < a.M; ++m) {
-      const _Float16* xr = a.x + (int64_t)m * a.lda;
-      for (int c = threadIdx.x; c < cpr; c += WPB * 64) {
-        const u32x4 d = *gp<u32x4>(xr + 8 * c);
+#pragma unroll
+    for (int r = 0; r < XPRE; ++r) {
+      const int i = threadIdx.x + r * WPB * 64;
+      const int m = i / cpr, c = i - m * cpr;
+      xpre[r] = i < nxc ? *gp<u32x4>(a.x + (int64_t)m * a.lda + 8 * c) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  if constexpr (PST) pst_preload<PRE>(a, pbase, np, WPB * 64, pre_s, pre_z);
+  if constexpr (XLDS || PST) {
+    if constexpr (XLDS) {
+      // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c
+      auto put = [&](int i, u32x4 d) {
+        const int m = i / cpr, c = i - m * cpr;
         const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
                           perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
         *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+      };
+#pragma unroll
+      for (int r = 0; r < XPRE; ++r) {
+        const int i = threadIdx.x + r * WPB * 64;
+        if (i < nxc) put(i, xpre[r]);
+      }
+      for (int i = threadIdx.x + XPRE * WPB * 64; i < nxc; i += WPB * 64) {  // long / many X rows
+        const int m = i / cpr, c = i - m * cpr;
+        put(i, *gp<u32x4>(a.x + (int64_t)m * a.lda + 8 * c));
       }
     }
+    if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, WPB * 64, pre_s, pre_z);
     __syncthreads();
   }
   const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+  // PST: this lane's column row of the staged parameters (tile, r16)
+  const uint32_t* prow = pst + (tile * 16 + r16) * (a.gpr + 1);
   const DqConst dq;
 
   f4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 accs = {0.f, 0.f, 0.f, 0.f};  // GF: the running k-step's partial tile
   for (int j0 = 0; j0 < nj; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int j = j0 + u;
       if (j >= nj) break;
       const int kt = ks + j * S;
-      const h2 s2 = perch ? h2{sc0, sc0} : h2{sv[u], sv[u]};
-      const h2 z2 = perch ? h2{zz0, zz0} : h2{zv[u], zv[u]};
+      h2 s2, z2;
+      float sf = 0.f;  // GF: the step's group scale
+      if constexpr (PST) {
+        const int kk = kt * BK + 32 * q;
+        const uint32_t sz = prow[a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group];
+        if constexpr (GF) sf = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz & 0xFFFFu));
+        else s2 = as_h2(__builtin_amdgcn_perm(sz, sz, 0x01000100u));
+        z2 = as_h2(__builtin_amdgcn_perm(sz, sz, 0x03020302u));
+      } else {
+        s2 = perch ? h2{sc0, sc0} : h2{sv[u], sv[u]};
+        z2 = perch ? h2{zz0, zz0} : h2{zv[u], zv[u]};
+        if constexpr (GF) sf = (float)sv[u];
+      }
       const h2 z1024 = z2 + k1024, z64 = z2 + k64;  // exact: z is a small integer
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -421,17 +511,22 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
         if constexpr (PROBE >= 1) {  // A/B probe only: no dequantization (wrong results)
           const uint32_t w = bc[u][s];
           bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
-        } else if constexpr (PC) {
+        } else if constexpr (PC || GF) {
           bf = dequant8_ns(bc[u][s], z1024, z64, dq);
         } else {
           bf = dequant8(bc[u][s], z1024, z64, s2, dq);
         }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
+        if constexpr (GF) accs = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, s == 0 ? f4{0.f, 0.f, 0.f, 0.f} : accs, 0, 0, 0);
+        else acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bf, acc, 0, 0, 0);
+      }
+      if constexpr (GF) {  // this lane's 4 accumulators all belong to its column r16: one scale
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(sf, accs[e], acc[e]);
       }
       if (j + PF < nj) load(j + PF, u);
     }
   }
-  if constexpr (XLDS) __syncthreads();  // X image dead: its LDS now holds the partial tiles
+  if constexpr (XLDS || PST) __syncthreads();  // X image / parameters dead: the LDS now holds the partial tiles
   float* red = reinterpret_cast<float*>(dsm);  // [WPB][256], wave (tile, ks) at index ks*T + tile
   *reinterpret_cast<f4*>(red + wid * 256 + lane * 4) = acc;
   __syncthreads();
@@ -454,9 +549,11 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
 // on-chip traffic: k_w4a16_gemv reads (or stages) X once per 16-column tile, M * 256 B per 1 KiB of
 // codes (M = 16: 4x the code bytes from L2).  Here each wave applies one A fragment to CT column
 // tiles (CT code loads per k-step, CT accumulators), so X traffic per code byte drops CT-fold.
-// Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits.
-template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false>
+// Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits
+// (GF: the grouped scale factored per k-step, as k_w4a16_gemv's PM 2).
+template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false, bool GF = false, bool PST = false>
 __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
+  static_assert(!PST || !PC, "staged parameters: grouped weights only");
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63;
   const int ks = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -489,7 +586,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
 #pragma unroll
     for (int c = 0; c < CT; ++c)
       bc[u][c] = __builtin_nontemporal_load(gp<u32x4>(cbase + c * tstride + kt * (TILED ? 1024 : BK / 2)));
-    if (!perch) {
+    if (!perch && !PST) {
       const int kk = kt * BK + 32 * q;
       const int gk = a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group;
 #pragma unroll
@@ -508,25 +605,35 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   for (int u = 0; u < PF; ++u)
     if (u < nj) load(u, u);
 
-  if constexpr (XLDS) {
-    const int cpr = a.K / 8;
-    for (int m = 0; m < a.M; ++m) {
-      const _Float16* xr = a.x + (int64_t)m * a.lda;
-      for (int c = threadIdx.x; c < cpr; c += S * 64) {
-        const u32x4 d = *gp<u32x4>(xr + 8 * c);
-        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
-                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
-        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+  // PST (round 5, as k_w4a16_gemv): the CT tiles' parameter rows, after the X image
+  constexpr int PRE = 4;
+  uint32_t* pst = reinterpret_cast<uint32_t*>(dsm + (XLDS ? (a.M * xpitch + 15) / 16 * 16 : 0));
+  const int np = PST ? CT * 16 * a.gpr : 0;
+  const int64_t pbase = (int64_t)tile0 * 16 * a.gpr;
+  uint32_t pre_s[PRE], pre_z[PRE];
+  if constexpr (PST) pst_preload<PRE>(a, pbase, np, S * 64, pre_s, pre_z);
+  if constexpr (XLDS || PST) {
+    if constexpr (XLDS) {
+      const int cpr = a.K / 8;
+      for (int m = 0; m < a.M; ++m) {
+        const _Float16* xr = a.x + (int64_t)m * a.lda;
+        for (int c = threadIdx.x; c < cpr; c += S * 64) {
+          const u32x4 d = *gp<u32x4>(xr + 8 * c);
+          const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                            perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+          *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+        }
       }
     }
+    if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, S * 64, pre_s, pre_z);
     __syncthreads();
   }
   const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
   const DqConst dq;
 
-  f4 acc[CT];
+  f4 acc[CT], accs[CT];
 #pragma unroll
-  for (int c = 0; c < CT; ++c) acc[c] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < CT; ++c) acc[c] = accs[c] = f4{0.f, 0.f, 0.f, 0.f};
   for (int j0 = 0; j0 < nj; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -534,10 +641,21 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
       if (j >= nj) break;
       const int kt = ks + j * S;
       h2 s2[CT], z1024[CT], z64[CT];
+      float sf[CT];  // GF: the step's group scale per tile
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
-        s2[c] = perch ? h2{sc0[c], sc0[c]} : h2{sv[u][c], sv[u][c]};
-        const h2 z2 = perch ? h2{zz0[c], zz0[c]} : h2{zv[u][c], zv[u][c]};
+        h2 z2;
+        if constexpr (PST) {
+          const int kk = kt * BK + 32 * q;
+          const uint32_t sz = pst[(c * 16 + r16) * (a.gpr + 1) + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group)];
+          s2[c] = as_h2(__builtin_amdgcn_perm(sz, sz, 0x01000100u));
+          z2 = as_h2(__builtin_amdgcn_perm(sz, sz, 0x03020302u));
+          sf[c] = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz & 0xFFFFu));
+        } else {
+          s2[c] = perch ? h2{sc0[c], sc0[c]} : h2{sv[u][c], sv[u][c]};
+          z2 = perch ? h2{zz0[c], zz0[c]} : h2{zv[u][c], zv[u][c]};
+          sf[c] = perch ? 0.f : (float)sv[u][c];
+        }
         z1024[c] = z2 + k1024;
         z64[c] = z2 + k64;
       }
@@ -553,15 +671,26 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
           af = __builtin_bit_cast(h8, pa);
         }
 #pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          if constexpr (GF)
+            accs[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq),
+                                                             s == 0 ? f4{0.f, 0.f, 0.f, 0.f} : accs[c], 0, 0, 0);
+          else
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, PC ? dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq) : dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
+                acc[c], 0, 0, 0);
+        }
+      }
+      if constexpr (GF) {
+#pragma unroll
         for (int c = 0; c < CT; ++c)
-          acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-              af, PC ? dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq) : dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
-              acc[c], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[c][e] = __builtin_fmaf(sf[c], accs[c][e], acc[c][e]);
       }
       if (j + PF < nj) load(j + PF, u);
     }
   }
-  if constexpr (XLDS) __syncthreads();
+  if constexpr (XLDS || PST) __syncthreads();
   float* red = reinterpret_cast<float*>(dsm);  // [S][CT][256]
 #pragma unroll
   for (int c = 0; c < CT; ++c) *reinterpret_cast<f4*>(red + (ks * CT + c) * 256 + lane * 4) = acc[c];
@@ -603,33 +732,60 @@ inline int gemv_auto_ct(int64_t M, int64_t N, int64_t K) {
 }
 
 template <int PF, int S, int CT, bool TILED>
-void launch_gemv_ct(const GemmArgs& a, hipStream_t st, bool allow_pc = true) {
+void launch_gemv_ct(const GemmArgs& a, hipStream_t st, bool allow_pc = true, bool allow_gf = true) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * CT));
   const size_t red = (size_t)S * CT * 256 * 4;
   const bool pc = a.gpr == 1 && allow_pc;
-  if (xbytes <= XLDS_MAX) {
+  const bool gf = !pc && allow_gf && a.group % BK == 0;  // the grouped scale factored per k-step
+  // grouped + gf: the CT tiles' parameter rows staged after the X image (PST)
+  const bool xl = xbytes <= XLDS_MAX;
+  const int64_t pend = (xl ? (xbytes + 15) / 16 * 16 : 0) + (int64_t)16 * CT * (a.gpr + 1) * 4;
+  const bool pst = gf && pend <= PST_LDS_MAX;
+  const size_t ldsp0 = red > (size_t)pend ? red : (size_t)pend;
+  if (xl) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, true>), dim3(blocks), dim3(S * 64), lds, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, false, true, true>), dim3(blocks), dim3(S * 64), ldsp, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, false, true>), dim3(blocks), dim3(S * 64), lds, st, a);
     else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED>), dim3(blocks), dim3(S * 64), lds, st, a);
   } else {
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, true>), dim3(blocks), dim3(S * 64), red, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, false, true, true>), dim3(blocks), dim3(S * 64), ldsp0, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, false, true>), dim3(blocks), dim3(S * 64), red, st, a);
     else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED>), dim3(blocks), dim3(S * 64), red, st, a);
   }
 }
 
 template <int PF, int S, int T, int PROBE = 0, bool TILED = false>
-void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds, bool allow_pc = true) {
+// pm (grouped weights): 0 = parameters per k-step from global memory, scale per weight (the form
+// before round 5), 1 = staged in LDS (PST) when they fit beside X, 2 = PST + the scale factored per
+// k-step (GF, where every k-step lies in one group; also without PST when X is not staged)
+void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds, bool allow_pc = true, int pm = 2) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * T));
   const size_t red = (size_t)S * T * 256 * 4;
   const bool pc = a.gpr == 1 && PROBE == 0 && allow_pc;
-  if (allow_lds && xbytes <= XLDS_MAX) {
+  // grouped: the staged parameters (PST) after the X image, 16 T rows of gpr + 1 dwords
+  const bool xl = allow_lds && xbytes <= XLDS_MAX;
+  const int64_t pend = (xl ? (xbytes + 15) / 16 * 16 : 0) + (int64_t)16 * T * (a.gpr + 1) * 4;
+  const bool pst = !pc && PROBE == 0 && pm > 0 && pend <= PST_LDS_MAX;
+  const bool gf = !pc && PROBE == 0 && pm == 2 && a.group % BK == 0;  // every k-step inside one group
+  const size_t ldsp0 = red > (size_t)pend ? red : (size_t)pend;
+  if (xl) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, true>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    else if (pst && gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, true, true>), dim3(blocks), dim3(S * T * 64), ldsp, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, true>), dim3(blocks), dim3(S * T * 64), ldsp, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, false, true>), dim3(blocks), dim3(S * T * 64), lds, st, a);
     else hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), lds, st, a);
   } else {
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED, true>), dim3(blocks), dim3(S * T * 64), red, st, a);
+    else if (pst && gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED, false, true, true>), dim3(blocks), dim3(S * T * 64), ldsp0, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED, false, true>), dim3(blocks), dim3(S * T * 64), ldsp0, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED, false, false, true>), dim3(blocks), dim3(S * T * 64), red, st, a);
     else hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, false, PROBE, TILED>), dim3(blocks), dim3(S * T * 64), red, st, a);
   }
 }
@@ -1318,8 +1474,10 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 102: launch_gemv<2, 8, 1, 2, true>(a, st, true); break;  // probe: k-major order
       case 103: launch_gemv<2, 16, 1, 2, true>(a, st, true); break;
       case 104: launch_gemv<2, 16, 1, 1, true>(a, st, true); break;
-      case 25: launch_gemv<2, 8, 1, 0, true>(a, st, true, false); break;  // per-element scale (A/B)
-      case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false); break;
+      case 25: launch_gemv<2, 8, 1, 0, true>(a, st, true, false, 0); break;  // per-element scale (A/B)
+      case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false, false); break;
+      case 27: launch_gemv<2, 8, 1, 0, true>(a, st, true, true, 0); break;  // grouped: params per step, global
+      case 28: launch_gemv<2, 8, 1, 0, true>(a, st, true, true, 1); break;  // grouped: staged, scale per weight
 #endif
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);

@@ -616,6 +616,28 @@ def test_w4a16_gemm_vs_fp32_reference(K, M, group, sym, bits):
     assert float((y.float() - y2.float()).abs().max()) <= 4 * float(err.max()) + 2e-3
 
 
+@pytest.mark.parametrize("group,sym", [(128, False), (128, True), (256, False), (64, False), (-2, False)])
+def test_gemv_identity_rows_give_w_deq(K, group, sym):
+    """Decode GEMV with X = rows of the identity (x[i, k_i] = 1): y[i, n] must be W_deq[n, k_i] BIT
+    FOR BIT -- the per-channel kernel's factored scale, the grouped kernel's scale factored per k-step
+    (group % 128 == 0: acc += s_g * partial) and the per-weight RN16((q - z) s) forms all keep each
+    weight the reference's fp16 value (s (q - z) is exact in fp32)."""
+    N, Kd, M = 384, 2048, 8
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 66)
+    r = K.quantize_minmax(w, 4, group, sym, 0, want_codes=True)
+    ks = [255 * i + 3 for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    for i, k in enumerate(ks):
+        x[i, k] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    tiled = K.tile_codes(r.codes, N, Kd)
+    for v in (0,) + (abv(27, 28) if group != -2 else ()):
+        for codes, tl in ((r.codes, False), (tiled, True)):
+            y = K.w4a16_gemm(x, codes, r.scales, r.zeros, 4, group, N, tiled=tl, flags=K.gemm_variant_flags(v))
+            assert torch.equal(y.view(torch.int16), want.view(torch.int16)), (v, tl)
+
+
 @pytest.mark.parametrize("Kd", [256, 1152, 4096])
 @pytest.mark.parametrize("M", [1, 16])
 def test_gemv_persistent_many_groups(K, Kd, M):
@@ -652,6 +674,10 @@ def test_gemv_tiled_layout_identical(K, group):
         y0 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, b)
         y1 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True)
         assert torch.equal(y0.view(torch.int16), y1.view(torch.int16)), m
+        if AB and group != -2:  # grouped, scale per weight: parameters per step from global memory (27)
+            y2 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True, flags=K.gemm_variant_flags(27))
+            y3 = K.w4a16_gemm(x, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True, flags=K.gemm_variant_flags(28))
+            assert torch.equal(y2.view(torch.int16), y3.view(torch.int16)), m  # vs staged in LDS (28)
     with pytest.raises(Exception):
         K.w4a16_gemm(torch.randn(32, Kd, device=DEV).half(), tiled, r.scales, r.zeros, 4, group, N, tiled=True)
     # tiled A/B variants: same S (k-split) => same summation order as the row-major variant of that
