@@ -475,7 +475,10 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   const DqConst dq;
 
   f4 acc = {0.f, 0.f, 0.f, 0.f};
-  f4 accs = {0.f, 0.f, 0.f, 0.f};  // GF: the running k-step's partial tile
+  // GF: the running k-step's partial tile, and the previous step's (folded into acc only after this
+  // step's MFMAs are issued, so the VALU never waits on the MFMA chain it just fed)
+  f4 accs = {0.f, 0.f, 0.f, 0.f}, accp = {0.f, 0.f, 0.f, 0.f};
+  float sfp = 0.f;
   for (int j0 = 0; j0 < nj; j0 += PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -521,10 +524,16 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
       }
       if constexpr (GF) {  // this lane's 4 accumulators all belong to its column r16: one scale
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(sf, accs[e], acc[e]);
+        for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(sfp, accp[e], acc[e]);  // step j - 1 (0 at j = 0)
+        accp = accs;
+        sfp = sf;
       }
       if (j + PF < nj) load(j + PF, u);
     }
+  }
+  if constexpr (GF) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(sfp, accp[e], acc[e]);  // the last step
   }
   if constexpr (XLDS || PST) __syncthreads();  // X image / parameters dead: the LDS now holds the partial tiles
   float* red = reinterpret_cast<float*>(dsm);  // [WPB][256], wave (tile, ks) at index ks*T + tile
