@@ -2626,7 +2626,10 @@ hipError_t launch_16e(const PrefillArgs& a, hipStream_t st) {
 // (row-major or the decode tile layout), decoded in natural order (dq8).  grid = (N / (16 CT),
 // ceil(M / (16 MT))): row tiles past M read row M-1 (discarded).
 // ---------------------------------------------------------------------------------------------
-template <int PF, int S, int CT, int MT, bool FACTOR, bool TILED>
+// PST (grouped, round 5; as the decode GEMV's): the CT tiles' (s, z) rows staged into LDS once per
+// workgroup -- one dword per group, rows padded to gpr + 1 dwords -- instead of 2 CT two-byte gathers
+// per k-step on the in-order vmcnt behind the code and X loads.
+template <int PF, int S, int CT, int MT, bool FACTOR, bool TILED, bool PST = false>
 __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
   constexpr bool SCALE = !FACTOR;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
@@ -2675,7 +2678,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int s = 0; s < 4; ++s) xa[u][mt][s] = *gp<u32x4>(xrow[mt] + kt * 128 + 8 * s);
-    if (!perch) {
+    if (!perch && !PST) {
       const int gk = (kt * 128 + 32 * q) / a.group;
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
@@ -2688,6 +2691,35 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (u < nj) load(u, u);
+  uint32_t* pst = reinterpret_cast<uint32_t*>(dsm);
+  if constexpr (PST) {
+    constexpr int PRE = 4, NT = S * 64;
+    const int np = CT * 16 * a.gpr;
+    const int64_t pbase = (int64_t)tile0 * 16 * a.gpr;
+    const uint32_t zs = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)a.zsym);
+    uint32_t ps[PRE], pz[PRE];
+#pragma unroll
+    for (int r = 0; r < PRE; ++r) {  // issued together: one round of latency
+      const int i = (int)threadIdx.x + r * NT;
+      ps[r] = i < np ? (uint32_t)gp<uint16_t>(a.scales)[pbase + i] : 0u;
+      pz[r] = i < np && a.zeros ? (uint32_t)gp<uint16_t>(a.zeros)[pbase + i] : zs;
+    }
+#pragma unroll
+    for (int r = 0; r < PRE; ++r) {
+      const int i = (int)threadIdx.x + r * NT;
+      if (i < np) {
+        const int c = i / a.gpr, g = i - c * a.gpr;
+        pst[c * (a.gpr + 1) + g] = ps[r] | (pz[r] << 16);
+      }
+    }
+    for (int i = (int)threadIdx.x + PRE * NT; i < np; i += NT) {
+      const int c = i / a.gpr, g = i - c * a.gpr;
+      const uint32_t sv16 = gp<uint16_t>(a.scales)[pbase + i];
+      const uint32_t zv16 = a.zeros ? (uint32_t)gp<uint16_t>(a.zeros)[pbase + i] : zs;
+      pst[c * (a.gpr + 1) + g] = sv16 | (zv16 << 16);
+    }
+    __syncthreads();
+  }
 
   f4 acc[MT][CT];
 #pragma unroll
@@ -2705,6 +2737,12 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
         if (perch) {
           s2[c] = sv0[c];
           z2[c] = zz0[c];
+        } else if constexpr (PST) {
+          const int kt = ks + j * S;
+          const uint32_t sz = pst[(c * 16 + r16) * (a.gpr + 1) + (kt * 128 + 32 * q) / a.group];
+          const float zf = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz >> 16));
+          s2[c] = as_h2(__builtin_amdgcn_perm(sz, sz, 0x01000100u));
+          z2[c] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
         } else {
           const float zf = (float)zv[u][c];
           s2[c] = h2{sv[u][c], sv[u][c]};
@@ -2727,6 +2765,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
     }
   }
   (void)SCALE;
+  if constexpr (PST) __syncthreads();  // the staged parameters are dead: the LDS holds the partial tiles
   float* red = reinterpret_cast<float*>(dsm);  // [S][MT * CT][256]
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -2754,8 +2793,17 @@ template <int PF, int S, int CT, int MT>
 hipError_t launch_mid(const PrefillArgs& a, bool tiled, hipStream_t st) {
   const dim3 grid((unsigned)(a.N / (16 * CT)), (unsigned)((a.M + 16 * MT - 1) / (16 * MT)));
   const size_t red = (size_t)S * MT * CT * 256 * 4;
-  if (tiled) hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true>), grid, dim3(S * 64), red, st, a);
-  else hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false>), grid, dim3(S * 64), red, st, a);
+  const size_t pbytes = (size_t)CT * 16 * (a.gpr + 1) * 4;
+  const bool pst = a.gpr > 1 && pbytes <= 64 * 1024;  // grouped: parameters staged (PST)
+  const size_t lds = pst && pbytes > red ? pbytes : red;
+  if (pst) {
+    if (tiled) hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true, true>), grid, dim3(S * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false, true>), grid, dim3(S * 64), lds, st, a);
+  } else if (tiled) {
+    hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true>), grid, dim3(S * 64), red, st, a);
+  } else {
+    hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false>), grid, dim3(S * 64), red, st, a);
+  }
   return hipGetLastError();
 }
 
