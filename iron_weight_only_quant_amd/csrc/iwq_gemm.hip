@@ -1340,8 +1340,8 @@ int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t 
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
   if (g <= 0 || K % g != 0) return 0;
-  int ns = 0;
-  if (prefill_short_split(M, N, K, (int)(K / g), (int)g, &ns)) return prefill_splitk_bytes_s(M, N, 2, ns);
+  int ns = 0, mtw = 2;
+  if (prefill_short_split(M, N, K, (int)(K / g), (int)g, &ns, &mtw)) return prefill_splitk_bytes_s(M, N, mtw, ns);
   if (!prefill_split_preferred(M, N, K, (int)(K / g), (int)g)) return 0;
   return prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
 }
@@ -1409,10 +1409,10 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     return IWQ_ERR_ARG;
   // default at M > 16: the split-K prefill where it is modelled faster (M >= 256: whenever a split
   // helps; 16 < M < 256: against the mid-M kernel) and the caller gave the workspace it needs
-  int short_ns = 0;
+  int short_ns = 0, short_mtw = 2;
   const bool short_pref = variant == 0 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
-                          prefill_short_split(M, N, K, a.gpr, a.group, &short_ns) &&
-                          workspace_bytes >= prefill_splitk_bytes_s(M, N, 2, short_ns);
+                          prefill_short_split(M, N, K, a.gpr, a.group, &short_ns, &short_mtw) &&
+                          workspace_bytes >= prefill_splitk_bytes_s(M, N, short_mtw, short_ns);
   const bool split_pref = !short_pref && variant == 0 && M > 16 && workspace && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
                           prefill_split_preferred(M, N, K, a.gpr, a.group) &&
                           workspace_bytes >= prefill_splitk_bytes(M, N, prefill_splitk_count(M, N, K, 0));
@@ -1556,7 +1556,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     // short-tile split prefill: the default's plan, or forced for A/B (110-125: 128-row tiles,
     // 130-145: 64-row tiles, S = v - 108 / v - 128)
     PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
-    const int mtw = short_pref ? 2 : (variant < 130 ? 4 : 2);
+    const int mtw = short_pref ? short_mtw : (variant < 130 ? 4 : 2);
     int ns = short_pref ? short_ns : (int)variant - (variant < 130 ? 108 : 128);
     if (ns > K / 64) ns = (int)(K / 64);
     if (!workspace || workspace_bytes < prefill_splitk_bytes_s(M, N, mtw, ns)) return IWQ_ERR_WORKSPACE;

@@ -50,7 +50,7 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 int64_t prefill_splitk_bytes_s(int64_t M, int64_t N, int mtw, int nsplit);
 hipError_t prefill_splitk_launch_s(const PrefillArgs& a, int mtw, hipStream_t st);
 // default plan for 16 < M < 256: the short-tile split (64-row tiles, *ns ranges) or not
-bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns);
+bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns, int* mtw);
 
 // 16x16x32 form of the prefill kernel (iwq_prefill16.hip), per channel: A/B variants 150 / 151
 bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);

@@ -2906,19 +2906,38 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 // 128 < M < 256: the short split also wins where it stays under ~128 tiles (q / down: 20 % / 12 %
 // over the 256-row split at M = 160-250, profiles/r02_ab_gemm_short_split_hi.jsonl); wider weights
 // (gate) keep the 256-row split.
-bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out) {
+// Round 5: 64 < M < 256 on wide weights (N >= 8192: 7B gate/up, 70B gate/up/down) takes 128-row
+// tiles (MTW 4: half the per-tile re-dequantization of the weights) with S = min(256 / tiles,
+// K-steps / 16, 8) -- profiles/r05_ab_short_split128.jsonl, M = 96 / 128: 70B gate g128 168 -> 100 us,
+// 70B down 139 -> 100, 7B gate 32.5 -> 28.8 (per channel 87 -> 79, 85 -> 68, 28.0 -> 26.5); past
+// M = 128 while the 128-row tiles stay <= 128 (70B down M = 160-224: g128 208-259 -> 163-172 us,
+// 7B gate neutral); more tiles (70B gate past 128 rows) keep the 256-row split, and the N = 4096
+// shapes the 64-row form (q / down: the mid kernel or 64-row tiles measured faster).
+bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out, int* mtw_out) {
   if (M <= 16 || M >= 256 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
   // grouped scales cost the mid kernel ~1.4x (profiles/r02_ab_gemm_g128_mid.jsonl)
   const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * (gpr != 1 ? 1.4 : 1.0);
   if (mid_us < 24.0) return false;
+  const int64_t nk = K / TK;
+  const int64_t tiles128 = ((M + 127) / 128) * (N / TN);
+  if (M > 64 && N >= 8192 && (M <= 128 || tiles128 <= 128)) {
+    const int64_t tiles = tiles128;
+    int64_t ns = 256 / tiles;
+    if (ns > nk / 16) ns = nk / 16;  // >= 16 K-steps per range
+    if (ns > 8) ns = 8;
+    if (ns < 2) ns = 2;
+    if (ns_out) *ns_out = (int)ns;
+    if (mtw_out) *mtw_out = 4;
+    return true;
+  }
   const int64_t tiles = ((M + 63) / 64) * (N / TN);
   if (M > 128 && tiles > 128) return false;
-  const int64_t nk = K / TK;
   int64_t ns = 256 / tiles;  // at most ~256 workgroups: best or within ~7 % in every sweep
   if (ns > 12) ns = 12;
   if (ns > nk / 4) ns = nk / 4;
   if (ns < 2) ns = 2;
   if (ns_out) *ns_out = (int)ns;
+  if (mtw_out) *mtw_out = 2;
   return true;
 }
 

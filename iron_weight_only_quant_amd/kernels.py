@@ -471,10 +471,17 @@ def auto_fused_preferred(M: int, N: int, K: int, group: int) -> bool:
     Llama-2-7B q / gate / down, 4-bit): per channel the fused kernels win at every M <= 192
     (1.01-3.6x) and on down-like weights (K >= 2N) up to M = 1024 (1.14-1.31x); g128 wins at every
     M <= 32 (1.06-3.2x) and on down-like weights up to M = 512 (1.08-1.72x), but not on q_proj at
-    M = 64 (0.86x) or gate_proj at 128-192 (0.92-0.94x)."""
+    M = 64 (0.86x) or gate_proj at 128-192 (0.92-0.94x).  Round 5 (g128 parameters staged in LDS in the
+    GEMV / mid kernels, 128-row split tiles on wide weights; profiles/r05_ab_auto_g128.jsonl): g128 now
+    also wins on gate-like weights (N > K) up to M = 128 (1.06-1.35x) and on square ones at
+    M = 96-192 (1.09-1.43x; 48-64 stay at 0.91-1.0x)."""
     if group == -2:
         return M <= 192 or (M <= 1024 and K >= 2 * N) or (M >= 4096 and (N, K) in LARGE_M_FUSED)
-    return M <= 32 or (M <= 512 and K >= 2 * N)
+    if K >= 2 * N:
+        return M <= 512
+    if N > K:
+        return M <= 128
+    return M <= 32 or 96 <= M <= 192
 
 
 def packed_fused_preferred(M: int, N: int, K: int, group: int) -> bool:

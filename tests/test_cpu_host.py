@@ -324,10 +324,13 @@ def test_quant_result_timeout_bit_raises():
 
 def test_auto_fused_policy():
     """QuantLinear(fused_forward="auto")'s rule (kernels.auto_fused_preferred, profiles/
-    r03_ab_auto_graph.jsonl): per channel fused up to 192 rows (1024 on K >= 2N weights) and from 4096
-    rows on the LARGE_M_FUSED shapes, grouped up to 32 rows (512 on K >= 2N), F.linear otherwise."""
+    r03_ab_auto_graph.jsonl, r05_ab_auto_g128.jsonl): per channel fused up to 192 rows (1024 on K >= 2N
+    weights) and from 4096 rows on the LARGE_M_FUSED shapes; grouped up to 512 rows on K >= 2N, 128 on
+    N > K, and on square weights up to 32 and from 96 to 192 rows; F.linear otherwise."""
     from iron_weight_only_quant_amd.kernels import auto_fused_preferred as P
     assert P(1, 11008, 4096, 128) and P(32, 4096, 4096, 128) and not P(64, 4096, 4096, 128)
+    assert P(96, 4096, 4096, 128) and P(192, 4096, 4096, 128) and not P(255, 4096, 4096, 128)
+    assert P(128, 11008, 4096, 128) and not P(192, 11008, 4096, 128)
     assert P(192, 11008, 4096, -2) and not P(193, 4096, 4096, -2) and not P(8192, 4096, 4096, -2)
     assert P(512, 4096, 11008, 128) and not P(1024, 4096, 11008, 128)
     assert P(1024, 4096, 11008, -2) and not P(2048, 4096, 11008, -2)

@@ -1473,9 +1473,14 @@ def test_w4a16_splitk_workspace_rule(K):
     assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 4096, -2) == 0  # mid-M kernel
     assert lib.iwq_w4a16_gemm_workspace_bytes(64, 11008, 4096, -2) == 43 * 5 * short
     assert lib.iwq_w4a16_gemm_workspace_bytes(64, 4096, 11008, -2) == 16 * 12 * short
-    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 86 * 2 * short
+    # 64 < M <= 128 on wide weights: 128-row tiles (twice the partial bytes), S = min(256 / tiles, nk / 16, 8)
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 11008, 4096, -2) == 43 * 4 * 2 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(128, 28672, 8192, 128) == 112 * 2 * 2 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(96, 8192, 28672, -2) == 32 * 8 * 2 * short
+    assert lib.iwq_w4a16_gemm_workspace_bytes(96, 4096, 11008, -2) == 32 * 8 * short  # N = 4096: 64-row
+    assert lib.iwq_w4a16_gemm_workspace_bytes(192, 8192, 28672, 128) == 64 * 4 * 2 * short  # <= 128 tiles
     assert lib.iwq_w4a16_gemm_workspace_bytes(200, 4096, 11008, -2) == 64 * 4 * short  # short: 4 x 16 tiles
-    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 11008, 4096, -2) == 43 * 4 * tile  # wide: 256-row split
+    assert lib.iwq_w4a16_gemm_workspace_bytes(200, 11008, 4096, -2) == 86 * 2 * 2 * short  # wide: 128-row tiles
     assert lib.iwq_w4a16_gemm_workspace_bytes(16, 11008, 4096, -2) == 0  # decode GEMV
     assert lib.iwq_w4a16_gemm_workspace_bytes(256, 4096, 4096, -2) == 16 * 8 * tile
     assert lib.iwq_w4a16_gemm_workspace_bytes(512, 4096, 4096, -2) == 32 * 5 * tile
