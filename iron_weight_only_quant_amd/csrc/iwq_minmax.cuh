@@ -623,9 +623,25 @@ template <int DT, bool SYM, int CODES, int TX, int TY, int RPT>
 __device__ __forceinline__ void column_reg_body(const ColArgs& a, int64_t bx, int64_t by) {
   using F = Fmt<DT>;
   constexpr int NC = TX * 8;  // columns per block
-  __shared__ int32_t s_mn[TY][NC];
-  __shared__ int32_t s_mx[TY][NC];
+  // Round 5 (LDS bank conflicts were 78 % of the kernel's LDS cycles, PMC): the partials live as
+  // [ty][i][tx] with a row pitch of NC + TX dwords, so the 8-column stores of a wave's lanes (tx, ty)
+  // hit distinct banks, and the fold threads (i, tx) read them in lane order; the fp16 fast path's
+  // per-column words go out structure-of-arrays [i][tx] (16 lanes of distinct tx, 64 consecutive
+  // dwords), replacing 8 GroupParams reads whose 192-B stride folded onto 4 banks and the 16-fold
+  // redundant biased_words math of the TY row slices.
+  // (SOA: fp16 up to 32 x 8 blocks; the 64 x 4 form of the short groups keeps the GroupParams
+  // reads, whose 12 KiB more LDS would cost it two of its five workgroups per CU)
+  // (the 64 x 4 form keeps the column-major partials [ty][8 tx + i]: its 8 consecutive dwords per
+  // thread go out as two b128 writes, and the transposed layout measured 3 % slower there, g = 32)
+  constexpr bool TL = TX <= 32;
+  constexpr int PP = TL ? NC + TX : NC;
+  constexpr bool SOA = DT == DT_F16 && TL;
+  constexpr int NW = SOA ? NC : 1;
+  __shared__ int32_t s_mn[TY * PP];
+  __shared__ int32_t s_mx[TY * PP];
   __shared__ GroupParams f_p[NC];
+  __shared__ uint32_t w_bounds[NW], w_sz[NW], w_kc[NW], w_fast[NW];
+  __shared__ float w_rs[NW], w_s[NW];
   const int tx = threadIdx.x % TX;
   const int ty = threadIdx.x / TX;
   const int64_t c0 = (bx * TX + tx) * 8;
@@ -685,16 +701,31 @@ __device__ __forceinline__ void column_reg_body(const ColArgs& a, int64_t bx, in
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s_mn[ty][tx * 8 + i] = mn[i]; s_mx[ty][tx * 8 + i] = mx[i]; }
+  for (int i = 0; i < 8; ++i) {
+    const int e = ty * PP + (TL ? i * TX + tx : tx * 8 + i);
+    s_mn[e] = mn[i];
+    s_mx[e] = mx[i];
+  }
   __syncthreads();
   // one thread per column folds the TY partials AND derives the group's parameters once (not once
   // per row slice: 8x less parameter math at TY = 8), shared through LDS
-  for (int cc = threadIdx.x; cc < NC; cc += TX * TY) {  // NC > threads for the 64 x 4 shape
+  for (int t = threadIdx.x; t < NC; t += TX * TY) {  // NC > threads for the 64 x 4 shape
+    const int fi = t / TX, ftx = t - fi * TX;          // TL: column ftx * 8 + fi
+    const int cc = TL ? ftx * 8 + fi : t;
     int32_t a_mn = 0x7FFFFFFF, a_mx = (int32_t)0x80000000;
 #pragma unroll 8
-    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y][cc]); a_mx = max(a_mx, s_mx[y][cc]); }
+    for (int y = 0; y < TY; ++y) { a_mn = min(a_mn, s_mn[y * PP + t]); a_mx = max(a_mx, s_mx[y * PP + t]); }
     const GroupParams q = params_from_keys<DT, SYM>(a_mn, a_mx, a.n_bits, rmax_for(a.n_bits, SYM));
     f_p[cc] = q;
+    if constexpr (SOA) {
+      const BiasedWords bw = biased_words<SYM>(q, a.n_bits);
+      w_bounds[t] = bw.bounds;
+      w_sz[t] = bw.sz;
+      w_kc[t] = bw.kc;
+      w_rs[t] = bw.rs;
+      w_s[t] = bw.s;
+      w_fast[t] = q.fast ? 1u : 0u;
+    }
     const int64_t col = bx * NC + cc;
     if (col < a.cols) {
       const int64_t gidx = col * (a.rows / a.g) + jr;
@@ -703,21 +734,41 @@ __device__ __forceinline__ void column_reg_body(const ColArgs& a, int64_t bx, in
     }
   }
   __syncthreads();
-  GroupParams p[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) p[i] = f_p[tx * 8 + i];
   bool any_nan = false;
   if (cvalid) {
     const uint32_t off = SYM ? (1u << (a.n_bits - 1)) : 0u;
     if constexpr (DT == DT_F16) {
       // all 8 columns of this thread on the fast path: packed pairs with per-half group operands
+      // (the pairs assembled from the fold's per-column words, biased_pair's packing)
       bool fast = a.n_bits <= 9;
+      GroupParams pf[8];
+      if constexpr (SOA) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) fast = fast && p[i].fast;
+        for (int i = 0; i < 8; ++i) fast = fast && w_fast[i * TX + tx] != 0u;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          pf[i] = f_p[tx * 8 + i];
+          fast = fast && pf[i].fast;
+        }
+      }
       if (fast) {
         BiasedPair bp[4];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) bp[jj] = biased_pair<SYM>(p[2 * jj], p[2 * jj + 1], a.n_bits);
+        for (int jj = 0; jj < 4; ++jj) {
+          if constexpr (SOA) {
+            const int e0 = (2 * jj) * TX + tx, e1 = (2 * jj + 1) * TX + tx;
+            bp[jj].rs = f2{w_rs[e0], w_rs[e1]};
+            bp[jj].s = f2{w_s[e0], w_s[e1]};
+            const uint32_t b0 = w_bounds[e0], b1 = w_bounds[e1];
+            bp[jj].lo = (b0 & 0xFFFFu) | (b1 << 16);
+            bp[jj].hi = (b0 >> 16) | (b1 & 0xFFFF0000u);
+            bp[jj].s16 = (w_sz[e0] & 0xFFFFu) | (w_sz[e1] << 16);
+            bp[jj].kc = (w_kc[e0] & 0xFFFFu) | (w_kc[e1] << 16);
+          } else {
+            bp[jj] = biased_pair<SYM>(pf[2 * jj], pf[2 * jj + 1], a.n_bits);
+          }
+        }
 #pragma unroll
         for (int k = 0; k < RPT; ++k) {
           const int64_t r = r0 + ty + k * TY;
@@ -732,6 +783,9 @@ __device__ __forceinline__ void column_reg_body(const ColArgs& a, int64_t bx, in
         return;
       }
     }
+    GroupParams p[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[i] = f_p[tx * 8 + i];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int64_t r = r0 + ty + k * TY;
