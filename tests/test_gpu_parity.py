@@ -1435,8 +1435,8 @@ def test_w4a16_short_tile_split(K, M, group):
 
 def test_w4a16_midm_split_default(K):
     """16 < M < 256 on a gate_proj-shaped weight: the default takes the split the plan prefers
-    (M = 128: the short-tile split, 64-row tiles, 2 K ranges; M = 200: the 256-row split, 4 K
-    ranges) -- same bits as forcing that plan, within tolerance of fp32."""
+    (round 5, N >= 8192: 128-row tiles -- M = 128: 4 K ranges, M = 200: 2 K ranges) -- same bits as
+    forcing that plan, within tolerance of fp32."""
     if torch.cuda.get_device_properties(0).multi_processor_count != 256:
         pytest.skip("the modelled split count is for 256 CUs")
     N, Kd, M = 11008, 4096, 128
@@ -1453,9 +1453,9 @@ def test_w4a16_midm_split_default(K):
     z0 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N)
     torch.testing.assert_close(z0.float(), x2.float() @ r.out.float().t(), rtol=2e-2, atol=2e-2)
     if AB:
-        y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(130))
+        y4 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(112))
         assert torch.equal(y0, y4)
-        z4 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(84))
+        z4 = K.w4a16_gemm(x2, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(110))
         assert torch.equal(z0, z4)
 
 
