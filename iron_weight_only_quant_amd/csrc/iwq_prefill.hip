@@ -2629,8 +2629,12 @@ hipError_t launch_16e(const PrefillArgs& a, hipStream_t st) {
 // PST (grouped, round 5; as the decode GEMV's): the CT tiles' (s, z) rows staged into LDS once per
 // workgroup -- one dword per group, rows padded to gpr + 1 dwords -- instead of 2 CT two-byte gathers
 // per k-step on the in-order vmcnt behind the code and X loads.
-template <int PF, int S, int CT, int MT, bool FACTOR, bool TILED, bool PST = false>
+// GF (group % 128 == 0, with PST): the scale factored per 128-k step as the decode GEMV's -- B =
+// (q - z) exactly, each (row tile, column tile)'s four MFMAs of the step into a fresh accumulator,
+// then acc += s_g * partial (A = I still gives W_deq bit for bit).
+template <int PF, int S, int CT, int MT, bool FACTOR, bool TILED, bool PST = false, bool GF = false>
 __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
+  static_assert(!GF || PST, "the factored scale reads the staged parameters");
   constexpr bool SCALE = !FACTOR;
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63;
@@ -2721,7 +2725,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
     __syncthreads();
   }
 
-  f4 acc[MT][CT];
+  f4 acc[MT][CT], accs[GF ? MT : 1][GF ? CT : 1];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -2732,6 +2736,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
       const int j = j0 + u;
       if (j >= nj) break;
       h2 s2[CT], z2[CT];
+      float sf[CT];  // GF: the step's group scale per column tile
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
         if (perch) {
@@ -2743,6 +2748,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
           const float zf = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz >> 16));
           s2[c] = as_h2(__builtin_amdgcn_perm(sz, sz, 0x01000100u));
           z2[c] = h2{(_Float16)(1024.0f + zf), (_Float16)(64.0f + zf)};
+          sf[c] = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz & 0xFFFFu));
         } else {
           const float zf = (float)zv[u][c];
           s2[c] = h2{sv[u][c], sv[u][c]};
@@ -2753,13 +2759,26 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
       for (int s = 0; s < 4; ++s) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-          const h8 bf = (perch && FACTOR) ? dq8<false>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v)
-                                          : dq8<true>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v);
+          const h8 bf = ((perch && FACTOR) || GF) ? dq8<false>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v)
+                                                  : dq8<true>(bc[u][c][s], z2[c], s2[c], mask_s, magic_v);
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, xa[u][mt][s]), bf,
-                                                                acc[mt][c], 0, 0, 0);
+          for (int mt = 0; mt < MT; ++mt) {
+            if constexpr (GF)
+              accs[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, xa[u][mt][s]), bf,
+                                                                   s == 0 ? f4{0.f, 0.f, 0.f, 0.f} : accs[mt][c], 0, 0, 0);
+            else
+              acc[mt][c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, xa[u][mt][s]), bf,
+                                                                  acc[mt][c], 0, 0, 0);
+          }
         }
+      }
+      if constexpr (GF) {  // a lane's 4 accumulators of a tile all belong to its column r16
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[mt][c][e] = __builtin_fmaf(sf[c], accs[mt][c][e], acc[mt][c][e]);
       }
       if (j + PF < nj) load(j + PF, u);
     }
@@ -2790,13 +2809,17 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_mid(PrefillArgs a) {
 }
 
 template <int PF, int S, int CT, int MT>
-hipError_t launch_mid(const PrefillArgs& a, bool tiled, hipStream_t st) {
+hipError_t launch_mid(const PrefillArgs& a, bool tiled, hipStream_t st, bool mid_no_gf = false) {
   const dim3 grid((unsigned)(a.N / (16 * CT)), (unsigned)((a.M + 16 * MT - 1) / (16 * MT)));
   const size_t red = (size_t)S * MT * CT * 256 * 4;
   const size_t pbytes = (size_t)CT * 16 * (a.gpr + 1) * 4;
   const bool pst = a.gpr > 1 && pbytes <= 64 * 1024;  // grouped: parameters staged (PST)
+  const bool gf = pst && a.group % 128 == 0 && !mid_no_gf;  // and the scale factored per k-step
   const size_t lds = pst && pbytes > red ? pbytes : red;
-  if (pst) {
+  if (gf) {
+    if (tiled) hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true, true, true>), grid, dim3(S * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false, true, true>), grid, dim3(S * 64), lds, st, a);
+  } else if (pst) {
     if (tiled) hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, true, true>), grid, dim3(S * 64), lds, st, a);
     else hipLaunchKernelGGL((k_w4a16_mid<PF, S, CT, MT, true, false, true>), grid, dim3(S * 64), lds, st, a);
   } else if (tiled) {
@@ -2824,6 +2847,14 @@ bool mid_supported(int64_t M, int64_t N, int64_t K, int gpr, int group) {
 // 0 = by M (interleaved A/B vs hipBLASLt on the Llama-2-7B shapes, profiles/r02_ab_mid*.jsonl:
 // M <= 32 -> 50, M <= 64 -> 52, above -> 53)
 hipError_t mid_launch(const PrefillArgs& a, int variant, bool tiled, hipStream_t st) {
+#if IWQ_AB
+  if (variant == 56) {  // the default's shapes with the grouped scale per weight (no GF; A/B)
+    const int v = a.M <= 32 ? 50 : (a.M <= 64 ? 52 : 53);
+    if (v == 50) return launch_mid<2, 8, 2, 1>(a, tiled, st, true);
+    if (v == 53) return launch_mid<2, 8, 4, 2>(a, tiled, st, true);
+    return launch_mid<2, 8, 2, 2>(a, tiled, st, true);
+  }
+#endif
   if (variant == 0) variant = a.M <= 32 ? 50 : (a.M <= 64 ? 52 : 53);
   switch (variant) {
     case 50: return launch_mid<2, 8, 2, 1>(a, tiled, st);
@@ -2915,8 +2946,10 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 // shapes the 64-row form (q / down: the mid kernel or 64-row tiles measured faster).
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out, int* mtw_out) {
   if (M <= 16 || M >= 256 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
-  // grouped scales cost the mid kernel ~1.4x (profiles/r02_ab_gemm_g128_mid.jsonl)
-  const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * (gpr != 1 ? 1.4 : 1.0);
+  // grouped scales cost the mid kernel ~1.4x (profiles/r02_ab_gemm_g128_mid.jsonl); ~1.1x since
+  // round 5 (parameters staged in LDS, the scale factored per k-step for g % 128 == 0:
+  // profiles/r05_ab_mid_gf.jsonl, q_proj g128 M = 128 mid 20.3 us vs the short split's 21.9)
+  const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * (gpr != 1 ? 1.1 : 1.0);
   if (mid_us < 24.0) return false;
   const int64_t nk = K / TK;
   const int64_t tiles128 = ((M + 127) / 128) * (N / TN);

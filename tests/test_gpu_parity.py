@@ -638,6 +638,34 @@ def test_gemv_identity_rows_give_w_deq(K, group, sym):
             assert torch.equal(y.view(torch.int16), want.view(torch.int16)), (v, tl)
 
 
+@pytest.mark.parametrize("M", [24, 48, 96])
+@pytest.mark.parametrize("group", [128, 64])
+def test_mid_m_identity_rows_give_w_deq(K, M, group):
+    """The mid-M kernel (17 <= M < 256 without a split workspace): X = rows of the identity gives
+    W_deq bit for bit -- with the group scale factored per 128-k step (g128) and per weight (g64),
+    and (A/B 56) the per-weight form at g128 within fp32 tolerance of the default."""
+    N, Kd = 512, 4096
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 67)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    ks = [(41 * i + 5) % Kd for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    for i, k in enumerate(ks):
+        x[i, k] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N)
+    assert torch.equal(y.view(torch.int16), want.view(torch.int16))
+    if AB and group == 128:
+        y56 = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(56))
+        assert torch.equal(y56.view(torch.int16), want.view(torch.int16))
+        xr = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+        ref = xr.float() @ r.out.float().t()
+        tol = 2e-3 * ref.abs() + 1e-3 * (xr.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+        for v in (0, 56):
+            yv = K.w4a16_gemm(xr, r.codes, r.scales, r.zeros, 4, group, N, flags=K.gemm_variant_flags(v))
+            assert bool(((yv.float() - ref).abs() <= tol).all()), v
+
+
 @pytest.mark.parametrize("Kd", [256, 1152, 4096])
 @pytest.mark.parametrize("M", [1, 16])
 def test_gemv_persistent_many_groups(K, Kd, M):
