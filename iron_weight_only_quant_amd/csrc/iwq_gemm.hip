@@ -421,49 +421,34 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
       for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
     }
   };
-  // the code prefetch first (DRAM: the longest latency); then the X image (XLDS) and the staged
-  // parameters (PST), their first XPRE / PRE chunks loaded into registers together before any is
-  // written, so their latencies overlap.  (Issuing X before the codes, so that its wait does not
+  // the code prefetch first (DRAM: the longest latency); then the staged parameters' first PRE
+  // chunks (PST) and the X image (XLDS).  (Issuing X before the codes, so that its wait does not
   // include them in vmcnt order, measured 4-7 % SLOWER on every shape: the codes' DRAM latency is
-  // the critical path, profiles/r05_gemv_grouped.jsonl.)
+  // the critical path.)
 #pragma unroll
   for (int u = 0; u < PF; ++u)
     if (u < nj) load(u, u);
-  constexpr int XPRE = 4, PRE = 4;
-  const int cpr = a.K / 8;                   // 16-B chunks per X row
-  const int nxc = XLDS ? a.M * cpr : 0;      // chunks of the X image
-  u32x4 xpre[XPRE];
+  constexpr int PRE = 4;
   // PST: after the X image (or at the start without one)
   uint32_t* pst = reinterpret_cast<uint32_t*>(dsm + (XLDS ? (a.M * xpitch + 15) / 16 * 16 : 0));
   const int np = PST ? T * 16 * a.gpr : 0;
   const int64_t pbase = (int64_t)blockIdx.x * np;
   uint32_t pre_s[PRE], pre_z[PRE];
-  if constexpr (XLDS) {
-#pragma unroll
-    for (int r = 0; r < XPRE; ++r) {
-      const int i = threadIdx.x + r * WPB * 64;
-      const int m = i / cpr, c = i - m * cpr;
-      xpre[r] = i < nxc ? *gp<u32x4>(a.x + (int64_t)m * a.lda + 8 * c) : u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  if constexpr (PST) pst_preload<PRE>(a, pbase, np, WPB * 64, pre_s, pre_z);
+  if constexpr (PST) pst_preload<PRE>(a, pbase, np, WPB * 64, pre_s, pre_z);  // before X's waits
   if constexpr (XLDS || PST) {
     if constexpr (XLDS) {
-      // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c
-      auto put = [&](int i, u32x4 d) {
-        const int m = i / cpr, c = i - m * cpr;
-        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
-                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
-        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
-      };
-#pragma unroll
-      for (int r = 0; r < XPRE; ++r) {
-        const int i = threadIdx.x + r * WPB * 64;
-        if (i < nxc) put(i, xpre[r]);
-      }
-      for (int i = threadIdx.x + XPRE * WPB * 64; i < nxc; i += WPB * 64) {  // long / many X rows
-        const int m = i / cpr, c = i - m * cpr;
-        put(i, *gp<u32x4>(a.x + (int64_t)m * a.lda + 8 * c));
+      // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c (load and store
+      // chunk by chunk: preloading the chunks first measured 3-4 % slower at M = 1 and 15 % at gate
+      // M = 4, per channel, profiles/r05_ab_gemv_xpre.jsonl)
+      const int cpr = a.K / 8;
+      for (int m = 0; m < a.M; ++m) {
+        const _Float16* xr = a.x + (int64_t)m * a.lda;
+        for (int c = threadIdx.x; c < cpr; c += WPB * 64) {
+          const u32x4 d = *gp<u32x4>(xr + 8 * c);
+          const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                            perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+          *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+        }
       }
     }
     if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, WPB * 64, pre_s, pre_z);

@@ -58,7 +58,12 @@ def main():
     ap.add_argument("--layouts", default="tiled,row")
     ap.add_argument("--rot-bytes", type=float, default=float(1 << 30))
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--lib", default="", help="A/B: load this libiwq.so build instead of the tree's")
+    ap.add_argument("--tag", default="", help="A/B: label added to every line")
     a = ap.parse_args()
+    if a.lib:
+        from iron_weight_only_quant_amd import _lib
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     from iron_weight_only_quant_amd import kernels
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
@@ -98,6 +103,8 @@ def main():
                            "hipblaslt_fp16_us": round(t_ref * 1e3, 2) if t_ref else None,
                            "speedup_vs_F_linear": round(t_ref / t, 3) if t_ref else None,
                            "max_abs_diff_vs_F_linear": err}
+                    if a.tag:
+                        rec["tag"] = a.tag
                     print(json.dumps(rec), flush=True)
         del rows, tiles, ref_w
         torch.cuda.empty_cache()
