@@ -41,9 +41,10 @@ __global__ __launch_bounds__(256) void k_zero_bytes(unsigned char* p, uint64_t n
   const uint64_t tail0 = head + body16 * 16;
   if (tail0 + t < n) p[tail0 + t] = 0;  // < 16 tail bytes
 }
-}  // namespace
 
-inline hipError_t zero_async(void* p, uint64_t n, hipStream_t st) {
+// in the same unnamed namespace as its kernel: each translation unit launches its own k_zero_bytes
+// (an inline function with external linkage would be one definition per TU of a different kernel)
+hipError_t zero_async(void* p, uint64_t n, hipStream_t st) {
   if (n == 0) return hipSuccess;
   unsigned char* c = static_cast<unsigned char*>(p);
   uint64_t head = (16 - (reinterpret_cast<uintptr_t>(c) & 15)) & 15;
@@ -55,6 +56,7 @@ inline hipError_t zero_async(void* p, uint64_t n, hipStream_t st) {
   hipLaunchKernelGGL(k_zero_bytes, dim3((unsigned)blocks), dim3(256), 0, st, c, n, head, body16);
   return hipGetLastError();
 }
+}  // namespace
 
 
 enum : int { DT_F16 = 0, DT_BF16 = 1, DT_F32 = 2 };

@@ -431,16 +431,43 @@ __device__ __forceinline__ FpParams bcast_fp_params(const FpParams& p, int k) {
   return q;
 }
 
+// E2M1 (the FP codec, bias 1: quant_linear.py:126-163 then :213-235) in closed form, two fp16
+// magnitudes a <= 6.0 per call (one per 16-bit half): the reference's encode-then-decode of |t| is
+//   a >= 1.0 : the binade of a with its one mantissa bit = (a's 10-bit mantissa > 256) -- RNE to one
+//              bit (the tie 256 goes to the even 0) with the no-carry clamp (768..1023 stay at .5);
+//              no fp16 input below 8 hits the torch.log2 quirk
+//   a <  1.0 : the subnormal 0.5 * clamp(rint(2 a), 0, 1) = 0.5 where a > 0.25, else 0
+// Checked against the exhaustive encode / decode fixtures (tests/golden/fp_small.npz, every fp16
+// magnitude <= 6: tests/test_cpu_host.py::test_e2m1_closed_form) and on the GPU bit for bit against
+// the table path.  Packed 16-bit ops: a + 0x7EFF (mantissa part) / a + 0x4400 / a + 0x4BFF set bit 15
+// exactly when the mantissa > 256 / a >= 0x3C00 / a > 0x3400 (no half overflows: a <= 0x4600).
+__device__ __forceinline__ uint32_t e2m1_mag2(uint32_t a) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 av = __builtin_bit_cast(u16x2, a);
+  const uint32_t mt = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a & 0x03FF03FFu) + (u16x2){0x7EFF, 0x7EFF});
+  const uint32_t nb = (a & 0x7C007C00u) | ((mt & 0x80008000u) >> 6);
+  const uint32_t ge1 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, av + (u16x2){0x4400, 0x4400}) >> (s16x2)15);
+  const uint32_t gtq = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, av + (u16x2){0x4BFF, 0x4BFF}) >> (s16x2)15);
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, nb & ge1),
+                                                               __builtin_bit_cast(u16x2, gtq & 0x38003800u)));
+}
+
 // k_fp_group with the decode table in LDS (no packed codes): 512-thread workgroups, each stages the
 // table (<= 48 KB for E4M3) once; finite groups take fp_pair_lut, the rest the exact ALU chain.
 // Group parameters are computed once per iteration of 4 units (g >= 32: lane l computes unit l % 4
 // of its group) and DPP-broadcast, as in k_group; GS = grid-stride walk (large single tensors).
-template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0>
+// E2A (E2M1 FP codec only, round 6): the table read replaced by the closed form of E2M1's decoded
+// magnitude (e2m1_mag2) -- no table is staged, so the workgroup starts streaming at once and LDS no
+// longer bounds the residency.
+// PF (single tensors, A/B round 6): the next iteration's loads issued before this one computes.
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false>
 __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
+  static_assert(!E2A || CODEC == CODEC_FP, "closed form: the FP codec's E2M1");
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
   __shared__ uint16_t tab_buf[120];
-  for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_QBLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
+  if constexpr (!E2A)
+    for (int32_t i = threadIdx.x; i < a.lut_n8 / 8; i += LUT_QBLOCK) lut_dyn[i] = gp<u32x4>(a.lut)[i];
   const Log2Tabs tabs = stage_log2_tables(tab_buf);  // its barrier also publishes the table
   lds_char* lut = (lds_char*)lut_dyn;
   constexpr int WPBL = LUT_QBLOCK / WAVE;
@@ -512,13 +539,21 @@ __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
         tb[j] = as_u32(__builtin_convertvector(pk_div_f16vals(__builtin_convertvector(d, f2), p.rs, p.s), h2));
         // 2|t| clamped to 2*bound: positive fp16 bit patterns order like their values and t is finite
         // (or +-inf) on a table group, so the clamp of t and the table byte offset are two packed ops
-        a2[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, tb[j]) << (u16x2)1,
-                                                                       bound2x));
+        if constexpr (E2A)  // |t| clamped to 6.0 (t finite or +-inf here): the fp16 bits of the magnitude
+          a2[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, tb[j] & 0x7FFF7FFFu),
+                                                                         (u16x2){0x4600, 0x4600}));
+        else
+          a2[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, tb[j]) << (u16x2)1,
+                                                                         bound2x));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const h2 rv = {*(lds_h*)(lut + (a2[j] & 0xFFFFu)), *(lds_h*)(lut + (a2[j] >> 16))};
-        r[j] = as_u32(rv);
+        if constexpr (E2A) {
+          r[j] = e2m1_mag2(a2[j]);
+        } else {
+          const h2 rv = {*(lds_h*)(lut + (a2[j] & 0xFFFFu)), *(lds_h*)(lut + (a2[j] >> 16))};
+          r[j] = as_u32(rv);
+        }
       }
       uint32_t cp[4];  // the codes of elements 2j, 2j+1 in the 16-bit halves of cp[j]
 #pragma unroll
@@ -558,17 +593,7 @@ __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
       }
     }
   };
-  while (u0 < cend) {
-    seek(u0);
-    const int32_t nu = (int32_t)min(min((int64_t)UNROLL, cend - u0), tnext - u0);
-    const int64_t eb = (u0 - tbeg) * UNIT + (int64_t)lane * 8;  // this lane's element in unit 0
-    Vec8<DT_F16> v[UNROLL];
-#pragma unroll
-    for (int k = 0; k < UNROLL; ++k) {
-      const int64_t e = eb + (int64_t)k * UNIT;
-      const bool ok = (k < nu) && e < tnumel;
-      v[k].load(tw + (ok ? e : 0) * F::BYTES);
-    }
+  auto compute_iter = [&](const Vec8<DT_F16> (&v)[UNROLL], int32_t nu, int64_t eb) {
     int32_t mn[UNROLL], mx[UNROLL];
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
@@ -600,12 +625,58 @@ __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
         }
       }
     }
+  };
+  auto load_iter = [&](int32_t nu, int64_t eb, Vec8<DT_F16> (&v)[UNROLL]) {
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) {
+      const int64_t e = eb + (int64_t)k * UNIT;
+      const bool ok = (k < nu) && e < tnumel;
+      v[k].load(tw + (ok ? e : 0) * F::BYTES);
+    }
+  };
+  auto advance = [&](int32_t nu) {
     u0 += nu;
     if constexpr (GS) {
       if (u0 >= cend) {
         u0 += (nwaves - 1) * UNROLL;
         cend = min(u0 + UNROLL, a.total_units);
       }
+    }
+  };
+  if constexpr (PF && !BATCHED) {
+    // the next iteration's loads in flight while this one computes (single tensors: the tensor
+    // descriptor never changes, so the loads need no seek)
+    if (u0 < cend) {
+      Vec8<DT_F16> vn[UNROLL];
+      int32_t nun = (int32_t)min((int64_t)UNROLL, cend - u0);
+      int64_t ebn = u0 * UNIT + (int64_t)lane * 8;
+      load_iter(nun, ebn, vn);
+      while (true) {
+        Vec8<DT_F16> v[UNROLL];
+#pragma unroll
+        for (int k = 0; k < UNROLL; ++k) v[k] = vn[k];
+        const int32_t nu = nun;
+        const int64_t eb = ebn;
+        advance(nu);
+        const bool more = u0 < cend;
+        if (more) {
+          nun = (int32_t)min((int64_t)UNROLL, cend - u0);
+          ebn = u0 * UNIT + (int64_t)lane * 8;
+          load_iter(nun, ebn, vn);
+        }
+        compute_iter(v, nu, eb);
+        if (!more) break;
+      }
+    }
+  } else {
+    while (u0 < cend) {
+      seek(u0);
+      const int32_t nu = (int32_t)min(min((int64_t)UNROLL, cend - u0), tnext - u0);
+      const int64_t eb = (u0 - tbeg) * UNIT + (int64_t)lane * 8;  // this lane's element in unit 0
+      Vec8<DT_F16> v[UNROLL];
+      load_iter(nu, eb, v);
+      compute_iter(v, nu, eb);
+      advance(nu);
     }
   }
   fp_flag_nan(a.nan_flag, any_nan);
@@ -882,12 +953,12 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, int G, bool SYM, int CODES = 0>
-hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
+template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool PF = false>
+hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
   // walk policy as k_group's single tensors: grid-stride at >= 2 grid rounds, else contiguous
-  auto kern = k_fp_group_lut<CODEC, G, SYM, false, false, CODES>;
-  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true, false, CODES>;
-  const size_t lds = (size_t)a.lut_n8 * 2;
+  auto kern = k_fp_group_lut<CODEC, G, SYM, false, false, CODES, E2A, PF>;
+  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true, false, CODES, E2A, PF>;
+  const size_t lds = E2A ? 0 : (size_t)a.lut_n8 * 2;
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_QBLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
   constexpr int WPBL = LUT_QBLOCK / WAVE;
@@ -899,6 +970,14 @@ hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
   if (gs) hipLaunchKernelGGL(kern_gs, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   return hipGetLastError();
+}
+// A/B (round 6): variant 3 = the next iteration's loads prefetched (PF); E2M1: 4 = PF + closed form
+template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false>
+hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
+#if IWQ_AB
+  if (a.variant == 3 || (E2A && a.variant == 4)) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, true>(a, st);
+#endif
+  return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false>(a, st);
 }
 
 template <int CODEC, int G, bool SYM>
@@ -930,18 +1009,27 @@ hipError_t launch_fp_lut_batched(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, bool SYM, int CODES = 0>
+template <int CODEC, bool SYM, int CODES = 0, bool E2A = false>
 hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
   switch (g) {
-    case 8: return launch_fp_lut_t<CODEC, 8, SYM, CODES>(a, st);
-    case 16: return launch_fp_lut_t<CODEC, 16, SYM, CODES>(a, st);
-    case 32: return launch_fp_lut_t<CODEC, 32, SYM, CODES>(a, st);
-    case 64: return launch_fp_lut_t<CODEC, 64, SYM, CODES>(a, st);
-    case 128: return launch_fp_lut_t<CODEC, 128, SYM, CODES>(a, st);
-    case 256: return launch_fp_lut_t<CODEC, 256, SYM, CODES>(a, st);
-    case 512: return launch_fp_lut_t<CODEC, 512, SYM, CODES>(a, st);
+    case 8: return launch_fp_lut_t<CODEC, 8, SYM, CODES, E2A>(a, st);
+    case 16: return launch_fp_lut_t<CODEC, 16, SYM, CODES, E2A>(a, st);
+    case 32: return launch_fp_lut_t<CODEC, 32, SYM, CODES, E2A>(a, st);
+    case 64: return launch_fp_lut_t<CODEC, 64, SYM, CODES, E2A>(a, st);
+    case 128: return launch_fp_lut_t<CODEC, 128, SYM, CODES, E2A>(a, st);
+    case 256: return launch_fp_lut_t<CODEC, 256, SYM, CODES, E2A>(a, st);
+    case 512: return launch_fp_lut_t<CODEC, 512, SYM, CODES, E2A>(a, st);
   }
   return hipErrorInvalidValue;
+}
+
+// E2M1 FP codec: the closed form (no table) -- A/B round 6: variant 1 forces it (4: with PF), 2 forces
+// the table
+template <bool SYM, int CODES>
+hipError_t launch_fp_e2m1(int64_t g, const FpArgs& a, hipStream_t st) {
+  if (a.variant == 2) return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
+  if (a.variant == 1 || a.variant == 4) return launch_fp_lut_g<CODEC_FP, SYM, CODES, true>(g, a, st);
+  return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
 }
 
 template <int G, int V>
@@ -980,13 +1068,16 @@ hipError_t launch_apx_double_lut(int64_t g, const FpArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpArgs& a, hipStream_t st) {
+  const bool e2m1 = codec == CODEC_FP && a.f.E == 2 && a.f.M == 1;
   if (a.lut && codes == 0) {
     if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true>(g, a, st);
     if (codec == CODEC_APX) return launch_fp_lut_g<CODEC_APX, true>(g, a, st);
+    if (e2m1) return sym ? launch_fp_e2m1<true, 0>(g, a, st) : launch_fp_e2m1<false, 0>(g, a, st);
     return sym ? launch_fp_lut_g<CODEC_FP, true>(g, a, st) : launch_fp_lut_g<CODEC_FP, false>(g, a, st);
   }
   if (a.lut) {  // codes re-encoded from the table's decoded values (code_of_value)
     if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true, 4>(g, a, st);
+    if (e2m1) return sym ? launch_fp_e2m1<true, 4>(g, a, st) : launch_fp_e2m1<false, 4>(g, a, st);
     if (codes == 4)
       return sym ? launch_fp_lut_g<CODEC_FP, true, 4>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 4>(g, a, st);
     return sym ? launch_fp_lut_g<CODEC_FP, true, 8>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 8>(g, a, st);
@@ -1107,6 +1198,7 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
     a.total_units = (a.numel + UNIT - 1) / UNIT;
     a.f = f;
     a.nan_flag = nan_flag;
+    a.variant = IWQ_AB ? (int32_t)((flags >> 16) & 0xFFu) : 0;  // A/B forms (E2M1: launch_fp_e2m1)
     if (lut) {
       if (!aligned16p(lut)) return IWQ_ERR_ARG;
       a.lut = static_cast<const uint16_t*>(lut);

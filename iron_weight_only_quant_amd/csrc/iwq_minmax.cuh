@@ -235,6 +235,15 @@ struct TensorCursor {
     if constexpr (BATCHED) {
       if (u >= next || next < 0) {
         const IWQ_GLOBAL iwq_batch_entry* tab = gp<iwq_batch_entry>(a.entries);
+        if (next < 0) {  // first seek: binary search (the last entry whose range starts at or before u)
+          int32_t lo = cur, hi = a.n_entries - 1;
+          while (lo < hi) {
+            const int32_t mid = (lo + hi + 1) >> 1;
+            if (tab[mid].unit_begin <= u) lo = mid;
+            else hi = mid - 1;
+          }
+          cur = lo;
+        }
         while (cur + 1 < a.n_entries && u >= tab[cur + 1].unit_begin) ++cur;
         cur = __builtin_amdgcn_readfirstlane(cur);
         t.w = rfl_ptr(tab[cur].w);
@@ -283,8 +292,17 @@ __device__ __forceinline__ void load_iter(const Iter& it, Vec8<DT> (&v)[UNROLL])
 // sized for full residency.
 // SKEL (roofline probe only, variant 118): the same walk, loads and 16-B stores with the arithmetic
 // removed (the input is copied to the output) -- this kernel's own memory stream as a ceiling.
+// PHASE (A/B, contiguous walk only): wave w starts its chunk at a wave-dependent iteration (a hash
+// of w) and wraps around to the chunk's start, so the waves do not sweep their chunks in lockstep
+// (without it every wave's address is congruent to the others' modulo the chunk length at every
+// moment).  PFD 2 (A/B): the loads of iteration i + 2 are in flight while iteration i is stored
+// (three register images).  RW > 1 (A/B, region walk): the units are cut into nwaves / RW
+// contiguous regions, RW consecutive waves share one and take its UNROLL-unit chunks round-robin
+// (RW = 1 is the contiguous walk, one region per wave; the grid-stride walk is one region for all) --
+// fewer distinct pages in flight at once.
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
-          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
+          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false, bool PHASE = false, int PFD = 0,
+          int RW = 1>
 __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * WAVES_PER_BLOCK + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -294,15 +312,39 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
   // UNROLL units (c*UNROLL for c = wave, wave + nwaves, ...: at any moment the grid works on one
   // contiguous window).  u0 = next unit, cend = end of the current chunk; u0 < cend <=> work left.
   int64_t u0, cend;
+  int64_t wrap_lo = 0, wrap_hi = 0;  // PHASE: the chunk's head, walked after its tail
+  int64_t rend = 0;                   // RW: end of this wave's region
   if constexpr (GS) {
     u0 = wave * UNROLL;
     cend = min(u0 + UNROLL, a.total_units);
+  } else if constexpr (RW > 1) {
+    const int64_t nreg = nwaves / RW;
+    const int64_t r = wave / RW;
+    int64_t per = (a.total_units + nreg - 1) / nreg;
+    per = (per + UNROLL - 1) / UNROLL * UNROLL;
+    const int64_t rbeg = r < nreg ? r * per : a.total_units;
+    rend = min(rbeg + per, a.total_units);
+    u0 = rbeg + (wave % RW) * UNROLL;
+    cend = min(u0 + UNROLL, rend);
   } else {
     int64_t per = (a.total_units + nwaves - 1) / nwaves;
     per = (per + UNROLL - 1) / UNROLL * UNROLL;
     u0 = wave * per;
     cend = min(u0 + per, a.total_units);
+    if constexpr (PHASE) {
+      if (u0 < cend) {
+        const int64_t nit = (cend - u0 + UNROLL - 1) / UNROLL;
+        const uint32_t h = (uint32_t)wave * 0x9E3779B1u;
+        const int64_t ph = (int64_t)((uint64_t)(h >> 8) % (uint64_t)nit) * UNROLL;
+        wrap_lo = u0;
+        wrap_hi = u0 + ph;
+        u0 += ph;
+      }
+    }
   }
+  bool any_nan = false;
+  TensorCursor<BATCHED> cursor;
+  cursor.init(a);
   auto advance = [&](int64_t n) {
     u0 += n;
     if constexpr (GS) {
@@ -311,10 +353,22 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
         cend = min(u0 + UNROLL, a.total_units);
       }
     }
+    if constexpr (RW > 1 && !GS) {
+      if (u0 >= cend) {
+        u0 += (RW - 1) * UNROLL;
+        cend = min(u0 + UNROLL, rend);
+      }
+    }
+    if constexpr (PHASE && !GS) {
+      if (u0 >= cend && wrap_hi > wrap_lo) {
+        u0 = wrap_lo;
+        cend = wrap_hi;
+        wrap_hi = wrap_lo;
+        cursor.cur = 0;  // the cursor only moves forward: search again from the first entry
+        cursor.next = BATCHED ? -1 : INT64_MAX;
+      }
+    }
   };
-  bool any_nan = false;
-  TensorCursor<BATCHED> cursor;
-  cursor.init(a);
   auto plan_iter = [&](int64_t u, Iter& it) {
     cursor.seek(a, u);
     const int64_t lim = min(cend, cursor.next);
@@ -350,7 +404,37 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
     flag_nan(a.nan_flag, false);
     return;
   }
-  if constexpr (PF) {
+  if constexpr (PFD == 2) {
+    // three register images: slot s is computed while slot (s + 2) % 3 loads
+    Iter it[3];
+    Vec8<DT> v[3][UNROLL];
+    bool has[3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      has[s] = u0 < cend;
+      if (has[s]) {
+        plan_iter(u0, it[s]);
+        load_iter<DT, UNROLL, NTL>(it[s], v[s]);
+        advance(it[s].n);
+      }
+    }
+    auto step = [&](auto S) -> bool {
+      constexpr int s = decltype(S)::value;
+      constexpr int l = (s + 2) % 3;
+      has[l] = u0 < cend;
+      if (has[l]) {
+        plan_iter(u0, it[l]);
+        load_iter<DT, UNROLL, NTL>(it[l], v[l]);
+        advance(it[l].n);
+      }
+      if (!has[s]) return false;
+      compute_iter(it[s], v[s]);
+      return true;
+    };
+    while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{}) &&
+           step(std::integral_constant<int, 2>{})) {
+    }
+  } else if constexpr (PF) {
     Iter itn;
     Vec8<DT> vn[UNROLL];
     plan_iter(u0, itn);
@@ -386,6 +470,11 @@ template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF 
           bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
   k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>(a);
+}
+// walk-order forms (A/B): PHASE / PFD as in k_group_body
+template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool SKEL, bool PHASE, int PFD, int RW = 1>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group_walk(GroupArgs a) {
+  k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, false, true, true, true, false, SKEL, PHASE, PFD, RW>(a);
 }
 // the same walk held to 64 VGPRs, i.e. 8 waves per SIMD (k_group needs 67-68 at fp16 g128: 7 waves)
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
@@ -1128,17 +1217,15 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   __syncthreads();
   // round 5: past the barrier no wave of this workgroup reads a granule any more -- count the
   // workgroup done; the LAST one zeroes the granules, the consensus word and the counter, so the next
-  // launch on the same workspace needs no memset (IWQ_FLAG_WS_ZEROED).  A relaxed increment is
-  // enough: wave 0's granule store, sweep loads and CAS all completed before the barrier (the loads
-  // and the CAS returned values that decided fin[]; the vector memory counter retires in order, so
-  // the earlier store was acknowledged too; the barrier's workgroup fences keep the compiler from
-  // hoisting the increment), and the last workgroup issues its clearing stores only after its
-  // increment returned the final count -- agent-scope atomics at the coherence point, so no clearing
-  // store overtakes a publish or a sweep.  The increment is issued here and its value used only at
-  // the end (clear_if_last), so its round trip overlaps this workgroup's output stores.
+  // launch on the same workspace needs no memset (IWQ_FLAG_WS_ZEROED).  The increment is made by the
+  // thread that published this workgroup's granule(s) and is acq_rel at agent scope: the release
+  // orders that publish before the count (on the abort path a workgroup may stop sweeping before its
+  // own granule is visible, so without it the publish could land after the last workgroup's clear),
+  // the acquire orders the last workgroup's clearing stores after every count.  Issued here, its
+  // value used only at the end (clear_if_last), so its round trip overlaps this workgroup's stores.
   unsigned long long done = 0;
   if (threadIdx.x == 0)
-    done = __hip_atomic_fetch_add(granules + (int)gridDim.x * KG + 1, 1ull, __ATOMIC_RELAXED,
+    done = __hip_atomic_fetch_add(granules + (int)gridDim.x * KG + 1, 1ull, __ATOMIC_ACQ_REL,
                                   __HIP_MEMORY_SCOPE_AGENT);
   auto clear_if_last = [&]() {
     if (threadIdx.x < 64) {

@@ -82,6 +82,12 @@ hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st, int max_blocks_p
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(BLOCK), 0, st, a);
   return hipGetLastError();
 }
+template <int UNROLL, bool SKEL, bool PHASE, int PFD, int RW = 1>
+hipError_t launch_walk_t(const GroupArgs& a, hipStream_t st) {
+  static int cache[64] = {0};
+  auto kern = k_group_walk<DT_F16, 128, false, 0, true, UNROLL, SKEL, PHASE, PFD, RW>;
+  return launch_persistent(kern, cache, UNROLL, a, st);
+}
 // Roofline probes (variants >= 100): the same bytes moved without arithmetic, to measure the
 // achievable HBM rate of a given access style on the box at hand.  Timing reference only.
 //   MODE 0: copy, nt load + nt store     MODE 1: copy, plain       MODE 2: copy, 4 x 16 B in flight/lane (nt)
@@ -199,6 +205,23 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 139: return launch_variant_t<1, false, true, true, true, true, true>(a, st);      // skeleton, grid-stride, 1 unit
     case 140: return launch_variant_t<2, false, true, true, true, true, true>(a, st);      // skeleton, grid-stride, 2 units
     case 141: return launch_variant_t<1, false, true, true, true, true>(a, st, 4);         // grid-stride, 1 unit, 4 waves
+    // walk order vs output placement (round 6, tools/ab_outplace.py): per-wave phase rotation,
+    // stores lagging the loads by two iterations, and their skeletons
+    case 142: return launch_walk_t<4, false, true, 0>(a, st);   // phase rotation
+    case 143: return launch_walk_t<4, false, false, 2>(a, st);  // loads of i + 2 in flight at the stores of i
+    case 144: return launch_walk_t<2, false, false, 2>(a, st);  // the same with 2-unit iterations
+    case 145: return launch_walk_t<2, false, true, 2>(a, st);   // both, 2-unit iterations
+    case 146: return launch_walk_t<4, true, true, 0>(a, st);    // skeleton of 142
+    case 147: return launch_walk_t<4, true, false, 2>(a, st);   // skeleton of 143
+    // region walks: RW consecutive waves share a contiguous region, chunks round-robin
+    case 148: return launch_walk_t<4, false, false, 0, 2>(a, st);
+    case 149: return launch_walk_t<4, false, false, 0, 4>(a, st);
+    case 150: return launch_walk_t<4, false, false, 0, 8>(a, st);
+    case 151: return launch_walk_t<4, false, false, 0, 16>(a, st);
+    case 152: return launch_walk_t<4, false, false, 0, 64>(a, st);
+    case 153: return launch_walk_t<4, true, false, 0, 8>(a, st);    // skeleton of 150
+    case 154: return launch_walk_t<4, true, false, 0, 64>(a, st);   // skeleton of 152
+    case 155: return launch_walk_t<4, false, false, 0, 256>(a, st);
     case 103: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 104: hipLaunchKernelGGL(k_probe<4>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 105: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 32)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();

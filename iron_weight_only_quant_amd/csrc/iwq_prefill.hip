@@ -2947,9 +2947,11 @@ bool prefill_split_preferred(int64_t M, int64_t N, int64_t K, int gpr, int group
 bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, int* ns_out, int* mtw_out) {
   if (M <= 16 || M >= 256 || !prefill_b32_supported(M, N, K, gpr, group)) return false;
   // grouped scales cost the mid kernel ~1.4x (profiles/r02_ab_gemm_g128_mid.jsonl); ~1.1x since
-  // round 5 (parameters staged in LDS, the scale factored per k-step for g % 128 == 0:
-  // profiles/r05_ab_mid_gf.jsonl, q_proj g128 M = 128 mid 20.3 us vs the short split's 21.9)
-  const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * (gpr != 1 ? 1.1 : 1.0);
+  // round 5 where the scale is factored per k-step, i.e. g % 128 == 0 (parameters staged in LDS:
+  // profiles/r05_ab_mid_gf.jsonl, q_proj g128 M = 128 mid 20.3 us vs the short split's 21.9); other
+  // groups (g = 64) still scale every weight: the measured 1.4x stands for them
+  const double gfac = gpr == 1 ? 1.0 : (group % 128 == 0 ? 1.1 : 1.4);
+  const double mid_us = (6.0 + 0.45e-6 * (double)((M + 63) / 64) * (double)N * (double)K) * gfac;
   if (mid_us < 24.0) return false;
   const int64_t nk = K / TK;
   const int64_t tiles128 = ((M + 127) / 128) * (N / TN);

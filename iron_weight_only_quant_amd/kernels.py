@@ -175,14 +175,17 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
             raise ValueError("packed codes need n_bits <= 8")
         codes = torch.empty(codes_nbytes(rows, cols, n_bits), dtype=torch.uint8, device=dev)
     nan_flag = _flags.take(dev)
+    # the caller's stream: the call and, if the one-pass hand-off aborts, its retry (settle() may run
+    # later under another current stream) both launch here -- the retry reuses this stream's workspace
+    cur_stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(cur_stream.cuda_stream)
 
     def call(ws, wsb):
         with L.on_device(dev):
             return lib.iwq_quantize_minmax(
                 L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group),
                 int(bool(symmetric)), int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols),
-                L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags),
-                L.stream_handle(dev))
+                L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(nan_flag), int(flags), sh)
     # the specialised kernels need no workspace; the C-ABI checks for one before launching anything,
     # so only the per-tensor and universal paths pay for the allocation (and a second call)
     st = call(None, 0)
@@ -209,15 +212,18 @@ def quantize_minmax(w: torch.Tensor, n_bits: int, group: int, symmetric: bool, q
         # per-tensor group is the whole tensor, so quant_dim does not change the walk; fp16, and bf16 /
         # fp32 without packed codes)
         if group == -1:
-            def retry():  # the one-pass hand-off aborted (QuantResult.settle): same call on the pair
-                flag2 = torch.zeros(1, dtype=torch.int32, device=dev)
+            def retry():  # the one-pass hand-off aborted (QuantResult.settle): same call on the pair,
+                # on the caller's stream (whose workspace it reuses), whatever stream settle() runs under
+                with torch.cuda.stream(cur_stream):
+                    flag2 = torch.zeros(1, dtype=torch.int32, device=dev)
                 with L.on_device(dev):
                     st2 = lib.iwq_quantize_minmax(
                         L.ptr(w), rows, cols, w.stride(0), L.DTYPE_CODE[w.dtype], int(n_bits), int(group),
                         int(bool(symmetric)), int(quant_dim), L.ptr(out), (out.stride(0) if out is not None else cols),
                         L.ptr(codes), L.ptr(scales), L.ptr(zeros), L.ptr(ws), wsb, L.ptr(flag2),
-                        (int(flags) & ~(0xFF << 16)) | _TENSOR_PAIR, L.stream_handle(dev))
+                        (int(flags) & ~(0xFF << 16)) | _TENSOR_PAIR, sh)
                 _raise_for(st2, "iwq_quantize_minmax")
+                cur_stream.synchronize()  # settle() reads flag2 from its own current stream
                 return flag2
     _raise_for(st, "iwq_quantize_minmax")
     return QuantResult(out, scales, zeros, codes, nan_flag, retry)

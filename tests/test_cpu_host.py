@@ -400,3 +400,23 @@ def test_trace_sections_cuts_a_kernel_trace_into_bench_regions(tmp_path):
     assert b["kernels"][1]["kernel"] == "k_tiny" and b["kernels"][1]["dispatches"] == 2
     assert b["bench"]["bench_ms_per_call_this_round"] == 0.0051  # median over the merged rounds
     assert abs(b["dominant_avg_over_bench"] - 5.0 / 5.1) < 1e-3
+
+
+def test_e2m1_closed_form():
+    """csrc/iwq_fp.hip e2m1_mag2: the E2M1 FP codec's encode-then-decode magnitude in closed form (the
+    table-free pack path) equals the reference's _float_to_fp / _fp_to_float (quant_linear.py:126-163,
+    213-235) on every fp16 magnitude the kernel can see (|t| clamped to fp_max = 6.0), per the
+    exhaustive fixtures tests/golden/make_golden.py wrote by importing the reference.  This restates
+    the kernel's packed 16-bit arithmetic lane by lane."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "fp_small.npz"))
+    x, enc, dec = d["in/all_fp16"], d["enc/e2m1"], d["dec/e2m1"]
+    a = x.view(np.uint16).astype(np.int64) & 0x7FFF
+    ref = np.abs(dec[enc].astype(np.float16)).view(np.uint16).astype(np.int64)
+    dom = a <= 0x4600
+    assert dom.sum() > 35000
+    mt = ((a & 0x3FF) + 0x7EFF) & 0xFFFF
+    nb = (a & 0x7C00) | ((mt & 0x8000) >> 6)
+    ge1 = np.where(((a + 0x4400) & 0x8000) != 0, 0xFFFF, 0)
+    gtq = np.where(((a + 0x4BFF) & 0x8000) != 0, 0xFFFF, 0)
+    got = np.maximum(nb & ge1, gtq & 0x3800)
+    assert np.array_equal(got[dom], ref[dom])

@@ -242,6 +242,46 @@ def test_bench_gpus2_spawns_ranks_and_rooted_gather_moves_each_byte_once():
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port" and "OPT-125M" in cpu["sample"]
 
 
+def test_bench_gpus8_dry_run_rehearses_the_eight_rank_path():
+    """The driver's N = 8 command form (`bench.py --gpus 8`, no WORLD_SIZE) on the CPU over gloo: 8
+    spawned ranks, 8 disjoint bins covering every weight, the rooted gather moving exactly the
+    non-root bins' packed bytes once, the scatter delivering every rank its own bin (checked on each
+    rank), and one per-rank roofline row with its own ceiling for each of the 8 ranks.  Its wall time is
+    recorded (the driver allows the 8-GPU bench 600 s)."""
+    import json
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--dry-run",
+                        "--model", "opt-125m"], capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    wall = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    shapes = shard.model_linear_shapes("opt-125m")
+    bins = shard.plan_shards(shapes, 8)
+    assert len(bins) == 8 and all(bins)
+    assert sorted(i for b in bins for i in b) == list(range(len(shapes)))
+    assert rec["world"] == 8 and rec["ranks"] == 8 and rec["tensors"] == 72 and rec["tensors_at_rank0"] == 72
+    per_rank = rec["plan_packed_bytes_per_rank"]
+    assert per_rank == [sum(shard.packed_nbytes(shapes[i][1], 4, 128, False) for i in b) for b in bins]
+    assert rec["gather_bytes_to_rank0"] == sum(per_rank[1:]) == rec["gather_sent_bytes"] == rec["gather_recv_bytes"]
+    assert rec["scatter_verified"] is True
+    lay = [shard.bin_layout(shapes, b)[1] for b in bins]
+    assert rec["scatter_bytes_from_rank0"] == 2 * sum(lay[1:])
+    roof = rec["roofline"]
+    assert [p["rank"] for p in roof["per_rank"]] == list(range(8))
+    assert all(p["ceiling_GBps"] > 0 and p["kernel_over_ceiling"] > 0 for p in roof["per_rank"])
+    assert roof["kernel_ms"] == 1.0 + 0.25 * 7 and roof["kernel_ms_basis"] == "max over ranks"
+    print(f"[8-rank dry run] wall {wall:.1f} s (driver limit 600 s)")
+    assert wall < 300
+
+
 def test_bench_world_size_must_match_gpus():
     import subprocess
     import sys

@@ -48,9 +48,12 @@ def _expected(codes_2d, scales, zeros, E, M):
     fp32 op, one rounding to fp16)."""
     bias, _ = FC.fp_params(E, M)
     dec = FC.fp_to_float(codes_2d, E, M, bias).astype(np.float16)
-    out = (dec * scales[:, None]).astype(np.float16)
-    if zeros is not None:
-        out = (out + zeros[:, None]).astype(np.float16)
+    # each op in fp32, then one rounding to fp16 (ATen's fp16 arithmetic, spelled out): products of
+    # large codes and 1e3 scales overflow fp16 to +-inf, which the kernels must give too
+    with np.errstate(over="ignore"):
+        out = (dec.astype(np.float32) * scales[:, None].astype(np.float32)).astype(np.float16)
+        if zeros is not None:
+            out = (out.astype(np.float32) + zeros[:, None].astype(np.float32)).astype(np.float16)
     return out
 
 
