@@ -572,6 +572,44 @@ def copy_ceiling(plan, steps=5, rounds=3):
     return {"GBps": max(forms.values()), "forms": forms}
 
 
+def fresh_ceiling(pairs=3, nbytes=1 << 30, steps=5, rounds=2):
+    """The box's copy rate on buffers that are NOT the plan's (box speed and the plan's
+    placement reported apart): `pairs` freshly allocated [n / 4096, 4096] fp16 inputs of `nbytes` each
+    (> the 256 MB MALL) with their own outputs, the guide's grid-stride 16-B copy (probe 100) and the
+    headline kernel's walk without arithmetic (118) on each; the best pair.  Round 6
+    (profiles/r06_ab_placement_2x2.jsonl): the same stream on two same-sized buffers of one box can
+    differ by 14 % (physical placement, read+write traffic only: read-only / write-only streams do
+    not), so one pair would be a draw, the best of several is the box."""
+    from iron_weight_only_quant_amd import kernels
+    stream = torch.cuda.current_stream()
+    rows = nbytes // (4096 * 2)
+    best, per_pair = {}, []
+    for i in range(pairs):
+        src = torch.empty(rows, 4096, dtype=torch.float16, device="cuda")
+        kernels.fill_synthetic(src, 7000 + i)
+        fp = kernels.BatchPlan([src], 4, 128, False)
+        row = {}
+        for v in (100, 118):
+            fp.run(stream, variant=v)
+            torch.cuda.synchronize()
+            for _ in range(rounds):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(steps):
+                    fp.run(stream, variant=v)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                gbs = rows * 4096 * 4 / (e0.elapsed_time(e1) / steps / 1e3) / 1e9
+                row[v] = max(row.get(v, 0.0), gbs)
+                best[v] = max(best.get(v, 0.0), gbs)
+        per_pair.append({CEILING_PROBES[v]: round(g, 1) for v, g in row.items()})
+        del fp, src
+    torch.cuda.empty_cache()
+    forms = {CEILING_PROBES[v]: round(g, 1) for v, g in best.items()}
+    return {"GBps": max(forms.values()), "forms": forms, "pairs": per_pair, "bytes_per_input": int(rows * 4096 * 2),
+            "basis": f"best of {pairs} fresh input/output pairs (not the plan's buffers)"}
+
+
 def launch_floor_us(reps=32):
     """Per-call device time of the smallest kernel of this library (iwq_fill_synthetic on 16
     elements: one wave, no memory traffic to speak of) in the same hipGraph replay form as the cold
@@ -1119,6 +1157,7 @@ def main():
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
     clock_ramp(plan, args.ramp_seconds)
     ceiling = copy_ceiling(plan)  # every rank: its own GPU's ceiling (roofline.per_rank)
+    fresh = fresh_ceiling()       # and the box's, on buffers that are not the plan's
     kernel_ms, ms_per_step = timed_steps(plan, args, ws_n, stream)
 
     other = None
@@ -1147,6 +1186,12 @@ def main():
         traffic, traffic_src = None, ("the committed PMC record is the 1-GPU workload's; at N > 1 every rank runs "
                                       "a different bin (profiles/traffic.json: +0.07 % over algorithmic at N = 1)")
     roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched>", traffic, traffic_src, ceiling, other)
+    fresh_g = gather_per_rank([fresh["GBps"]], ws_n)
+    roofline["fresh_ceiling"] = fresh if ws_n == 1 else {**fresh, "GBps_per_rank": [round(f[0], 1) for f in fresh_g]}
+    if roofline.get("achieved"):
+        lo = min(f[0] for f in fresh_g)
+        roofline["kernel_over_fresh_ceiling"] = round(roofline["achieved"] / lo, 4)
+        roofline["plan_ceiling_over_fresh_ceiling"] = round(min(p[2] for p in per_rank) / lo, 4)
 
     if ws_n > 1 and not args.no_collectives and not args.scatter:
         # bounded: the headline model's fp16 weights scattered from rank 0 (its own buffers are freed

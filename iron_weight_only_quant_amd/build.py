@@ -38,7 +38,19 @@ def _stale(ab=False):
         return True
     t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, d) for d in DEPS] + [os.path.join(HERE, "..", "include", "iwq.h")]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    if any(os.path.getmtime(d) > t for d in deps if os.path.exists(d)):
+        return True
+    # a source edited while a build was running is older than the library that build linked, but
+    # newer than the object compiled from its previous text: compare objects with their sources too
+    out_dir = AB_OUT_DIR if ab else OUT_DIR
+    headers = [os.path.join(CSRC, d) for d in DEPS if d not in SOURCES] + [os.path.join(HERE, "..", "include", "iwq.h")]
+    newest_header = max(os.path.getmtime(h) for h in headers if os.path.exists(h))
+    for src in SOURCES:
+        obj = os.path.join(out_dir, os.path.splitext(src)[0] + ".o")
+        if os.path.exists(obj) and (os.path.getmtime(obj) < os.path.getmtime(os.path.join(CSRC, src))
+                                    or os.path.getmtime(obj) < newest_header):
+            return True
+    return False
 
 
 def build_library(force=False, verbose=True, ab=None):

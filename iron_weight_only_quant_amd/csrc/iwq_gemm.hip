@@ -322,6 +322,60 @@ __global__ __launch_bounds__(WAVES * 64) void k_w4a16_decode(GemmArgs a) {
 //     column tile are summed through LDS in k-split order (deterministic).
 // ---------------------------------------------------------------------------------------------
 constexpr int XLDS_MAX = 64 * 1024;  // dynamic LDS per workgroup for the X image (2+ workgroups per CU)
+// Round 6, batched decode (M = 8..16): where the grid is at most one workgroup per CU (q / o / down
+// shapes, N / 16 <= 256 column tiles; the fused q/k/v at CT 4) the X image may take most of the CU's
+// LDS -- 16 rows of K = 4096 are 128 KiB -- instead of being re-read from L2 at every k-step (the
+// ring form below 64 KiB); staged with XB rows of loads in flight per thread.
+constexpr int XLDS_BIG = 150 * 1024;
+inline int gemm_cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+// the X image of M rows into LDS, pre-permuted to the nibble-pair order (chunk c of row m at
+// dsm + m * xpitch + 16 c); XB > 1: XB rows' loads issued before their stores
+template <int XB>
+__device__ __forceinline__ void stage_x(const GemmArgs& a, uint8_t* dsm, int xpitch, int nthr) {
+  const int cpr = a.K / 8;
+  if constexpr (XB <= 1) {
+    // load and store chunk by chunk: preloading the chunks first measured 3-4 % slower at M = 1 and
+    // 15 % at gate M = 4, per channel (profiles/r05_ab_gemv_xpre.jsonl)
+    for (int m = 0; m < a.M; ++m) {
+      const _Float16* xr = a.x + (int64_t)m * a.lda;
+      for (int c = threadIdx.x; c < cpr; c += nthr) {
+        const u32x4 d = *gp<u32x4>(xr + 8 * c);
+        const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
+                          perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
+        *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
+      }
+    }
+  } else {
+    for (int m0 = 0; m0 < a.M; m0 += XB) {
+      for (int c = threadIdx.x; c < cpr; c += nthr) {
+        u32x4 d[XB];
+#pragma unroll
+        for (int r = 0; r < XB; ++r) {
+          const int m = m0 + r < a.M ? m0 + r : a.M - 1;
+          d[r] = *gp<u32x4>(a.x + (int64_t)m * a.lda + 8 * c);
+        }
+#pragma unroll
+        for (int r = 0; r < XB; ++r) {
+          if (m0 + r < a.M) {
+            const u32x4 pd = {perm(d[r].z, d[r].x, 0x05040100u), perm(d[r].z, d[r].x, 0x07060302u),
+                              perm(d[r].w, d[r].y, 0x05040100u), perm(d[r].w, d[r].y, 0x07060302u)};
+            *reinterpret_cast<u32x4*>(dsm + (m0 + r) * xpitch + 16 * c) = pd;
+          }
+        }
+      }
+    }
+  }
+}
 // grouped decode (round 5): the (s, z) rows of np / gpr consecutive columns starting at parameter
 // index pbase, staged as one dword per group (s | z << 16), rows padded to gpr + 1 dwords.  The first
 // PRE chunks per thread are loaded by pst_preload (issued together with the X image's loads) and
@@ -374,7 +428,7 @@ __device__ __forceinline__ void pst_store(const GemmArgs& a, uint32_t* pst, int6
 // acc += s_g * step -- the PC numerics per group, y = RN16(sum_g s_g sum_{k in g} x (q - z) + b)
 // (A = I still gives W_deq exactly), 16 fewer VALU per k-step than RN16((q - z) s) per weight.
 template <int PF, int S, int T, bool XLDS, int PROBE = 0, bool TILED = false, bool PC = false, bool PST = false,
-          bool GF = false>
+          bool GF = false, int XB = 1>
 __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   static_assert(!PST || !PC, "staged parameters: grouped weights only");
   constexpr int WPB = S * T;
@@ -436,21 +490,8 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
   uint32_t pre_s[PRE], pre_z[PRE];
   if constexpr (PST) pst_preload<PRE>(a, pbase, np, WPB * 64, pre_s, pre_z);  // before X's waits
   if constexpr (XLDS || PST) {
-    if constexpr (XLDS) {
-      // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c (load and store
-      // chunk by chunk: preloading the chunks first measured 3-4 % slower at M = 1 and 15 % at gate
-      // M = 4, per channel, profiles/r05_ab_gemv_xpre.jsonl)
-      const int cpr = a.K / 8;
-      for (int m = 0; m < a.M; ++m) {
-        const _Float16* xr = a.x + (int64_t)m * a.lda;
-        for (int c = threadIdx.x; c < cpr; c += WPB * 64) {
-          const u32x4 d = *gp<u32x4>(xr + 8 * c);
-          const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
-                            perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
-          *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
-        }
-      }
-    }
+    // 16-B chunk c of X row m -> permuted (0,4,1,5,2,6,3,7) at dsm + m*xpitch + 16c
+    if constexpr (XLDS) stage_x<XB>(a, dsm, xpitch, WPB * 64);
     if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, WPB * 64, pre_s, pre_z);
     __syncthreads();
   }
@@ -545,7 +586,8 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
 // tiles (CT code loads per k-step, CT accumulators), so X traffic per code byte drops CT-fold.
 // Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits
 // (GF: the grouped scale factored per k-step, as k_w4a16_gemv's PM 2).
-template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false, bool GF = false, bool PST = false>
+template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false, bool GF = false, bool PST = false,
+          int XB = 1>
 __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   static_assert(!PST || !PC, "staged parameters: grouped weights only");
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
@@ -607,18 +649,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   uint32_t pre_s[PRE], pre_z[PRE];
   if constexpr (PST) pst_preload<PRE>(a, pbase, np, S * 64, pre_s, pre_z);
   if constexpr (XLDS || PST) {
-    if constexpr (XLDS) {
-      const int cpr = a.K / 8;
-      for (int m = 0; m < a.M; ++m) {
-        const _Float16* xr = a.x + (int64_t)m * a.lda;
-        for (int c = threadIdx.x; c < cpr; c += S * 64) {
-          const u32x4 d = *gp<u32x4>(xr + 8 * c);
-          const u32x4 pd = {perm(d.z, d.x, 0x05040100u), perm(d.z, d.x, 0x07060302u),
-                            perm(d.w, d.y, 0x05040100u), perm(d.w, d.y, 0x07060302u)};
-          *reinterpret_cast<u32x4*>(dsm + m * xpitch + 16 * c) = pd;
-        }
-      }
-    }
+    if constexpr (XLDS) stage_x<XB>(a, dsm, xpitch, S * 64);
     if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, S * 64, pre_s, pre_z);
     __syncthreads();
   }
@@ -725,19 +756,28 @@ inline int gemv_auto_ct(int64_t M, int64_t N, int64_t K) {
   return 1;
 }
 
-template <int PF, int S, int CT, bool TILED>
+template <int PF, int S, int CT, bool TILED, bool BIGX = false>
 void launch_gemv_ct(const GemmArgs& a, hipStream_t st, bool allow_pc = true, bool allow_gf = true) {
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * CT));
   const size_t red = (size_t)S * CT * 256 * 4;
   const bool pc = a.gpr == 1 && allow_pc;
   const bool gf = !pc && allow_gf && a.group % BK == 0;  // the grouped scale factored per k-step
+  // BIGX: the large image where the grid is at most one workgroup per CU (XLDS_BIG)
+  const int64_t xmax = (BIGX && (int64_t)blocks <= gemm_cu_count()) ? XLDS_BIG : XLDS_MAX;
   // grouped + gf: the CT tiles' parameter rows staged after the X image (PST)
-  const bool xl = xbytes <= XLDS_MAX;
+  const bool xl = xbytes <= xmax;
   const int64_t pend = (xl ? (xbytes + 15) / 16 * 16 : 0) + (int64_t)16 * CT * (a.gpr + 1) * 4;
-  const bool pst = gf && pend <= PST_LDS_MAX;
+  const bool pst = gf && pend <= (BIGX ? xmax + 16 * 1024 : PST_LDS_MAX);
   const size_t ldsp0 = red > (size_t)pend ? red : (size_t)pend;
-  if (xl) {
+  if (xl && BIGX && xbytes > XLDS_MAX) {
+    const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, true, false, false, 8>), dim3(blocks), dim3(S * 64), lds, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, false, true, true, 8>), dim3(blocks), dim3(S * 64), ldsp, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, false, true, false, 8>), dim3(blocks), dim3(S * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, false, false, false, 8>), dim3(blocks), dim3(S * 64), lds, st, a);
+  } else if (xl) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
     const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, true, TILED, true>), dim3(blocks), dim3(S * 64), lds, st, a);
@@ -752,7 +792,7 @@ void launch_gemv_ct(const GemmArgs& a, hipStream_t st, bool allow_pc = true, boo
   }
 }
 
-template <int PF, int S, int T, int PROBE = 0, bool TILED = false>
+template <int PF, int S, int T, int PROBE = 0, bool TILED = false, bool BIGX = false>
 // pm (grouped weights): 0 = parameters per k-step from global memory, scale per weight (the form
 // before round 5), 1 = staged in LDS (PST) when they fit beside X, 2 = PST + the scale factored per
 // k-step (GF, where every k-step lies in one group; also without PST when X is not staged)
@@ -761,13 +801,23 @@ void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds, bool allow_p
   const unsigned blocks = (unsigned)(a.N / (16 * T));
   const size_t red = (size_t)S * T * 256 * 4;
   const bool pc = a.gpr == 1 && PROBE == 0 && allow_pc;
+  // BIGX: the large image where the grid is at most one workgroup per CU (XLDS_BIG)
+  const int64_t xmax = (BIGX && (int64_t)blocks <= gemm_cu_count()) ? XLDS_BIG : XLDS_MAX;
   // grouped: the staged parameters (PST) after the X image, 16 T rows of gpr + 1 dwords
-  const bool xl = allow_lds && xbytes <= XLDS_MAX;
+  const bool xl = allow_lds && xbytes <= xmax;
   const int64_t pend = (xl ? (xbytes + 15) / 16 * 16 : 0) + (int64_t)16 * T * (a.gpr + 1) * 4;
-  const bool pst = !pc && PROBE == 0 && pm > 0 && pend <= PST_LDS_MAX;
+  const bool pst = !pc && PROBE == 0 && pm > 0 && pend <= (BIGX ? xmax + 16 * 1024 : PST_LDS_MAX);
   const bool gf = !pc && PROBE == 0 && pm == 2 && a.group % BK == 0;  // every k-step inside one group
   const size_t ldsp0 = red > (size_t)pend ? red : (size_t)pend;
-  if (xl) {
+  if (xl && BIGX && xbytes > XLDS_MAX) {
+    const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
+    const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
+    if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, true, false, false, 8>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    else if (pst && gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, true, true, 8>), dim3(blocks), dim3(S * T * 64), ldsp, st, a);
+    else if (pst) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, true, false, 8>), dim3(blocks), dim3(S * T * 64), ldsp, st, a);
+    else if (gf) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, false, true, 8>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+    else hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, false, false, false, 8>), dim3(blocks), dim3(S * T * 64), lds, st, a);
+  } else if (xl) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
     const size_t ldsp = lds > (size_t)pend ? lds : (size_t)pend;
     if (pc) hipLaunchKernelGGL((k_w4a16_gemv<PF, S, T, true, PROBE, TILED, true>), dim3(blocks), dim3(S * T * 64), lds, st, a);
@@ -1472,6 +1522,16 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false, false); break;
       case 27: launch_gemv<2, 8, 1, 0, true>(a, st, true, true, 0); break;  // grouped: params per step, global
       case 28: launch_gemv<2, 8, 1, 0, true>(a, st, true, true, 1); break;  // grouped: staged, scale per weight
+      case 29:  // round 6: the default's kernels with the large X image (XLDS_BIG) where it applies
+        if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true, true>(a, st);
+        else if (ct == 2) launch_gemv_ct<3, 8, 2, true, true>(a, st);
+        else if (gemv_long_k(M, K)) launch_gemv<2, 16, 1, 0, true, true>(a, st, true);
+        else launch_gemv<2, 8, 1, 0, true, true>(a, st, true);
+        break;
+      case 30:  // the same with the 16-way k-split (more waves per CU to stage and stream)
+        if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 16, 4, true, true>(a, st);
+        else launch_gemv<2, 16, 1, 0, true, true>(a, st, true);
+        break;
 #endif
       default:
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);

@@ -1017,7 +1017,9 @@ __global__ __launch_bounds__(BLOCK) void k_tensor_apply(const char* w, char* out
 //     them are published and this sweep ends (bounded; a second give-up -- not reachable while
 //     stores become visible -- sets nan_flag bit 2: outputs invalid).
 // On ABORT no byte of any output is written and nan_flag bit 1 is set, so the host can re-run the
-// same call on the two-kernel pair, IN PLACE too: the input is untouched.
+// same call on the two-kernel pair, IN PLACE too: the input is untouched.  Round 6: with outputs that
+// cannot alias the input, a completed sweep goes without the CAS (the CAS decides only give-ups); an
+// ABORT then may leave some outputs written, which the host's re-run on the pair overwrites.
 // ---------------------------------------------------------------------------------------------
 constexpr int OP_THR = 512;
 constexpr uint32_t OP_SPIN_LIMIT = 1u << 22;
@@ -1117,7 +1119,21 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
       __hip_atomic_store(granules + blockIdx.x, ((unsigned long long)tag << 32) | keys, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the publish is acknowledged at agent scope before this thread issues anything else -- in
+    // particular before its done-counter increment below (a workgroup that gives up its
+    // sweep early must not let its publish land after the last workgroup's clearing stores).  A wait,
+    // not a release fence: the granules are agent-scope atomic stores, there is no cached data to
+    // write back, and the wait sits where this wave waits for the other publishes anyway.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  // Round 6: when the outputs cannot alias the input (out of place -- pseudo_quantize_tensor's
+  // default -- or codes / parameters only) a workgroup whose sweep saw every granule goes WITHOUT the
+  // consensus compare-and-swap (one agent-scope round trip less on the hand-off's critical path):
+  // if another workgroup gives up, it still CASes ABORT and sets nan_flag bit 1, and the host re-runs
+  // the call on the pair, which rewrites every output from the untouched input.  In place, the CAS
+  // protocol stands (an input overwritten by a GO-er could not be re-read by the retry).
+  const int64_t tbytes = nvec * VB;
+  const bool alias = out != nullptr && out < w + tbytes && w < out + tbytes;
   if (wv == 0) {
     // sweep every workgroup's granule(s) until all carry the tag (relaxed agent-scope loads bypass L1)
     const int ng = (int)gridDim.x * KG;
@@ -1187,9 +1203,10 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
     };
     // spin_limit 0 (test-only variant 9): every workgroup gives up, so the launch ABORTs
     bool timed_out = sweep(spin_limit) || spin_limit == 0;
-    // one outcome for the whole launch: the first CAS on the consensus word decides
-    unsigned long long decided = 0;
-    if (lane == 0) {
+    // one outcome for the whole launch: the first CAS on the consensus word decides (in place, or
+    // after a give-up; out of place a completed sweep is its own decision)
+    unsigned long long decided = (!alias && !timed_out) ? OP_GO : 0;
+    if (lane == 0 && decided == 0) {
       unsigned long long expect = 0;
       const unsigned long long want = timed_out ? OP_ABORT : OP_GO;
       decided = __hip_atomic_compare_exchange_strong(granules + ng, &expect, want, __ATOMIC_RELAXED,
@@ -1218,14 +1235,14 @@ __global__ __launch_bounds__(OP_THR) void k_tensor_onepass(const char* w, char* 
   // round 5: past the barrier no wave of this workgroup reads a granule any more -- count the
   // workgroup done; the LAST one zeroes the granules, the consensus word and the counter, so the next
   // launch on the same workspace needs no memset (IWQ_FLAG_WS_ZEROED).  The increment is made by the
-  // thread that published this workgroup's granule(s) and is acq_rel at agent scope: the release
-  // orders that publish before the count (on the abort path a workgroup may stop sweeping before its
-  // own granule is visible, so without it the publish could land after the last workgroup's clear),
-  // the acquire orders the last workgroup's clearing stores after every count.  Issued here, its
-  // value used only at the end (clear_if_last), so its round trip overlaps this workgroup's stores.
+  // thread that published this workgroup's granule(s), after its explicit wait for that publish's
+  // acknowledgement (above), so every publish is performed before its workgroup's count; the last
+  // workgroup issues its clearing stores only once its increment has returned the final count (a
+  // data dependency on an agent-scope atomic).  Issued here, its value used only at the end
+  // (clear_if_last), so its round trip overlaps this workgroup's output stores.
   unsigned long long done = 0;
   if (threadIdx.x == 0)
-    done = __hip_atomic_fetch_add(granules + (int)gridDim.x * KG + 1, 1ull, __ATOMIC_ACQ_REL,
+    done = __hip_atomic_fetch_add(granules + (int)gridDim.x * KG + 1, 1ull, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
   auto clear_if_last = [&]() {
     if (threadIdx.x < 64) {

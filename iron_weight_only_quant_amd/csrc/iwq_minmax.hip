@@ -222,6 +222,12 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 153: return launch_walk_t<4, true, false, 0, 8>(a, st);    // skeleton of 150
     case 154: return launch_walk_t<4, true, false, 0, 64>(a, st);   // skeleton of 152
     case 155: return launch_walk_t<4, false, false, 0, 256>(a, st);
+    case 156: return launch_walk_t<4, false, false, 0, 128>(a, st);
+    case 157: return launch_walk_t<4, false, false, 0, 512>(a, st);
+    case 158: return launch_walk_t<4, false, false, 0, 1024>(a, st);
+    case 159: return launch_walk_t<4, false, false, 0, 2048>(a, st);
+    case 160: return launch_walk_t<4, true, false, 0, 256>(a, st);   // skeleton of 155
+    case 161: return launch_walk_t<2, false, false, 0, 256>(a, st);  // 2-unit chunks
     case 103: hipLaunchKernelGGL(k_probe<3>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 104: hipLaunchKernelGGL(k_probe<4>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 105: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 32)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();

@@ -898,9 +898,11 @@ def test_per_tensor_fast_path(K, dtype):
 def test_per_tensor_onepass_timeout_retry(K):
     """A one-pass hand-off that gives up (test-only variant 9: every granule sweep gives up at once,
     as it would with workgroups held off the CUs by another stream) ABORTS the launch through the
-    consensus word: nan_flag bit 1, and NOT ONE output byte written.  has_nan() then re-runs the call
-    on the two-kernel form into the same outputs -- out of place and IN PLACE (the input is untouched)
-    -- bit-exact vs the oracle.  QuantLinear(w_group_size=-1) settles the same way."""
+    consensus word: nan_flag bit 1, and in place NOT ONE byte written (out of place, round 6, a
+    workgroup whose sweep completed may go without the consensus; here every sweep gives up, so none
+    does).  has_nan() then re-runs the call on the two-kernel form into the same outputs -- out of place
+    and IN PLACE (the input is untouched) -- bit-exact vs the oracle.  QuantLinear(w_group_size=-1)
+    settles the same way."""
     x = synth(56, (1536, 2048), "float16")
     exp = O.quantlinear_int(x, 4, -1, False, 0, "float16")
     # out of place

@@ -19,7 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 SHAPES = {"q_proj": (4096, 4096), "gate_proj": (11008, 4096), "down_proj": (4096, 11008),
-          "70b_gate": (28672, 8192), "70b_down": (8192, 28672), "70b_q": (8192, 8192)}
+          "70b_gate": (28672, 8192), "70b_down": (8192, 28672), "70b_q": (8192, 8192),
+          "qkv_fused": (12288, 4096), "gate_up_fused": (22016, 4096)}
 
 
 def graph_time(calls, rounds=5):
@@ -88,6 +89,7 @@ def main():
                 t_ref = graph_time([(lambda wt=wt: torch.nn.functional.linear(x, wt)) for wt in ref_w])
             for layout in a.layouts.split(","):
                 srcs = tiles if layout == "tiled" else rows
+                y0 = None
                 for v in [int(t) for t in a.variants.split(",")]:
                     fl = kernels.gemm_variant_flags(v)
                     mk = lambda c: (lambda: kernels.w4a16_gemm(x, c, r.scales, r.zeros, 4, a.group, N, flags=fl,
@@ -95,6 +97,9 @@ def main():
                     mk(srcs[0])()
                     torch.cuda.synchronize()
                     err = float((y.float() - want).abs().max())
+                    if y0 is None:
+                        y0 = y.clone()
+                    same = bool(torch.equal(y.view(torch.int16), y0.view(torch.int16)))
                     t = graph_time([mk(c) for c in srcs])
                     rec = {"shape": name, "N": N, "K": K, "M": M, "group": a.group, "layout": layout,
                            "variant": v, "copies": len(srcs), "us": round(t * 1e3, 2),
@@ -102,7 +107,7 @@ def main():
                            "frac_of_8TBps": round(wbytes / t / 1e6 / 8000, 3),
                            "hipblaslt_fp16_us": round(t_ref * 1e3, 2) if t_ref else None,
                            "speedup_vs_F_linear": round(t_ref / t, 3) if t_ref else None,
-                           "max_abs_diff_vs_F_linear": err}
+                           "max_abs_diff_vs_F_linear": err, "bits_equal_first_variant": same}
                     if a.tag:
                         rec["tag"] = a.tag
                     print(json.dumps(rec), flush=True)
