@@ -481,7 +481,7 @@ def dry_run(args, ws_n, rank):
     alg = numel * 4 + (numel // args.group) * 2 * (1 if args.symmetric else 2)
     ceil = 5000.0 - 100.0 * rank  # stand-in: each rank's own in-run copy ceiling
     per_rank = gather_per_rank([kernel_ms, alg, ceil], ws_n)
-    roof = roofline_record(per_rank, "k_group<f16,128,asym,batched>", None, "dry run: no PMC",
+    roof = roofline_record(per_rank, "k_group<f16,128,asym,batched,RW256>", None, "dry run: no PMC",
                            {"GBps": ceil, "forms": {"stand-in": ceil}})
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -1095,7 +1095,7 @@ def model70b_section(args, ws_n, rank, steps=5, warmup=2):
                       f"INT{args.bits} g={args.group} {'sym' if args.symmetric else 'asym'}, in place",
             "value": round(total * 2 / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
             "steps": steps, "warmup": warmup, "fp16_weights_total": total, "scaling": "strong",
-            "roofline": roofline_record(per_rank, "k_group<f16,128,asym,batched> in place", traffic, src)}
+            "roofline": roofline_record(per_rank, "k_group<f16,128,asym,batched,RW256> in place", traffic, src)}
 
 
 def build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, roofline, extra):
@@ -1185,7 +1185,7 @@ def main():
     else:
         traffic, traffic_src = None, ("the committed PMC record is the 1-GPU workload's; at N > 1 every rank runs "
                                       "a different bin (profiles/traffic.json: +0.07 % over algorithmic at N = 1)")
-    roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched>", traffic, traffic_src, ceiling, other)
+    roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched,RW256>", traffic, traffic_src, ceiling, other)
     fresh_g = gather_per_rank([fresh["GBps"]], ws_n)
     roofline["fresh_ceiling"] = fresh if ws_n == 1 else {**fresh, "GBps_per_rank": [round(f[0], 1) for f in fresh_g]}
     if roofline.get("achieved"):

@@ -735,6 +735,238 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   }
 }
 
+// k_w4a16_gemv_ks (round 6): batched decode, 8 <= M <= 16, where X (M x K fp16) outgrows the LDS
+// image and every workgroup would otherwise re-read all of it from L2 -- at M = 16 the X bytes a CU
+// reads per call are 4x its code bytes (7B down_proj: 352 KiB of X per 16-column tile; the whole
+// call 90 MB of L2 traffic against 22.5 MB of codes).  The K range is split over KS workgroups per CT
+// column tiles: each stages its X SLICE (M x K / KS) in LDS once, streams its k-steps with
+// k_w4a16_gemv_ct's inner loop (wave w: the slice's k-steps w, w + S, ...), sums its S waves' partial
+// tiles in LDS in wave order and writes one fp32 slab ws[ks][m][n]; k_gemv_ks_reduce then sums the
+// KS slabs in ks order, applies the per-channel scale and the bias and rounds to fp16 once --
+// deterministic, X traffic / KS, one extra launch.  Per-channel numerics as PC (y = RN16(s sum x (q - z)
+// + b)), grouped as GF (acc += s_g step); X = rows of the identity still gives W_deq bit for bit.
+template <int PF, int S, int CT, bool TILED, bool PC = false, bool GF = false, bool PST = false>
+__global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ks(GemmArgs a, float* ws, int KS) {
+  static_assert(!PST || !PC, "staged parameters: grouped weights only");
+  extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int q = lane >> 4, r16 = lane & 15;
+  const int cg = blockIdx.x / KS, ksi = blockIdx.x - (blockIdx.x / KS) * KS;
+  const int tile0 = cg * CT;
+  const int nks = a.K / BK;
+  const int k0 = (int)((int64_t)nks * ksi / KS), k1 = (int)((int64_t)nks * (ksi + 1) / KS);
+  const int nkr = k1 - k0;
+  const int nj = nkr > wv ? (nkr - wv + S - 1) / S : 0;  // steps of this wave: kt = k0 + wv + j S
+  const int64_t crow = a.K / 2;
+  const int arow = r16 < a.M ? r16 : a.M - 1;
+  const int xpitch = nkr * BK * 2 + 16;
+  const int64_t tstride = TILED ? (int64_t)nks * 1024 : 16 * crow;
+  const uint8_t* cbase = TILED ? a.codes + (int64_t)tile0 * tstride + lane * 16
+                               : a.codes + (int64_t)(tile0 * 16 + r16) * crow + q * 16;
+  constexpr bool perch = PC;
+  _Float16 zz0[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int n = (tile0 + c) * 16 + r16;
+    zz0[c] = perch ? (a.zeros ? gp<_Float16>(a.zeros)[n] : (_Float16)a.zsym) : (_Float16)0.f;
+  }
+  const h2 k1024 = h2{(_Float16)1024.0f, (_Float16)1024.0f}, k64 = h2{(_Float16)64.0f, (_Float16)64.0f};
+  u32x4 bc[PF][CT];
+  _Float16 sv[PF][CT], zv[PF][CT];
+  auto load = [&](int j, int u) {
+    const int kt = k0 + wv + j * S;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+      bc[u][c] = __builtin_nontemporal_load(gp<u32x4>(cbase + c * tstride + kt * (TILED ? 1024 : BK / 2)));
+    if (!perch && !PST) {
+      const int kk = kt * BK + 32 * q;
+      const int gk = a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int64_t gi = (int64_t)((tile0 + c) * 16 + r16) * a.gpr + gk;
+        sv[u][c] = gp<_Float16>(a.scales)[gi];
+        zv[u][c] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
+      }
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < nj) load(u, u);
+  // the X slice (permuted as the image of k_w4a16_gemv), then the staged parameters (PST)
+  constexpr int PRE = 4;
+  uint32_t* pst = reinterpret_cast<uint32_t*>(dsm + (a.M * xpitch + 15) / 16 * 16);
+  const int np = PST ? CT * 16 * a.gpr : 0;
+  const int64_t pbase = (int64_t)tile0 * 16 * a.gpr;
+  uint32_t pre_s[PRE], pre_z[PRE];
+  if constexpr (PST) pst_preload<PRE>(a, pbase, np, S * 64, pre_s, pre_z);
+  {
+    const int cpr = nkr * (BK / 8);  // 16-B chunks per row of the slice
+    for (int m0 = 0; m0 < a.M; m0 += 8) {
+      for (int c = threadIdx.x; c < cpr; c += S * 64) {
+        u32x4 d[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int m = m0 + r < a.M ? m0 + r : a.M - 1;
+          d[r] = *gp<u32x4>(a.x + (int64_t)m * a.lda + (int64_t)k0 * BK + 8 * c);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          if (m0 + r < a.M) {
+            const u32x4 pd = {perm(d[r].z, d[r].x, 0x05040100u), perm(d[r].z, d[r].x, 0x07060302u),
+                              perm(d[r].w, d[r].y, 0x05040100u), perm(d[r].w, d[r].y, 0x07060302u)};
+            *reinterpret_cast<u32x4*>(dsm + (m0 + r) * xpitch + 16 * c) = pd;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (PST) pst_store<PRE>(a, pst, pbase, np, S * 64, pre_s, pre_z);
+  __syncthreads();
+  const uint8_t* xsrow = dsm + arow * xpitch + 64 * q;
+  const DqConst dq;
+  f4 acc[CT], accs[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) acc[c] = accs[c] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nj; j0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int j = j0 + u;
+      if (j >= nj) break;
+      const int kt = k0 + wv + j * S;
+      h2 s2[CT], z1024[CT], z64[CT];
+      float sf[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        h2 z2;
+        if constexpr (PST) {
+          const int kk = kt * BK + 32 * q;
+          const uint32_t sz = pst[(c * 16 + r16) * (a.gpr + 1) + (a.gshift >= 0 ? (kk >> a.gshift) : kk / a.group)];
+          s2[c] = as_h2(__builtin_amdgcn_perm(sz, sz, 0x01000100u));
+          z2 = as_h2(__builtin_amdgcn_perm(sz, sz, 0x03020302u));
+          sf[c] = (float)__builtin_bit_cast(_Float16, (uint16_t)(sz & 0xFFFFu));
+        } else {
+          s2[c] = perch ? h2{(_Float16)0.f, (_Float16)0.f} : h2{sv[u][c], sv[u][c]};
+          z2 = perch ? h2{zz0[c], zz0[c]} : h2{zv[u][c], zv[u][c]};
+          sf[c] = perch ? 0.f : (float)sv[u][c];
+        }
+        z1024[c] = z2 + k1024;
+        z64[c] = z2 + k64;
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const h8 af = *reinterpret_cast<const h8*>(xsrow + (kt - k0) * (BK * 2) + 16 * s);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          if constexpr (GF)
+            accs[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq),
+                                                             s == 0 ? f4{0.f, 0.f, 0.f, 0.f} : accs[c], 0, 0, 0);
+          else
+            acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                af, PC ? dequant8_ns(bc[u][c][s], z1024[c], z64[c], dq) : dequant8(bc[u][c][s], z1024[c], z64[c], s2[c], dq),
+                acc[c], 0, 0, 0);
+        }
+      }
+      if constexpr (GF) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[c][e] = __builtin_fmaf(sf[c], accs[c][e], acc[c][e]);
+      }
+      if (j + PF < nj) load(j + PF, u);
+    }
+  }
+  __syncthreads();  // the X slice and parameters are dead: the LDS now holds the waves' partial tiles
+  float* red = reinterpret_cast<float*>(dsm);  // [S][CT][256]
+#pragma unroll
+  for (int c = 0; c < CT; ++c) *reinterpret_cast<f4*>(red + (wv * CT + c) * 256 + lane * 4) = acc[c];
+  __syncthreads();
+  float* slab = ws + (int64_t)ksi * a.M * a.N;
+  for (int o = threadIdx.x; o < CT * 256; o += S * 64) {
+    const int c = o >> 8, e = o & 255;
+    const int ln = e >> 2, reg = e & 3;
+    const int row = 4 * (ln >> 4) + reg, col = (tile0 + c) * 16 + (ln & 15);
+    if (row < a.M) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < S; ++k) v += red[(k * CT + c) * 256 + e];
+      slab[(int64_t)row * a.N + col] = v;
+    }
+  }
+}
+
+// the KS fp32 slabs of k_w4a16_gemv_ks summed in ks order, per-channel scale (PC) and bias, one
+// rounding to fp16; 4 consecutive columns per thread (N % 16 == 0)
+template <bool PC>
+__global__ __launch_bounds__(256) void k_gemv_ks_reduce(GemmArgs a, const float* ws, int KS) {
+  const int64_t total = (int64_t)a.M * a.N, n4 = total / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f4 v = *gp<f4>(ws + 4 * i);
+    for (int k = 1; k < KS; ++k) {
+      const f4 t = *gp<f4>(ws + (int64_t)k * total + 4 * i);
+      v = v + t;
+    }
+    const int64_t e0 = 4 * i;
+    const int row = (int)(e0 / a.N), col = (int)(e0 - (int64_t)row * a.N);
+    _Float16* yr = a.y + (int64_t)row * a.ldy + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float r = v[j];
+      if constexpr (PC) r = opaque(r * (float)gp<_Float16>(a.scales)[col + j]);  // no fma_mix fold
+      if (a.bias) r += (float)gp<_Float16>(a.bias)[col + j];
+      gp<_Float16>(yr)[j] = (_Float16)r;
+    }
+  }
+}
+
+// The K-split decode plan: 8 <= M <= 16, X over the 64 KiB image budget; CT 4 column tiles per
+// workgroup, KS the smallest power of two whose X slice fits 80 KiB (two workgroups per CU) and whose
+// grid covers the CUs.  Returns false where the one-launch kernels keep X resident.
+inline bool gemv_ks_plan(int64_t M, int64_t N, int64_t K, int* ct_out, int* ks_out) {
+  if (M < 8 || M > 16 || N % 64 != 0 || K % BK != 0) return false;
+  if (M * (2 * K + 16) <= XLDS_MAX) return false;
+  const int64_t nks = K / BK, groups = N / 64;
+  for (int ks = 2; ks <= 16; ks *= 2) {
+    const int64_t steps = (nks + ks - 1) / ks;
+    if (steps < 8) return false;  // at least one k-step per wave
+    if (M * (steps * BK * 2 + 16) > 80 * 1024) continue;
+    if (groups * ks < gemm_cu_count() && ks < 16) continue;
+    if (ct_out) *ct_out = 4;
+    if (ks_out) *ks_out = ks;
+    return true;
+  }
+  return false;
+}
+constexpr bool GEMV_KS_DEFAULT = false;
+inline int64_t gemv_ks_bytes(int64_t M, int64_t N, int64_t K) {
+  int ks = 0;
+  return gemv_ks_plan(M, N, K, nullptr, &ks) ? (int64_t)ks * M * N * 4 : 0;
+}
+
+template <int PF, int S, bool TILED>
+void launch_gemv_ks(const GemmArgs& a, hipStream_t st, float* ws, int KS) {
+  constexpr int CT = 4;
+  const int nks = a.K / BK;
+  const int smax = (nks + KS - 1) / KS;
+  const int64_t xbytes = ((int64_t)a.M * (smax * BK * 2 + 16) + 15) / 16 * 16;
+  const unsigned blocks = (unsigned)(a.N / (16 * CT) * KS);
+  const size_t red = (size_t)S * CT * 256 * 4;
+  const bool pc = a.gpr == 1;
+  const bool gf = !pc && a.group % BK == 0;
+  const int64_t pend = xbytes + (int64_t)16 * CT * (a.gpr + 1) * 4;
+  const bool pst = gf && pend <= 96 * 1024;
+  const size_t lds = red > (size_t)(pst ? pend : xbytes) ? red : (size_t)(pst ? pend : xbytes);
+  if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ks<PF, S, CT, TILED, true>), dim3(blocks), dim3(S * 64), lds, st, a, ws, KS);
+  else if (pst) hipLaunchKernelGGL((k_w4a16_gemv_ks<PF, S, CT, TILED, false, true, true>), dim3(blocks), dim3(S * 64), lds, st, a, ws, KS);
+  else if (gf) hipLaunchKernelGGL((k_w4a16_gemv_ks<PF, S, CT, TILED, false, true>), dim3(blocks), dim3(S * 64), lds, st, a, ws, KS);
+  else hipLaunchKernelGGL((k_w4a16_gemv_ks<PF, S, CT, TILED>), dim3(blocks), dim3(S * 64), lds, st, a, ws, KS);
+  const int64_t n4 = (int64_t)a.M * a.N / 4;
+  int64_t rb = (n4 + 255) / 256;
+  if (rb > 1024) rb = 1024;
+  if (pc) hipLaunchKernelGGL(k_gemv_ks_reduce<true>, dim3((unsigned)rb), dim3(256), 0, st, a, ws, KS);
+  else hipLaunchKernelGGL(k_gemv_ks_reduce<false>, dim3((unsigned)rb), dim3(256), 0, st, a, ws, KS);
+}
+
 // Column tiles per wave for the decode default (cold sweep, profiles/r01_gemv_ct.jsonl): X traffic
 // only matters from M = 4 on, and a CT-fold smaller grid must still cover the chip: CT = 4 when that
 // leaves >= 256 workgroups (or >= 160 at M >= 8: 7B gate/up), CT = 2 for >= 256 workgroups once M*K
@@ -1373,6 +1605,7 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
 
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (M <= 16) return gemv_ks_bytes(M, N, K);  // the K-split decode's slabs (round 6), where planned
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
   if (g <= 0 || K % g != 0) return 0;
   int ns = 0, mtw = 2;
@@ -1493,6 +1726,22 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     }
     return IWQ_OK;
   }
+  // the K-split decode (round 6, k_w4a16_gemv_ks) where planned and the caller gave its workspace;
+  // GEMV_KS_DEFAULT decides whether the default takes it (A/B variant 31 forces it, 32 refuses it)
+  int ks_ct = 0, ks_n = 0;
+  const bool ks_ok = M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC) && (variant == 0 || variant == 31 || variant == 32) &&
+                     gemv_ks_plan(M, N, K, &ks_ct, &ks_n) && workspace &&
+                     workspace_bytes >= gemv_ks_bytes(M, N, K) && (variant == 31 || (variant == 0 && GEMV_KS_DEFAULT));
+  if (ks_ok) {
+    if (flags & IWQ_FLAG_TILED_CODES) launch_gemv_ks<2, 8, true>(a, st, static_cast<float*>(workspace), ks_n);
+    else launch_gemv_ks<2, 8, false>(a, st, static_cast<float*>(workspace), ks_n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
+  }
   if (flags & IWQ_FLAG_TILED_CODES) {  // decode tile layout: the weight-streaming kernel only
     if (M > 16) return IWQ_ERR_ARG;
     switch (variant) {  // same shapes as the row-major variants of the same number (A/B)
@@ -1537,7 +1786,10 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, true>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, true>(a, st);
         else if (gemv_long_k(M, K)) launch_gemv<2, 16, 1, 0, true>(a, st, true);
-        else launch_gemv<2, 8, 1, 0, true>(a, st, true);
+        // round 6: the large X image where the one-tile grid is at most one workgroup per CU (M >= 8
+        // on K = 4096: q / o; variant 29 vs the ring, cold, profiles/r06_gemv_bigx.jsonl: M = 16 per
+        // channel 6.84 -> 6.49 us, g128 7.60 -> 6.91; M = 8 g128 6.28 -> 5.84, per channel +2 %)
+        else launch_gemv<2, 8, 1, 0, true, true>(a, st, true);
         break;
     }
   } else if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
@@ -1577,7 +1829,7 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
         if (const int ct = gemv_auto_ct(M, N, K); ct == 4) launch_gemv_ct<1, 8, 4, false>(a, st);
         else if (ct == 2) launch_gemv_ct<3, 8, 2, false>(a, st);
         else if (gemv_long_k(M, K)) launch_gemv<2, 16, 1>(a, st, true);
-        else launch_gemv<2, 8, 1>(a, st, true);
+        else launch_gemv<2, 8, 1, 0, false, true>(a, st, true);  // (the large X image, as tiled)
         break;
     }
   } else if (((variant == 0 && !split_pref && !short_pref &&

@@ -467,9 +467,9 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
 }
 
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool PF = false, bool NTL = true,
-          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false>
+          bool NTS = true, bool SHARED = true, bool GS = false, bool SKEL = false, int RW = 1>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) void k_group(GroupArgs a) {
-  k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>(a);
+  k_group_body<DT, G, SYM, CODES, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL, false, 0, RW>(a);
 }
 // walk-order forms (A/B): PHASE / PFD as in k_group_body
 template <int DT, int G, bool SYM, int CODES, bool BATCHED, int UNROLL, bool SKEL, bool PHASE, int PFD, int RW = 1>

@@ -33,8 +33,13 @@ namespace {
 
 // Walk policy, picked by cold in-run A/B (tools/ab_single.py rotating over >= 1 GB of distinct
 // tensors, bench.py --variants; profiles/r01_ab_*):
-//  * whole-model batched walk (hundreds of iterations per wave): contiguous chunk per wave, no
-//    prefetch (grid-stride: 4.68 vs 4.40 ms per 7B);
+//  * whole-model batched walk (hundreds of iterations per wave): no prefetch (grid-stride: 4.68 vs
+//    4.40 ms per 7B); round 6: the REGION walk, 256 consecutive waves share one contiguous region and
+//    take its 4-unit chunks round-robin (RW = 256: 32 regions at 8192 waves), instead of one contiguous
+//    chunk per wave -- +1...+3.5 % on every output placement measured, most where the placement is
+//    slow (tools/ab_outplace.py, profiles/r06_ab_outplace_regions.jsonl / r06_ab_outplace_rw.jsonl:
+//    per-tensor outputs 0.759 -> 0.764 / 0.735 -> 0.749, in place 0.735 -> 0.748 / 0.741 -> 0.750,
+//    one packed arena 0.629 -> 0.647 / 0.631 -> 0.649; same bits, checked on every weight);
 //  * single fp16 tensors of >= 2 grid-rounds (11008x4096: 34.3 vs 36.8 us): grid-stride chunks;
 //  * smaller single tensors (4096x4096, ~1 round): contiguous chunk with the next iteration's
 //    loads prefetched (14.2 vs 15.1 us).
@@ -50,11 +55,13 @@ hipError_t launch_persistent(Kern kern, int* cache, int unroll, const GroupArgs&
   return hipGetLastError();
 }
 
+constexpr int BATCH_RW = 256;  // the batched walk's waves per region (k_group_body RW)
 template <int DT, int G, bool SYM, int CODES, bool BATCHED>
 hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
   constexpr int UNROLL = 4;
   static int cache[64] = {0};
-  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ true>;
+  auto kern = k_group<DT, G, SYM, CODES, BATCHED, UNROLL, /*PF*/ !BATCHED, /*NTL*/ true, /*NTS*/ true,
+                      /*SHARED*/ true, /*GS*/ false, /*SKEL*/ false, /*RW*/ BATCHED ? BATCH_RW : 1>;
   if constexpr (!BATCHED && DT == DT_F16) {
     static int cache_gs[64] = {0};
     auto kern_gs = k_group<DT, G, SYM, CODES, false, UNROLL, /*PF*/ false, /*NTL*/ true, /*NTS*/ true,
@@ -69,10 +76,10 @@ hipError_t launch_group_t(const GroupArgs& a, hipStream_t st) {
 // Tuning variants of the headline configuration (fp16, g=128, asymmetric, no codes, batched),
 // selected by flags bits 16..23 for in-process A/B timing (bench.py --variants).
 template <int UNROLL, bool PF, bool NTL, bool NTS, bool SHARED = true, bool GS = false, bool SKEL = false,
-          bool BATCHED = true>
+          bool BATCHED = true, int RW = 1>
 hipError_t launch_variant_t(const GroupArgs& a, hipStream_t st, int max_blocks_per_cu = 8) {
   static int cache[64] = {0};
-  auto kern = k_group<DT_F16, 128, false, 0, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL>;
+  auto kern = k_group<DT_F16, 128, false, 0, BATCHED, UNROLL, PF, NTL, NTS, SHARED, GS, SKEL, RW>;
   const int64_t waves_needed = (a.total_units + UNROLL - 1) / UNROLL;
   int64_t blocks = (waves_needed + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
   const int per_cu = resident_blocks_per_cu(kern, cache);
@@ -160,7 +167,8 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 100: hipLaunchKernelGGL(k_probe<0>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 101: hipLaunchKernelGGL(k_probe<1>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
     case 102: hipLaunchKernelGGL(k_probe<2>, dim3((unsigned)(device_cu_count() * 8)), dim3(BLOCK), 0, st, a.entries, a.n_entries, a.nan_flag); return hipGetLastError();
-    case 118: return launch_variant_t<4, false, true, true, true, false, true>(a, st);  // default walk, no arithmetic
+    case 118:  // the default (region) walk, no arithmetic
+      return launch_variant_t<4, false, true, true, true, false, true, true, BATCH_RW>(a, st);
   }
 #if IWQ_AB
   switch (v) {
@@ -175,7 +183,8 @@ hipError_t launch_variant(int v, const GroupArgs& a, hipStream_t st) {
     case 9: return launch_variant_t<4, false, true, true>(a, st, 7);            // default kernel, 7 waves/SIMD
     case 10: return launch_variant_t<4, false, true, true>(a, st, 6);           // default kernel, 6 waves/SIMD
     case 11: return launch_variant_t<4, false, true, true>(a, st, 4);           // default kernel, 4 waves/SIMD
-    case 12: return launch_variant_t<4, false, true, true>(a, st, 8);           // default kernel (same as 0)
+    case 12: return launch_variant_t<4, false, true, true>(a, st, 8);           // the contiguous walk (r1-r5 default)
+    case 163: return launch_variant_t<4, false, true, true, true, false, true>(a, st);  // skeleton of 12
     case 13: return launch_variant_t<4, false, true, false>(a, st);             // default walk, plain stores
     case 14: return launch_variant_t<4, false, false, false>(a, st);            // plain loads + plain stores
     // memory-stream probes on the same skeleton (no arithmetic): which walk moves the bytes fastest

@@ -605,7 +605,8 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
         raise ValueError(f"w4a16_gemm: NIB-layout codes need M >= {NIB_MIN_M} rows, got {M}")
     with L.on_device(x.device):
         # the size depends on the CU count of the device it is queried on: ask x's device
-        ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if not tiled else 0
+        # (M <= 16: the K-split decode's fp32 slabs where it applies, tile layout or row-major)
+        ws_bytes = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group))) if (not tiled or M <= 16) else 0
         v = (int(flags) >> 16) & 0xFF
         if 81 < v < 96 and N % 256 == 0:
             ws_bytes = max(ws_bytes, ((M + 255) // 256) * (N // 256) * (v - 80) * 65536 * 4)

@@ -638,6 +638,74 @@ def test_gemv_identity_rows_give_w_deq(K, group, sym):
             assert torch.equal(y.view(torch.int16), want.view(torch.int16)), (v, tl)
 
 
+@pytest.mark.parametrize("group", [128, -2])
+@pytest.mark.parametrize("M", [8, 16])
+def test_gemv_large_x_image_identity_and_reference(K, group, M):
+    """Round 6: M >= 8 on K = 4096 stages the whole X (M x 8 KiB > the 64 KiB ring budget) in LDS when
+    the one-tile grid is at most one workgroup per CU (XLDS_BIG): X = rows of the identity still gives
+    W_deq bit for bit (row-major and tile layout), random X stays within the fp32-GEMM tolerance, and
+    the tile layout is bit-identical to the row-major codes."""
+    N, Kd = 512, 4096
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 68)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    tiled = K.tile_codes(r.codes, N, Kd)
+    ks = [(257 * i + 9) % Kd for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    for i, k in enumerate(ks):
+        x[i, k] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    for codes, tl in ((r.codes, False), (tiled, True)):
+        y = K.w4a16_gemm(x, codes, r.scales, r.zeros, 4, group, N, tiled=tl)
+        assert torch.equal(y.view(torch.int16), want.view(torch.int16)), tl
+    xr = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = xr.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (xr.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    y0 = K.w4a16_gemm(xr, r.codes, r.scales, r.zeros, 4, group, N, b)
+    y1 = K.w4a16_gemm(xr, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True)
+    assert bool(((y0.float() - ref).abs() <= tol).all())
+    assert torch.equal(y0.view(torch.int16), y1.view(torch.int16))
+    if AB:  # the ring form (X from L2 per k-step, variant 2's kernels) gives the same bits
+        y2 = K.w4a16_gemm(xr, tiled, r.scales, r.zeros, 4, group, N, b, tiled=True, flags=K.gemm_variant_flags(13))
+        assert bool(((y2.float() - ref).abs() <= tol).all())
+
+
+@pytest.mark.parametrize("Kd", [4096, 11008])
+@pytest.mark.parametrize("group", [128, -2])
+@pytest.mark.parametrize("M", [8, 16])
+def test_gemv_ksplit_identity_and_reference(K, Kd, group, M):
+    """Round 6, the K-split decode (k_w4a16_gemv_ks + k_gemv_ks_reduce: KS workgroups per 64 columns,
+    each with its X slice in LDS, fp32 slabs summed in ks order by the reduce): on the q_proj / down_proj
+    shapes X = rows of the identity gives W_deq bit for bit and random X stays within the fp32-GEMM
+    tolerance, through the default dispatch (row-major and tile layout, bit-identical to each other)
+    and, in A/B builds, forced (31) and refused (32)."""
+    N = 4096
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 69)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    tiled = K.tile_codes(r.codes, N, Kd)
+    ks = [(263 * i + 11) % Kd for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    for i, k in enumerate(ks):
+        x[i, k] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    xr = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = xr.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (xr.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (0,) + abv(31, 32):
+        fl = K.gemm_variant_flags(v)
+        outs = []
+        for codes, tl in ((r.codes, False), (tiled, True)):
+            y = K.w4a16_gemm(x, codes, r.scales, r.zeros, 4, group, N, tiled=tl, flags=fl)
+            assert torch.equal(y.view(torch.int16), want.view(torch.int16)), (v, tl)
+            yr = K.w4a16_gemm(xr, codes, r.scales, r.zeros, 4, group, N, b, tiled=tl, flags=fl)
+            assert bool(((yr.float() - ref).abs() <= tol).all()), (v, tl, float((yr.float() - ref).abs().max()))
+            outs.append(yr)
+        assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16)), v
+
+
 @pytest.mark.parametrize("M", [24, 48, 96])
 @pytest.mark.parametrize("group", [128, 64])
 def test_mid_m_identity_rows_give_w_deq(K, M, group):

@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 
 
 # copy probes and arithmetic-free skeletons (iwq_minmax.hip launch_variant): not quantizers
-NON_QUANTIZING = set(range(100, 128)) | {133, 134, 135, 139, 140, 146, 147, 153, 154, 160}
+NON_QUANTIZING = set(range(100, 128)) | {133, 134, 135, 139, 140, 146, 147, 153, 154, 160, 163}
 
 
 def main():

@@ -64,14 +64,14 @@ for s in "${STEPS[@]}"; do
       step pmc_write 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/${T}pmc_write" -o run -- python3 "$ROOT/bench.py" $HEAD
       cd "$ROOT"
       step traffic 60 python3 tools/pmc_traffic.py "$OUT/${T}pmc_fetch" "$OUT/${T}pmc_write" --numel 6476005376 \
-        --kernel "k_group<0, 128, false, 0, true, 4, false, true, true, true, false, false>" -o "$OUT/${T}traffic.json" ;;
+        --kernel "k_group<0, 128, false, 0, true, 4, false, true, true, true, false, false, 256>" -o "$OUT/${T}traffic.json" ;;
     pmc70)
       cd /tmp
       step pmc70_fetch 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/${T}pmc70_fetch" -o run -- python3 "$ROOT/bench.py" --model llama2-70b $HEAD
       step pmc70_write 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/${T}pmc70_write" -o run -- python3 "$ROOT/bench.py" --model llama2-70b $HEAD
       cd "$ROOT"
       step traffic70 60 python3 tools/pmc_traffic.py "$OUT/${T}pmc70_fetch" "$OUT/${T}pmc70_write" --numel 68451041280 \
-        --kernel "k_group<0, 128, false, 0, true, 4, false, true, true, true, false, false>" --placement in-place -o "$OUT/${T}traffic_70b.json" ;;
+        --kernel "k_group<0, 128, false, 0, true, 4, false, true, true, true, false, false, 256>" --placement in-place -o "$OUT/${T}traffic_70b.json" ;;
     pmcsq)
       cd /tmp
       step pmc_sq 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/${T}pmc_sq" -o run -- python3 "$ROOT/bench.py" $HEAD
