@@ -544,7 +544,7 @@ def clock_ramp(plan, seconds):
 CEILING_PROBES = {100: "copy, nt 16-B load + nt store, grid-stride",
                   101: "copy, plain 16-B load + store, grid-stride",
                   102: "copy, 4 x 16 B in flight per lane (nt), grid-stride",
-                  118: "k_group's own walk and load/store stream, no arithmetic (same grid, same units)"}
+                  118: "k_group's own (region) walk and load/store stream, no arithmetic (same grid, same units)"}
 
 
 def copy_ceiling(plan, steps=5, rounds=3):
@@ -572,42 +572,38 @@ def copy_ceiling(plan, steps=5, rounds=3):
     return {"GBps": max(forms.values()), "forms": forms}
 
 
-def fresh_ceiling(pairs=3, nbytes=1 << 30, steps=5, rounds=2):
+def fresh_ceiling(plan, steps=5, rounds=2):
     """The box's copy rate on buffers that are NOT the plan's (box speed and the plan's
-    placement reported apart): `pairs` freshly allocated [n / 4096, 4096] fp16 inputs of `nbytes` each
-    (> the 256 MB MALL) with their own outputs, the guide's grid-stride 16-B copy (probe 100) and the
-    headline kernel's walk without arithmetic (118) on each; the best pair.  Round 6
-    (profiles/r06_ab_placement_2x2.jsonl): the same stream on two same-sized buffers of one box can
-    differ by 14 % (physical placement, read+write traffic only: read-only / write-only streams do
-    not), so one pair would be a draw, the best of several is the box."""
+    placement reported apart): a fresh input and output allocated for every weight of the plan (the
+    same shapes, the same number of allocations -- a single large buffer is its own placement draw,
+    profiles/r06_ab_placement_2x2.jsonl), timed with the guide's grid-stride 16-B copy (probe 100)
+    and the headline kernel's walk without arithmetic (118).  The contents are never read as
+    numbers, so the buffers are left unfilled."""
     from iron_weight_only_quant_amd import kernels
     stream = torch.cuda.current_stream()
-    rows = nbytes // (4096 * 2)
-    best, per_pair = {}, []
-    for i in range(pairs):
-        src = torch.empty(rows, 4096, dtype=torch.float16, device="cuda")
-        kernels.fill_synthetic(src, 7000 + i)
-        fp = kernels.BatchPlan([src], 4, 128, False)
-        row = {}
-        for v in (100, 118):
-            fp.run(stream, variant=v)
+    need = plan.numel * plan.weights[0].element_size() * 2
+    if torch.cuda.mem_get_info()[0] < need * 1.15:  # (the 70B run in place: no room for a second model)
+        return None
+    ins = [torch.empty_like(w) for w in plan.weights]
+    fp = kernels.BatchPlan(ins, plan.n_bits, plan.group, plan.symmetric)
+    nbytes = plan.numel * 4
+    best = {}
+    for v in (100, 118):
+        fp.run(stream, variant=v)
+        torch.cuda.synchronize()
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(steps):
+                fp.run(stream, variant=v)
+            e1.record(stream)
             torch.cuda.synchronize()
-            for _ in range(rounds):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                for _ in range(steps):
-                    fp.run(stream, variant=v)
-                e1.record(stream)
-                torch.cuda.synchronize()
-                gbs = rows * 4096 * 4 / (e0.elapsed_time(e1) / steps / 1e3) / 1e9
-                row[v] = max(row.get(v, 0.0), gbs)
-                best[v] = max(best.get(v, 0.0), gbs)
-        per_pair.append({CEILING_PROBES[v]: round(g, 1) for v, g in row.items()})
-        del fp, src
+            best[v] = max(best.get(v, 0.0), nbytes / (e0.elapsed_time(e1) / steps / 1e3) / 1e9)
+    del fp, ins
     torch.cuda.empty_cache()
     forms = {CEILING_PROBES[v]: round(g, 1) for v, g in best.items()}
-    return {"GBps": max(forms.values()), "forms": forms, "pairs": per_pair, "bytes_per_input": int(rows * 4096 * 2),
-            "basis": f"best of {pairs} fresh input/output pairs (not the plan's buffers)"}
+    return {"GBps": max(forms.values()), "forms": forms,
+            "basis": "fresh input + output per weight of the plan (same shapes, not the plan's buffers)"}
 
 
 def launch_floor_us(reps=32):
@@ -1157,7 +1153,7 @@ def main():
         ab_variants(plan, [int(v) for v in args.variants.split(",")], args)
     clock_ramp(plan, args.ramp_seconds)
     ceiling = copy_ceiling(plan)  # every rank: its own GPU's ceiling (roofline.per_rank)
-    fresh = fresh_ceiling()       # and the box's, on buffers that are not the plan's
+    fresh = fresh_ceiling(plan)   # and the box's, on buffers that are not the plan's
     kernel_ms, ms_per_step = timed_steps(plan, args, ws_n, stream)
 
     other = None
@@ -1186,9 +1182,10 @@ def main():
         traffic, traffic_src = None, ("the committed PMC record is the 1-GPU workload's; at N > 1 every rank runs "
                                       "a different bin (profiles/traffic.json: +0.07 % over algorithmic at N = 1)")
     roofline = roofline_record(per_rank, "k_group<f16,128,asym,batched,RW256>", traffic, traffic_src, ceiling, other)
-    fresh_g = gather_per_rank([fresh["GBps"]], ws_n)
-    roofline["fresh_ceiling"] = fresh if ws_n == 1 else {**fresh, "GBps_per_rank": [round(f[0], 1) for f in fresh_g]}
-    if roofline.get("achieved"):
+    fresh_g = gather_per_rank([fresh["GBps"] if fresh else 0.0], ws_n)
+    roofline["fresh_ceiling"] = (fresh if ws_n == 1 or not fresh else
+                                 {**fresh, "GBps_per_rank": [round(f[0], 1) for f in fresh_g]})
+    if roofline.get("achieved") and min(f[0] for f in fresh_g) > 0:
         lo = min(f[0] for f in fresh_g)
         roofline["kernel_over_fresh_ceiling"] = round(roofline["achieved"] / lo, 4)
         roofline["plan_ceiling_over_fresh_ceiling"] = round(min(p[2] for p in per_rank) / lo, 4)
