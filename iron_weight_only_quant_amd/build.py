@@ -16,7 +16,7 @@ LIB_AB = os.path.join(OUT_DIR, "libiwq_ab.so")
 def ab_requested():
     return os.environ.get("IWQ_AB", "0") == "1"
 SOURCES = ["iwq_minmax.hip", "iwq_batched.hip", "iwq_fp.hip", "iwq_bfp.hip", "iwq_gemm.hip", "iwq_prefill.hip", "iwq_synth.hip",
-           "iwq_fpunpack.hip", "iwq_codes.hip", "iwq_prefill16.hip", "iwq_fpdt.hip"]
+           "iwq_fpunpack.hip", "iwq_codes.hip", "iwq_prefill16.hip", "iwq_fpdt.hip", "iwq_prefill_ws.hip"]
 DEPS = SOURCES + ["iwq_minmax.cuh", "iwq_common.cuh", "iwq_seg.cuh", "iwq_fp.cuh", "iwq_fp_tables.h", "iwq_prefill.h",
                   "iwq_fp_tables_dt.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

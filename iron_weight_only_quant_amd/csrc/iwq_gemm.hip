@@ -1865,6 +1865,16 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       return IWQ_ERR_HIP;
     }
     return IWQ_OK;
+  } else if (IWQ_AB && variant >= 180 && variant <= 183 && !(flags & IWQ_FLAG_FORCE_GENERIC)) {
+    // round 6 A/B: the warp-specialised prefill (iwq_prefill_ws.hip; per channel, row-major codes)
+    if (!prefill_ws_supported(M, N, K, a.gpr, a.group)) return IWQ_ERR_ARG;
+    PrefillArgs p{a.x, a.lda, a.codes, a.scales, a.zeros, a.bias, a.y, a.ldy, a.M, a.N, a.K, a.gpr, a.group, a.zsym};
+    const hipError_t e = prefill_ws_launch(p, (int)variant, st);
+    if (e != hipSuccess) {
+      iwq::last_hip_error() = (int)e;
+      return IWQ_ERR_HIP;
+    }
+    return IWQ_OK;
   } else if (((variant == 0 && (M >= 256 || split_pref)) || (variant >= 40 && variant < 50) || (variant >= 60 && variant < 82) || variant == 97 || variant == 98 || variant == 99 || (variant >= 150 && variant <= 172) ||
               (variant > 81 && variant < 97)) && !(flags & IWQ_FLAG_FORCE_GENERIC) &&
              prefill_b32_supported(M, N, K, a.gpr, a.group)) {

@@ -56,4 +56,9 @@ bool prefill_short_split(int64_t M, int64_t N, int64_t K, int gpr, int group, in
 bool prefill16_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);
 hipError_t prefill16_launch(const PrefillArgs& a, int variant, hipStream_t st);
 
+// warp-specialised prefill (iwq_prefill_ws.hip, round 6 A/B variants 180-183): per channel, N % 256 == 0,
+// K % 64 == 0
+bool prefill_ws_supported(int64_t M, int64_t N, int64_t K, int gpr, int group);
+hipError_t prefill_ws_launch(const PrefillArgs& a, int variant, hipStream_t st);
+
 }  // namespace iwq

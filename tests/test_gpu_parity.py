@@ -706,6 +706,33 @@ def test_gemv_ksplit_identity_and_reference(K, Kd, group, M):
         assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16)), v
 
 
+@pytest.mark.skipif(not AB, reason="A/B library only (warp-specialised prefill variants 180-183)")
+@pytest.mark.parametrize("M", [256, 300, 1024])
+@pytest.mark.parametrize("sym", [False, True])
+def test_prefill_warp_specialised(K, M, sym):
+    """Round 6 A/B: the warp-specialised prefill (producer waves dequantize into an fp16 B image, consumer
+    waves run the MFMA loop; iwq_prefill_ws.hip) -- X = rows of the identity gives W_deq bit for bit
+    (per-channel numerics), random X within the fp32-GEMM tolerance, ragged M included, for the
+    pipeline depths 180 / 181 and the producer-priority form 182."""
+    N, Kd = 512, 4096
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 70)
+    r = K.quantize_minmax(w, 4, -2, sym, 0, want_codes=True)
+    ks = [(131 * i + 7) % Kd for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    x[torch.arange(M, device=DEV), torch.tensor(ks, device=DEV)] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    xr = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = xr.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (xr.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (180, 181, 182):
+        y = K.w4a16_gemm(x, r.codes, r.scales, r.zeros, 4, -2, N, flags=K.gemm_variant_flags(v))
+        assert torch.equal(y.view(torch.int16), want.view(torch.int16)), v
+        yr = K.w4a16_gemm(xr, r.codes, r.scales, r.zeros, 4, -2, N, b, flags=K.gemm_variant_flags(v))
+        assert bool(((yr.float() - ref).abs() <= tol).all()), (v, float((yr.float() - ref).abs().max()))
+
+
 @pytest.mark.parametrize("M", [24, 48, 96])
 @pytest.mark.parametrize("group", [128, 64])
 def test_mid_m_identity_rows_give_w_deq(K, M, group):
