@@ -85,7 +85,11 @@ enum iwq_status {
                                         path leaves that half zero on exit (the one-pass kernel's last
                                         workgroup clears its hand-off words; the two-kernel and
                                         universal forms use only the second half, which needs no
-                                        zeroing).  Ignored by other calls.                           */
+                                        zeroing).
+                                        iwq_w4a16_gemm, M <= 16 (round 6): the first 16 KiB of the
+                                        workspace (the batched decode K-split's arrival counters) are
+                                        zero on entry and left zero; without the flag that form is not
+                                        taken.  Ignored by other calls.                              */
 /* bits 16..23: kernel variant for A/B (0 = default; never needed for correct results): the batched
  * fp16/g128/asym quantize kernel (iwq_quantize_minmax_batched), and iwq_w4a16_gemm's kernel choice
  * (40-49 / 60-81 / 150-172 prefill kernels, 50-55 mid-M, 82-95 forced split-K ranges, 96 the first

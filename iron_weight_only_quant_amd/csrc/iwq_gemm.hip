@@ -46,6 +46,13 @@ struct GemmArgs {
   int group;            // group length along K (K for per-channel)
   int gshift;           // log2(group) when group is a power of two, else -1
   float zsym;           // symmetric code offset 2^(b-1)
+  // the cross-workgroup K-split of the batched decode (k_w4a16_gemv_ct<.., KSX>, round 6): ks K ranges
+  // per column group, fp32 slabs ksws[ks][M][N], one arrival counter per column group (zero on entry,
+  // left zero by the last arrival)
+  float* ksws;
+  int* kscnt;
+  int ks;
+  int ksxcd;  // A/B: the ks workgroups of a column group on one XCD (block b on XCD b % 8)
 };
 
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
@@ -471,8 +478,17 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
       zv[u] = a.zeros ? gp<_Float16>(a.zeros)[gi] : (_Float16)a.zsym;
     }
     if constexpr (!XLDS) {
+      if constexpr (PROBE == 5) {  // A/B probe (wrong results): the same X bytes, lanes q of a row on
+        // one contiguous 64 B per instruction (piece 4 s + q instead of 4 q + s)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
+        for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow - 32 * q + kt * BK + 32 * s + 8 * q);
+      } else if constexpr (PROBE == 6) {  // A/B probe (wrong results): no X loads at all
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xa[u][s] = (u32x4){(uint32_t)kt, (uint32_t)s, 0x3C003C00u, 0u};
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xa[u][s] = *gp<u32x4>(xrow + kt * BK + 8 * s);
+      }
     }
   };
   // the code prefetch first (DRAM: the longest latency); then the staged parameters' first PRE
@@ -537,7 +553,7 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
           af = __builtin_bit_cast(h8, pa);
         }
         h8 bf;
-        if constexpr (PROBE >= 1) {  // A/B probe only: no dequantization (wrong results)
+        if constexpr (PROBE == 1 || PROBE == 2) {  // A/B probe only: no dequantization (wrong results)
           const uint32_t w = bc[u][s];
           bf = __builtin_bit_cast(h8, (u32x4){w, w ^ 1u, w ^ 2u, w ^ 3u});
         } else if constexpr (PC || GF) {
@@ -587,16 +603,27 @@ __global__ __launch_bounds__(S * T * 64) void k_w4a16_gemv(GemmArgs a) {
 // Same k-split S and the same per-tile accumulation order as k_w4a16_gemv<.., S, ..>: identical bits
 // (GF: the grouped scale factored per k-step, as k_w4a16_gemv's PM 2).
 template <int PF, int S, int CT, bool XLDS, bool TILED, bool PC = false, bool GF = false, bool PST = false,
-          int XB = 1>
+          int XB = 1, bool KSX = false>
 __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   static_assert(!PST || !PC, "staged parameters: grouped weights only");
+  static_assert(!KSX || !XLDS, "the K-split form reads X per k-step (no whole-row image)");
   extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
   const int lane = threadIdx.x & 63;
   const int ks = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int q = lane >> 4, r16 = lane & 15;
-  const int tile0 = blockIdx.x * CT;
+  // KSX: workgroup b = column group b / a.ks, K range b % a.ks (k-steps [kb, ke) of the nks)
+  int cgrp = KSX ? (int)blockIdx.x / a.ks : (int)blockIdx.x;
+  int ksi = KSX ? (int)blockIdx.x - cgrp * a.ks : 0;
+  if (KSX && a.ksxcd) {  // block b = x + 8 j: XCD x's j-th workgroup -> group x + 8 (j / ks), range j % ks
+    const int xj = (int)blockIdx.x >> 3;
+    cgrp = ((int)blockIdx.x & 7) + 8 * (xj / a.ks);
+    ksi = xj - (xj / a.ks) * a.ks;
+  }
+  const int tile0 = cgrp * CT;
   const int nks = a.K / BK;
-  const int nj = nks > ks ? (nks - ks + S - 1) / S : 0;
+  const int kb = KSX ? (int)((int64_t)nks * ksi / a.ks) : 0;
+  const int nkr = KSX ? (int)((int64_t)nks * (ksi + 1) / a.ks) - kb : nks;
+  const int nj = nkr > ks ? (nkr - ks + S - 1) / S : 0;
   const int64_t crow = a.K / 2;
   const int arow = r16 < a.M ? r16 : a.M - 1;
   const int xpitch = a.K * 2 + 16;
@@ -618,7 +645,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
   _Float16 sv[PF][CT], zv[PF][CT];
   u32x4 xa[XLDS ? 1 : PF][4];
   auto load = [&](int j, int u) {
-    const int kt = ks + j * S;
+    const int kt = kb + ks + j * S;
 #pragma unroll
     for (int c = 0; c < CT; ++c)
       bc[u][c] = __builtin_nontemporal_load(gp<u32x4>(cbase + c * tstride + kt * (TILED ? 1024 : BK / 2)));
@@ -664,7 +691,7 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
     for (int u = 0; u < PF; ++u) {
       const int j = j0 + u;
       if (j >= nj) break;
-      const int kt = ks + j * S;
+      const int kt = kb + ks + j * S;
       h2 s2[CT], z1024[CT], z64[CT];
       float sf[CT];  // GF: the step's group scale per tile
 #pragma unroll
@@ -720,6 +747,12 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
 #pragma unroll
   for (int c = 0; c < CT; ++c) *reinterpret_cast<f4*>(red + (ks * CT + c) * 256 + lane * 4) = acc[c];
   __syncthreads();
+  auto finish = [&](float v, int row, int col) {
+    if constexpr (PC) v = opaque(v * (float)gp<_Float16>(a.scales)[col]);  // no fma_mix fold
+    if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
+    gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+  };
+  const bool split = KSX && a.ks > 1;
   for (int o = threadIdx.x; o < CT * 256; o += S * 64) {
     const int c = o >> 8, e = o & 255;
     const int ln = e >> 2, reg = e & 3;
@@ -728,9 +761,41 @@ __global__ __launch_bounds__(S * 64) void k_w4a16_gemv_ct(GemmArgs a) {
       float v = 0.f;
 #pragma unroll
       for (int k = 0; k < S; ++k) v += red[(k * CT + c) * 256 + e];
-      if constexpr (PC) v = opaque(v * (float)gp<_Float16>(a.scales)[col]);  // no fma_mix fold
-      if (a.bias) v += (float)gp<_Float16>(a.bias)[col];
-      gp<_Float16>(a.y)[(int64_t)row * a.ldy + col] = (_Float16)v;
+      if (split)  // this K range's partial, device-coherent (the last arrival may sit on another XCD)
+        __hip_atomic_store(a.ksws + ((int64_t)ksi * a.M + row) * a.N + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        finish(v, row, col);
+    }
+  }
+  if constexpr (KSX) {
+    if (split) {
+      // every wave's slab stores complete before the arrival (the stores are device-coherent: a wait
+      // for them, not an agent-scope release fence -- on gfx950 that fence writes back the whole L2,
+      // and one per workgroup serialised the grid: 20-550 us per call, profiles/r06_gemv_ksx_ab.jsonl);
+      // the last of the a.ks workgroups of the column group sums the slabs in K-range order
+      // (deterministic) with device-coherent loads, finishes the tile and clears the counter
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __shared__ int last;
+      if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(a.kscnt + cgrp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == a.ks - 1;
+        if (last) __hip_atomic_store(a.kscnt + cgrp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (last) {
+        for (int o = threadIdx.x; o < CT * 256; o += S * 64) {
+          const int c = o >> 8, e = o & 255;
+          const int ln = e >> 2, reg = e & 3;
+          const int row = 4 * (ln >> 4) + reg, col = (tile0 + c) * 16 + (ln & 15);
+          if (row < a.M) {
+            float v = 0.f;
+            for (int k = 0; k < a.ks; ++k)
+              v += __hip_atomic_load(a.ksws + ((int64_t)k * a.M + row) * a.N + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            finish(v, row, col);
+          }
+        }
+      }
     }
   }
 }
@@ -967,6 +1032,61 @@ void launch_gemv_ks(const GemmArgs& a, hipStream_t st, float* ws, int KS) {
   else hipLaunchKernelGGL(k_gemv_ks_reduce<false>, dim3((unsigned)rb), dim3(256), 0, st, a, ws, KS);
 }
 
+// The cross-workgroup K-split of the batched decode (round 6, k_w4a16_gemv_ct<.., KSX>).  At M = 16
+// the X rows, not the codes, are what a workgroup waits for: every workgroup of the unsplit kernels reads
+// all of X (M x K fp16) from L2 -- 128 KiB per CU on K = 4096, 344 KiB on K = 11008 -- at the ~70 GB/s
+// per CU an L2-served stream gets (MI355X_MICROARCH.md §Indexed rows), 2.3 / 5.7 us of the 6.7 / 13.6
+// us q / down calls (an A/B probe without X loads runs M = 16 at the M = 1 time: profiles/
+// r06_gemv_xstream.jsonl).  X bytes per workgroup are M * 2 * (its K range) against 8 * CT * (its K
+// range) of codes, so CT = 4 tiles per workgroup make X 1 : 1 with the codes at M = 16, and KS K ranges
+// per column group bring the grid back to the CU count: KS times less X per CU.  The KS partial tiles
+// meet in fp32 slabs; the last workgroup of a column group to arrive (one agent-scope counter per group,
+// zero on entry and cleared again by that workgroup: IWQ_FLAG_WS_ZEROED) sums them in K-range order and
+// finishes the tile in the same launch.  Workspace: the counters (GEMV_KSX_CNT_BYTES, G <= 4096 of them
+// used), then KS * M * N fp32.
+constexpr int GEMV_KSX_CT = 4;
+// the counter region has one fixed size, whatever the call's N: a per-stream workspace serves calls of
+// every shape, and one call's slabs must never lie where another call expects zero counters
+constexpr int64_t GEMV_KSX_CNT_BYTES = 16384;
+inline bool gemv_ksx_plan(int64_t M, int64_t N, int64_t K, int* ct_out, int* ks_out) {
+  if (M < 8 || M > 16 || N % (16 * GEMV_KSX_CT) != 0 || K % BK != 0) return false;
+  const int64_t g = N / (16 * GEMV_KSX_CT), nks = K / BK, cus = gemm_cu_count();
+  if (g >= cus || g * 4 > GEMV_KSX_CNT_BYTES) return false;
+  const int64_t ks = (cus + g - 1) / g;
+  if (nks / ks < 4) return false;
+  if (ct_out) *ct_out = GEMV_KSX_CT;
+  if (ks_out) *ks_out = (int)ks;
+  return true;
+}
+inline int64_t gemv_ksx_cnt_bytes(int64_t N, int ct) { return (void)N, (void)ct, GEMV_KSX_CNT_BYTES; }
+inline int64_t gemv_ksx_bytes_for(int64_t M, int64_t N, int ct, int ks) {
+  return gemv_ksx_cnt_bytes(N, ct) + (int64_t)ks * M * N * 4;
+}
+inline int64_t gemv_ksx_bytes(int64_t M, int64_t N, int64_t K) {
+  int ct = 0, ks = 0;
+  return gemv_ksx_plan(M, N, K, &ct, &ks) ? gemv_ksx_bytes_for(M, N, ct, ks) : 0;
+}
+constexpr bool GEMV_KSX_DEFAULT = false;
+
+template <int PF, int S, int CT, bool TILED>
+void launch_gemv_ksx(GemmArgs a, hipStream_t st, void* ws, int KS, bool xcd = false) {
+  a.ksxcd = xcd ? 1 : 0;
+  a.kscnt = static_cast<int*>(ws);
+  a.ksws = reinterpret_cast<float*>(static_cast<uint8_t*>(ws) + gemv_ksx_cnt_bytes(a.N, CT));
+  a.ks = KS;
+  const unsigned blocks = (unsigned)(a.N / (16 * CT) * KS);
+  const size_t red = (size_t)S * CT * 256 * 4;
+  const bool pc = a.gpr == 1;
+  const bool gf = !pc && a.group % BK == 0;
+  const int64_t pend = (int64_t)16 * CT * (a.gpr + 1) * 4;
+  const bool pst = gf && pend <= PST_LDS_MAX;
+  const size_t ldsp = red > (size_t)pend ? red : (size_t)pend;
+  if (pc) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, true, false, false, 1, true>), dim3(blocks), dim3(S * 64), red, st, a);
+  else if (pst) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, false, true, true, 1, true>), dim3(blocks), dim3(S * 64), ldsp, st, a);
+  else if (gf) hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, false, true, false, 1, true>), dim3(blocks), dim3(S * 64), red, st, a);
+  else hipLaunchKernelGGL((k_w4a16_gemv_ct<PF, S, CT, false, TILED, false, false, false, 1, true>), dim3(blocks), dim3(S * 64), red, st, a);
+}
+
 // Column tiles per wave for the decode default (cold sweep, profiles/r01_gemv_ct.jsonl): X traffic
 // only matters from M = 4 on, and a CT-fold smaller grid must still cover the chip: CT = 4 when that
 // leaves >= 256 workgroups (or >= 160 at M >= 8: 7B gate/up), CT = 2 for >= 256 workgroups once M*K
@@ -1032,14 +1152,14 @@ void launch_gemv(const GemmArgs& a, hipStream_t st, bool allow_lds, bool allow_p
   const int64_t xbytes = (int64_t)a.M * (a.K * 2 + 16);
   const unsigned blocks = (unsigned)(a.N / (16 * T));
   const size_t red = (size_t)S * T * 256 * 4;
-  const bool pc = a.gpr == 1 && PROBE == 0 && allow_pc;
+  const bool pc = a.gpr == 1 && (PROBE == 0 || PROBE >= 5) && allow_pc;  // 5, 6: X-stream probes
   // BIGX: the large image where the grid is at most one workgroup per CU (XLDS_BIG)
   const int64_t xmax = (BIGX && (int64_t)blocks <= gemm_cu_count()) ? XLDS_BIG : XLDS_MAX;
   // grouped: the staged parameters (PST) after the X image, 16 T rows of gpr + 1 dwords
   const bool xl = allow_lds && xbytes <= xmax;
   const int64_t pend = (xl ? (xbytes + 15) / 16 * 16 : 0) + (int64_t)16 * T * (a.gpr + 1) * 4;
-  const bool pst = !pc && PROBE == 0 && pm > 0 && pend <= (BIGX ? xmax + 16 * 1024 : PST_LDS_MAX);
-  const bool gf = !pc && PROBE == 0 && pm == 2 && a.group % BK == 0;  // every k-step inside one group
+  const bool pst = !pc && (PROBE == 0 || PROBE >= 5) && pm > 0 && pend <= (BIGX ? xmax + 16 * 1024 : PST_LDS_MAX);
+  const bool gf = !pc && (PROBE == 0 || PROBE >= 5) && pm == 2 && a.group % BK == 0;  // every k-step inside one group
   const size_t ldsp0 = red > (size_t)pend ? red : (size_t)pend;
   if (xl && BIGX && xbytes > XLDS_MAX) {
     const size_t lds = red > (size_t)xbytes ? red : (size_t)xbytes;
@@ -1605,7 +1725,10 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
 
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (M <= 16) return gemv_ks_bytes(M, N, K);  // the K-split decode's slabs (round 6), where planned
+  if (M <= 16) {  // the K-split decodes' slabs (round 6), where planned
+    const int64_t a = gemv_ks_bytes(M, N, K), b = gemv_ksx_bytes(M, N, K);
+    return a > b ? a : b;
+  }
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;
   if (g <= 0 || K % g != 0) return 0;
   int ns = 0, mtw = 2;
@@ -1726,6 +1849,39 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
     }
     return IWQ_OK;
   }
+  // the cross-workgroup K-split decode (round 6, KSX) where planned, given a workspace whose counters
+  // are zero (IWQ_FLAG_WS_ZEROED); A/B variants 200-239 force (CT, KS) = (4 | 8, 1 + (v - 200) % 20)
+  if (M <= 16 && !(flags & IWQ_FLAG_FORCE_GENERIC) && workspace && (flags & IWQ_FLAG_WS_ZEROED) &&
+      ((variant == 0 && GEMV_KSX_DEFAULT) || (IWQ_AB && variant >= 200 && variant < 260))) {
+    int ct = 0, ksn = 0;
+    bool ok = false;
+    if (variant == 0) {
+      ok = gemv_ksx_plan(M, N, K, &ct, &ksn);
+    } else {
+      ct = (variant < 220 || variant >= 240) ? 4 : 8;
+      ksn = 1 + (int)(variant - 200) % 20;
+      ok = N % (16 * ct) == 0 && K / BK >= ksn && N / (16 * ct) * 4 <= GEMV_KSX_CNT_BYTES;
+      if (variant >= 240) ok = ok && (N / (16 * ct)) % 8 == 0;  // the XCD-local map
+    }
+    const bool xcd = variant >= 240;
+    if (ok && workspace_bytes >= gemv_ksx_bytes_for(M, N, ct, ksn)) {
+      const bool tl = (flags & IWQ_FLAG_TILED_CODES) != 0;
+      if (ct == 8) {
+        if (tl) launch_gemv_ksx<2, 8, 8, true>(a, st, workspace, ksn, xcd);
+        else launch_gemv_ksx<2, 8, 8, false>(a, st, workspace, ksn, xcd);
+      } else {
+        if (tl) launch_gemv_ksx<2, 8, 4, true>(a, st, workspace, ksn, xcd);
+        else launch_gemv_ksx<2, 8, 4, false>(a, st, workspace, ksn, xcd);
+      }
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) {
+        iwq::last_hip_error() = (int)e;
+        return IWQ_ERR_HIP;
+      }
+      return IWQ_OK;
+    }
+    if (variant != 0) return IWQ_ERR_ARG;
+  }
   // the K-split decode (round 6, k_w4a16_gemv_ks) where planned and the caller gave its workspace;
   // GEMV_KS_DEFAULT decides whether the default takes it (A/B variant 31 forces it, 32 refuses it)
   int ks_ct = 0, ks_n = 0;
@@ -1767,6 +1923,11 @@ static int w4a16_gemm_impl(const void* x, int64_t M, int64_t K, int64_t lda, con
       case 102: launch_gemv<2, 8, 1, 2, true>(a, st, true); break;  // probe: k-major order
       case 103: launch_gemv<2, 16, 1, 2, true>(a, st, true); break;
       case 104: launch_gemv<2, 16, 1, 1, true>(a, st, true); break;
+      // round 6, the X stream of the ring form (no LDS image) at batched decode: 107 the ring itself,
+      // 105 its X loads made line-contiguous (same bytes, wrong results), 106 no X loads (wrong results)
+      case 105: launch_gemv<2, 8, 1, 5, true>(a, st, false); break;
+      case 106: launch_gemv<2, 8, 1, 6, true>(a, st, false); break;
+      case 107: launch_gemv<2, 8, 1, 0, true>(a, st, false); break;
       case 25: launch_gemv<2, 8, 1, 0, true>(a, st, true, false, 0); break;  // per-element scale (A/B)
       case 26: launch_gemv_ct<1, 8, 4, true>(a, st, false, false); break;
       case 27: launch_gemv<2, 8, 1, 0, true>(a, st, true, true, 0); break;  // grouped: params per step, global

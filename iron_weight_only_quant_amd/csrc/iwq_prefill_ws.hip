@@ -36,12 +36,13 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int WS_TM = 128, WS_TN = 256, WS_TK = 64, WS_THR = 512;
+constexpr int WS_TM = 128, WS_TN = 256, WS_TK = 64;
+[[maybe_unused]] constexpr int WS_THR = 512;
 constexpr int WS_AS = WS_TM * WS_TK * 2;  // 16 KiB of X per stage
 constexpr int WS_BS = WS_TN * WS_TK * 2;  // 32 KiB of fp16 B per stage
 constexpr int WS_CS = WS_TN * WS_TK / 2;  // 8 KiB of packed codes per stage
 constexpr int WS_NA = 4, WS_NB = 2;       // ring slots (the codes ring has WS_NA slots too)
-constexpr int WS_LDS = WS_NA * (WS_AS + WS_CS) + WS_NB * WS_BS;  // 160 KiB
+[[maybe_unused]] constexpr int WS_LDS = WS_NA * (WS_AS + WS_CS) + WS_NB * WS_BS;  // 160 KiB
 
 __device__ __forceinline__ int ws_xh(int r) { return ((r >> 1) & 1) | (((r >> 3) & 1) * 6); }
 // B column c's chunk q sits at slot q ^ bz(c), bz(c) = (c & 7) ^ ((c >> 3) & 1): conflict-free for both

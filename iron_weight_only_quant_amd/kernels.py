@@ -109,6 +109,9 @@ class _TensorWsCache:
 
 
 _tws = _TensorWsCache()
+# the decode GEMV's per-stream workspace (round 6): its leading counters zero, left zero by every call
+# (the cross-workgroup K-split, IWQ_FLAG_WS_ZEROED); the fp32 slabs after them are scratch
+_gws = _TensorWsCache()
 
 
 def group_geometry(rows, cols, group, quant_dim):
@@ -571,13 +574,18 @@ def gm_prefill_applies(M: int, N: int, K: int, group: int) -> bool:
 def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros: Optional[torch.Tensor],
                n_bits: int, group: int, N: int, bias: Optional[torch.Tensor] = None, flags: int = 0,
                tiled: bool = False, out: Optional[torch.Tensor] = None, nib: bool = False,
-               scales_gm: Optional[torch.Tensor] = None, zeros_gm: Optional[torch.Tensor] = None) -> torch.Tensor:
+               scales_gm: Optional[torch.Tensor] = None, zeros_gm: Optional[torch.Tensor] = None,
+               zeroed_workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = x @ W_deq^T (+ bias) with W_deq dequantized in registers from packed codes (MFMA).
     tiled: `codes` is in the decode tile layout (tile_codes), M <= 16 only.
     nib: `codes` is in the NIB layout (nib_codes), M >= NIB_MIN_M only (the prefill kernel).
     scales_gm / zeros_gm: optional group-major copies of the grouped parameters
     (group_major_params), read where gm_prefill_applies (same bits; scales / zeros elsewhere).
-    out: optional contiguous fp16 [M, N] destination (rows of x flattened)."""
+    out: optional contiguous fp16 [M, N] destination (rows of x flattened).
+    zeroed_workspace: M <= 16 only, for graph capture: a uint8 device tensor of >= gemm_workspace_bytes
+    whose first gemm_counter_bytes are zero and which the call leaves so (IWQ_FLAG_WS_ZEROED: the
+    batched decode's cross-workgroup K-split); eager calls use a per-stream one without asking, calls
+    captured without one take the unsplit kernels."""
     if tiled:
         flags |= L.IWQ_FLAG_TILED_CODES
     if nib:
@@ -620,12 +628,43 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
                 raise ValueError("w4a16_gemm: zeros_gm must accompany zeros (and only zeros)")
             flags |= L.IWQ_FLAG_GROUP_MAJOR
             scales, zeros = scales_gm, zeros_gm
-        ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
+        if 200 <= v < 260:  # A/B: the K-split decode forced to (CT, KS) (iwq_gemm.hip)
+            ksn = 1 + (v - 200) % 20
+            ws_bytes = max(ws_bytes, 16384 + ksn * M * N * 4)  # GEMV_KSX_CNT_BYTES + slabs
+        gkey = None
+        if M <= 16 and ws_bytes:
+            if zeroed_workspace is not None:
+                if (zeroed_workspace.dtype != torch.uint8 or zeroed_workspace.numel() < ws_bytes
+                        or zeroed_workspace.device != x.device):
+                    raise ValueError(f"w4a16_gemm: zeroed_workspace must be >= {ws_bytes} uint8 bytes on {x.device}")
+                ws = zeroed_workspace
+                flags |= L.IWQ_FLAG_WS_ZEROED
+            elif not torch.cuda.is_current_stream_capturing():
+                gkey = torch.cuda.current_stream(x.device).cuda_stream
+                ws = _gws.get(x.device, gkey, ws_bytes)
+                flags |= L.IWQ_FLAG_WS_ZEROED
+            else:
+                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+        else:
+            ws = torch.empty(ws_bytes // 4, dtype=torch.float32, device=x.device) if ws_bytes else None
         st = lib.iwq_w4a16_gemm_ws(L.ptr(x2), M, K, x2.stride(0), L.ptr(codes), L.ptr(scales), L.ptr(zeros),
                                    int(n_bits), int(group), N, L.ptr(bias), L.ptr(y), N, L.ptr(ws), ws_bytes,
                                    int(flags), L.stream_handle(x.device))
+        if st != L.IWQ_OK and gkey is not None:
+            _gws.drop(x.device, gkey)  # a failed launch may have left its counters dirty
     _raise_for(st, "iwq_w4a16_gemm")
     return y.reshape(*x.shape[:-1], N)
+
+
+def gemm_workspace_bytes(M: int, N: int, K: int, group: int, flags: int = 0) -> int:
+    """Workspace w4a16_gemm uses for this call (0: none); for a zeroed_workspace at M <= 16."""
+    lib = L.load()
+    n = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group)))
+    v = (int(flags) >> 16) & 0xFF
+    if M <= 16 and 200 <= v < 260:
+        ksn = 1 + (v - 200) % 20
+        n = max(n, 16384 + ksn * M * N * 4)  # GEMV_KSX_CNT_BYTES + slabs
+    return n
 
 
 def tile_codes(codes: torch.Tensor, N: int, K: int) -> torch.Tensor:

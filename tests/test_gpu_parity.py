@@ -706,6 +706,42 @@ def test_gemv_ksplit_identity_and_reference(K, Kd, group, M):
         assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16)), v
 
 
+@pytest.mark.skipif(not AB, reason="A/B library only (cross-workgroup K-split decode variants 200-259)")
+@pytest.mark.parametrize("Kd,group", [(4096, -2), (11008, 128)])
+def test_gemv_cross_workgroup_ksplit(K, Kd, group):
+    """Round 6 A/B: the batched decode's cross-workgroup K-split (k_w4a16_gemv_ct<.., KSX>: KS K ranges
+    per 4 or 8 column tiles, fp32 slabs, the last arrival finishes the tile) -- X = rows of the identity
+    gives W_deq bit for bit, random X within the fp32-GEMM tolerance, three calls in a row on one zeroed
+    workspace (the arrival counters are left zero: every call after the first is right too), and the
+    workspace's counter region is zero afterwards; grid map per column group (203, 227) and XCD-local
+    (243)."""
+    N, M = 4096, 16
+    w = torch.empty(N, Kd, dtype=torch.float16, device=DEV)
+    K.fill_synthetic(w, 71)
+    r = K.quantize_minmax(w, 4, group, False, 0, want_codes=True)
+    tiled = K.tile_codes(r.codes, N, Kd)
+    ks = [(263 * i + 11) % Kd for i in range(M)]
+    x = torch.zeros(M, Kd, dtype=torch.float16, device=DEV)
+    for i, k in enumerate(ks):
+        x[i, k] = 1.0
+    want = r.out[:, ks].t().contiguous()
+    xr = (torch.randn(M, Kd, device=DEV) * 0.5).half()
+    b = (torch.randn(N, device=DEV) * 0.1).half()
+    ref = xr.float() @ r.out.float().t() + b.float()
+    tol = 2e-3 * ref.abs() + 1e-3 * (xr.float().abs() @ r.out.float().abs().t()).max() / Kd ** 0.5 + 1e-3
+    for v in (203, 227, 243):
+        fl = K.gemm_variant_flags(v)
+        zws = torch.zeros(K.gemm_workspace_bytes(M, N, Kd, group, fl), dtype=torch.uint8, device=DEV)
+        for codes, tl in ((r.codes, False), (tiled, True)):
+            for _ in range(3):
+                y = K.w4a16_gemm(x, codes, r.scales, r.zeros, 4, group, N, tiled=tl, flags=fl, zeroed_workspace=zws)
+                assert torch.equal(y.view(torch.int16), want.view(torch.int16)), (v, tl)
+                yr = K.w4a16_gemm(xr, codes, r.scales, r.zeros, 4, group, N, b, tiled=tl, flags=fl, zeroed_workspace=zws)
+                assert bool(((yr.float() - ref).abs() <= tol).all()), (v, tl, float((yr.float() - ref).abs().max()))
+        torch.cuda.synchronize()
+        assert int(zws[:16384].count_nonzero()) == 0, v
+
+
 @pytest.mark.skipif(not AB, reason="A/B library only (warp-specialised prefill variants 180-183)")
 @pytest.mark.parametrize("M", [256, 300, 1024])
 @pytest.mark.parametrize("sym", [False, True])

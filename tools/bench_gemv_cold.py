@@ -92,8 +92,13 @@ def main():
                 y0 = None
                 for v in [int(t) for t in a.variants.split(",")]:
                     fl = kernels.gemm_variant_flags(v)
+                    # the batched decode's K-split needs zero counters: one zeroed workspace serves every
+                    # call of the graph (they run in order on one stream and each leaves it zeroed)
+                    wsb = kernels.gemm_workspace_bytes(M, N, K, a.group, fl) if M <= 16 else 0
+                    zws = torch.zeros(wsb, dtype=torch.uint8, device="cuda") if wsb else None
                     mk = lambda c: (lambda: kernels.w4a16_gemm(x, c, r.scales, r.zeros, 4, a.group, N, flags=fl,
-                                                               tiled=(layout == "tiled"), out=y))
+                                                               tiled=(layout == "tiled"), out=y,
+                                                               zeroed_workspace=zws))
                     mk(srcs[0])()
                     torch.cuda.synchronize()
                     err = float((y.float() - want).abs().max())
