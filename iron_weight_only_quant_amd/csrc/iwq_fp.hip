@@ -461,7 +461,7 @@ __device__ __forceinline__ uint32_t e2m1_mag2(uint32_t a) {
 // longer bounds the residency.
 // PF (single tensors, A/B round 6): the next iteration's loads issued before this one computes.
 template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false>
-__global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
+__device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
   static_assert(!E2A || CODEC == CODEC_FP, "closed form: the FP codec's E2M1");
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
@@ -681,6 +681,18 @@ __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
   }
   fp_flag_nan(a.nan_flag, any_nan);
 }
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false>
+__global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
+  fp_group_lut_body<CODEC, G, SYM, GS, BATCHED, CODES, E2A, PF>(a);
+}
+#if IWQ_AB
+// A/B (round 6): the same kernel held to 8 waves per SIMD (<= 64 VGPRs, 4 workgroups per CU) -- the
+// closed-form E2M1 form stages no table, so only the registers bound its residency
+template <int CODEC, int G, bool SYM, bool GS, int CODES, bool E2A>
+__global__ __launch_bounds__(LUT_QBLOCK, 8) void k_fp_group_lut_w8(FpArgs a) {
+  fp_group_lut_body<CODEC, G, SYM, GS, false, CODES, E2A, false>(a);
+}
+#endif
 
 // Double-approximate decode in ONE pass (g in {32, 64, 128}, quant_dim 0, group count % 4 == 0):
 // a quad is 4 consecutive groups at one in-group position, i.e. lanes l, l^LPG, l^2LPG, l^3LPG of
@@ -953,12 +965,9 @@ hipError_t launch_fp_group_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool PF = false>
-hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
-  // walk policy as k_group's single tensors: grid-stride at >= 2 grid rounds, else contiguous
-  auto kern = k_fp_group_lut<CODEC, G, SYM, false, false, CODES, E2A, PF>;
-  auto kern_gs = k_fp_group_lut<CODEC, G, SYM, true, false, CODES, E2A, PF>;
-  const size_t lds = E2A ? 0 : (size_t)a.lut_n8 * 2;
+// walk policy as k_group's single tensors: grid-stride at >= 2 grid rounds, else contiguous
+inline hipError_t launch_fp_lut_kern(void (*kern)(FpArgs), void (*kern_gs)(FpArgs), size_t lds, const FpArgs& a,
+                                     hipStream_t st) {
   int occ = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, LUT_QBLOCK, lds) != hipSuccess || occ <= 0) occ = 1;
   constexpr int WPBL = LUT_QBLOCK / WAVE;
@@ -971,11 +980,26 @@ hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   return hipGetLastError();
 }
+template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool PF = false, bool W8 = false>
+hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
+  const size_t lds = E2A ? 0 : (size_t)a.lut_n8 * 2;
+#if IWQ_AB
+  if constexpr (W8)
+    return launch_fp_lut_kern(k_fp_group_lut_w8<CODEC, G, SYM, false, CODES, E2A>, k_fp_group_lut_w8<CODEC, G, SYM, true, CODES, E2A>,
+                              lds, a, st);
+#else
+  static_assert(!W8, "A/B form");
+#endif
+  return launch_fp_lut_kern(k_fp_group_lut<CODEC, G, SYM, false, false, CODES, E2A, PF>,
+                            k_fp_group_lut<CODEC, G, SYM, true, false, CODES, E2A, PF>, lds, a, st);
+}
 // A/B (round 6): variant 3 = the next iteration's loads prefetched (PF); E2M1: 4 = PF + closed form
 template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false>
 hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
 #if IWQ_AB
   if (a.variant == 3 || (E2A && a.variant == 4)) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, true>(a, st);
+  if constexpr (G == 128)  // 5 / 6: held to 8 waves per SIMD (the formats rows' group only)
+    if (a.variant == 5 || a.variant == 6) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, true>(a, st);
 #endif
   return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false>(a, st);
 }
@@ -1023,12 +1047,12 @@ hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-// E2M1 FP codec: the closed form (no table) -- A/B round 6: variant 1 forces it (4: with PF), 2 forces
-// the table
+// E2M1 FP codec: the closed form (no table) -- A/B round 6: variant 1 forces it (4: with PF, 5: held to
+// 8 waves per SIMD), 2 forces the table (6: the table form held to 8 waves per SIMD)
 template <bool SYM, int CODES>
 hipError_t launch_fp_e2m1(int64_t g, const FpArgs& a, hipStream_t st) {
   if (a.variant == 2) return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
-  if (a.variant == 1 || a.variant == 4) return launch_fp_lut_g<CODEC_FP, SYM, CODES, true>(g, a, st);
+  if (a.variant == 1 || a.variant == 4 || a.variant == 5) return launch_fp_lut_g<CODEC_FP, SYM, CODES, true>(g, a, st);
   return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
 }
 

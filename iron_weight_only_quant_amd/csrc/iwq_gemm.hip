@@ -1725,8 +1725,9 @@ int iwq_dequant_packed(const void* codes, const void* scales, const void* zeros,
 
 int64_t iwq_w4a16_gemm_workspace_bytes(int64_t M, int64_t N, int64_t K, int64_t group) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (M <= 16) {  // the K-split decodes' slabs (round 6), where planned
-    const int64_t a = gemv_ks_bytes(M, N, K), b = gemv_ksx_bytes(M, N, K);
+  if (M <= 16) {  // the K-split decodes' slabs (round 6), where the default takes one (A/B forms: the
+    // caller sizes its own)
+    const int64_t a = GEMV_KS_DEFAULT ? gemv_ks_bytes(M, N, K) : 0, b = GEMV_KSX_DEFAULT ? gemv_ksx_bytes(M, N, K) : 0;
     return a > b ? a : b;
   }
   const int64_t g = group == IWQ_GROUP_PER_CHANNEL ? K : group;

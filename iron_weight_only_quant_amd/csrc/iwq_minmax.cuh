@@ -314,17 +314,19 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
   int64_t u0, cend;
   int64_t wrap_lo = 0, wrap_hi = 0;  // PHASE: the chunk's head, walked after its tail
   int64_t rend = 0;                   // RW: end of this wave's region
+  // RW: waves per region, at most the grid's (a grid of fewer than RW waves is one region)
+  const int64_t rw = RW > 1 && nwaves < RW ? nwaves : RW;
   if constexpr (GS) {
     u0 = wave * UNROLL;
     cend = min(u0 + UNROLL, a.total_units);
   } else if constexpr (RW > 1) {
-    const int64_t nreg = nwaves / RW;
-    const int64_t r = wave / RW;
+    const int64_t nreg = nwaves / rw;
+    const int64_t r = wave / rw;
     int64_t per = (a.total_units + nreg - 1) / nreg;
     per = (per + UNROLL - 1) / UNROLL * UNROLL;
     const int64_t rbeg = r < nreg ? r * per : a.total_units;
     rend = min(rbeg + per, a.total_units);
-    u0 = rbeg + (wave % RW) * UNROLL;
+    u0 = rbeg + (wave % rw) * UNROLL;
     cend = min(u0 + UNROLL, rend);
   } else {
     int64_t per = (a.total_units + nwaves - 1) / nwaves;
@@ -355,7 +357,7 @@ __device__ __forceinline__ void k_group_body(const GroupArgs& a) {
     }
     if constexpr (RW > 1 && !GS) {
       if (u0 >= cend) {
-        u0 += (RW - 1) * UNROLL;
+        u0 += (rw - 1) * UNROLL;
         cend = min(u0 + UNROLL, rend);
       }
     }

@@ -628,6 +628,8 @@ def w4a16_gemm(x: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, zeros
                 raise ValueError("w4a16_gemm: zeros_gm must accompany zeros (and only zeros)")
             flags |= L.IWQ_FLAG_GROUP_MAJOR
             scales, zeros = scales_gm, zeros_gm
+        if v == 31 and M <= 16:  # A/B: the K-split decode with a reduce launch (KS <= 16 slabs)
+            ws_bytes = max(ws_bytes, 16 * M * N * 4)
         if 200 <= v < 260:  # A/B: the K-split decode forced to (CT, KS) (iwq_gemm.hip)
             ksn = 1 + (v - 200) % 20
             ws_bytes = max(ws_bytes, 16384 + ksn * M * N * 4)  # GEMV_KSX_CNT_BYTES + slabs
@@ -661,6 +663,8 @@ def gemm_workspace_bytes(M: int, N: int, K: int, group: int, flags: int = 0) -> 
     lib = L.load()
     n = int(lib.iwq_w4a16_gemm_workspace_bytes(M, N, K, int(group)))
     v = (int(flags) >> 16) & 0xFF
+    if M <= 16 and v == 31:
+        n = max(n, 16 * M * N * 4)
     if M <= 16 and 200 <= v < 260:
         ksn = 1 + (v - 200) % 20
         n = max(n, 16384 + ksn * M * N * 4)  # GEMV_KSX_CNT_BYTES + slabs
