@@ -1117,7 +1117,35 @@ def build_record(args, ws_n, n_dev, weak, all_shapes, total_numel, ms_per_step, 
     rec.update(extra)
     if n_dev < ws_n:
         rec["note"] = f"{ws_n} ranks shared {n_dev} GPU(s) (gloo rehearsal): one GPU's bandwidth, not a scaling point"
+    rec["summary"] = summary_of(rec)
     return rec
+
+
+def summary_of(rec):
+    """The record's key figures in a few hundred bytes, emitted as the LAST key of the line: the
+    driver keeps only the tail of stdout, which otherwise ends inside the long sections."""
+    def g(d, *ks):
+        for k in ks:
+            d = d.get(k) if isinstance(d, dict) else None
+        return d
+    r = rec.get("roofline") or {}
+    s = {"frac": r.get("frac"), "kernel_over_ceiling": r.get("kernel_over_ceiling"),
+         "fresh_ceiling_GBps": g(r, "fresh_ceiling", "GBps"), "kernel_over_fresh_ceiling": r.get("kernel_over_fresh_ceiling"),
+         "other_placement": [g(r, "other_placement", "placement"), g(r, "other_placement", "frac")], "traffic_over_alg": (
+             round(r["traffic"] / r["alg_bytes_per_launch"], 4) if r.get("traffic") and r.get("alg_bytes_per_launch") else None)}
+    if rec.get("shapes"):
+        s["shapes_frac"] = {k: [v.get("frac"), v.get("frac_beyond_launch_floor")] for k, v in rec["shapes"].items()}
+    if rec.get("fused_forward"):
+        s["fused_vs_F_linear"] = {f"{x['shape']}/{'pc' if x['weights'] == 'per-channel' else x['weights']}/M{x['M']}":
+                                  x.get("fused_vs_F_linear") for x in rec["fused_forward"].get("rows", [])}
+    if rec.get("formats"):
+        s["formats_frac"] = {x["path"]: x.get("frac_of_hbm_peak") for x in rec["formats"].get("rows", [])}
+    if rec.get("llama2_70b"):
+        s["llama2_70b_frac"] = g(rec["llama2_70b"], "roofline", "frac")
+    cpu = rec.get("cpu_baseline")
+    if cpu:
+        s["cpu_baseline_GBps"] = cpu.get("value")
+    return s
 
 
 def main():
