@@ -660,11 +660,13 @@ __device__ __forceinline__ uint32_t quant2_biased_pair(uint32_t wpair, const Bia
 template <int CODES>
 __device__ __forceinline__ void store_codes8(uint8_t* base, int64_t elem0, const uint32_t (&c)[4]) {
   if constexpr (CODES == 4) {
-    uint32_t b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = (c[j] | (c[j] >> 12)) & 0xFFu;  // lo | hi << 4
-    const uint32_t v = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
-    *gp<uint32_t>(base + elem0 / 2) = v;
+    // c[j] holds the codes of elements 2j / 2j + 1 (< 16) in bytes 0 / 2: gather the even elements'
+    // bytes and the odd elements' bytes (four byte permutes), then one shift-or interleaves the nibbles
+    const uint32_t p01 = __builtin_amdgcn_perm(c[1], c[0], 0x06020400u);  // [e0, e2, e1, e3]
+    const uint32_t p23 = __builtin_amdgcn_perm(c[3], c[2], 0x06020400u);  // [e4, e6, e5, e7]
+    const uint32_t ev = __builtin_amdgcn_perm(p23, p01, 0x05040100u);     // [e0, e2, e4, e6]
+    const uint32_t od = __builtin_amdgcn_perm(p23, p01, 0x07060302u);     // [e1, e3, e5, e7]
+    *gp<uint32_t>(base + elem0 / 2) = ev | (od << 4);
   } else if constexpr (CODES == 8) {
     const uint32_t lo = __builtin_amdgcn_perm(c[1], c[0], 0x06040200u);
     const uint32_t hi = __builtin_amdgcn_perm(c[3], c[2], 0x06040200u);

@@ -62,6 +62,8 @@ struct FpArgs {
   uint32_t* nan_flag;
   const uint16_t* lut;  // decode table (iwq_fp_build_lut) or null: ALU codec
   int32_t lut_n8;       // table entries, rounded up to a multiple of 8
+  uint32_t lut_vmask;   // per 16-bit half: the entry's decoded-magnitude bits (lut_fields)
+  int32_t lut_ec;       // entries carry the magnitude code in their low E + M bits (lut_fields)
   const iwq_batch_entry* entries;  // batched form (whole model): tensor table, else null
   int32_t n_entries;
   int32_t variant;                 // A/B variant (flags bits 16..23) where a launcher has them
@@ -88,6 +90,24 @@ constexpr int LUT_MAX = 32768;
 
 __host__ __device__ inline uint32_t lut_bound_bits(int codec, const FpSpec& f) {
   return codec == CODEC_GRID ? 0x4600u /* 6.0 */ : (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)f.fp_max16);
+}
+// Round 6: FP / grid table entries carry the magnitude CODE of their decoded value in the low E + M
+// bits.  Every decoded magnitude is an fp16 value with at most M mantissa bits after the leading one
+// (normal in fp16: 2^(1 - bias - M) >= 2^-14 for every format fp_spec accepts), so its low 10 - M
+// mantissa bits are zero; where E + M <= 10 - M (FP4 / FP6 / E4M3, not E3M4 / E2M5 / E1M5-6) the code
+// fits beside the value: the packing kernels then take the code with one and-or per element pair
+// instead of re-encoding the decoded value (codes_of_values, 6 VALU per pair), and every table reader
+// masks it off (lut_vmask) in the and-or that already attaches the sign.
+__host__ __device__ inline bool lut_codes_embedded(int codec, const FpSpec& f) {
+  return (codec == CODEC_FP || codec == CODEC_GRID) && f.E + 2 * f.M <= 10;
+}
+__host__ __device__ inline uint32_t lut_code_mask(const FpSpec& f) { return (1u << (f.E + f.M)) - 1u; }
+inline void lut_fields(int codec, const FpSpec& f, const void* lut, FpArgs& a) {
+  a.lut = static_cast<const uint16_t*>(lut);
+  a.lut_n8 = (int32_t)((lut_bound_bits(codec, f) + 1 + 7) / 8 * 8);
+  a.lut_ec = lut_codes_embedded(codec, f) ? 1 : 0;
+  const uint32_t cm = a.lut_ec ? lut_code_mask(f) : 0u;
+  a.lut_vmask = 0x7FFF7FFFu & ~(cm | (cm << 16));
 }
 
 // Double-approximate decoder (quant_linear.py:288-363), split at the quad.  Per code (sign aside)
@@ -238,8 +258,17 @@ __global__ __launch_bounds__(BLOCK) void k_fp_build_lut(FpSpec f, uint16_t* lut,
         d = fp_decode(fp_encode(u, f, tabs), f);
       }
     }
-    if constexpr (CODEC == CODEC_APXD) lut[i] = (uint16_t)apxd_info(i < n ? fp_encode((uint32_t)i, f, tabs) : 0u, f);
-    else lut[i] = (uint16_t)(Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu);
+    if constexpr (CODEC == CODEC_APXD) {
+      lut[i] = (uint16_t)apxd_info(i < n ? fp_encode((uint32_t)i, f, tabs) : 0u, f);
+    } else {
+      uint32_t e = Fmt<DT_F16>::from_f(f16r(d)) & 0x7FFFu;
+      if (lut_codes_embedded(CODEC, f)) {  // the code of the decoded value, as codes_of_values derives it
+        const _Float16 rb = (_Float16)__builtin_ldexpf(1.0f, f.bias - 15);
+        const uint32_t t = __builtin_bit_cast(uint16_t, (_Float16)(__builtin_bit_cast(_Float16, (uint16_t)e) * rb));
+        e |= (t >> (10 - f.M)) & lut_code_mask(f);
+      }
+      lut[i] = (uint16_t)e;
+    }
   }
   if constexpr (CODEC == CODEC_APXD) {  // table 2: (tgt, magnitude code) -> value, after table 1;
                                         // codes >= 2^(E+M) (incl. the zero-code column 0x80) -> +0
@@ -460,9 +489,15 @@ __device__ __forceinline__ uint32_t e2m1_mag2(uint32_t a) {
 // magnitude (e2m1_mag2) -- no table is staged, so the workgroup starts streaming at once and LDS no
 // longer bounds the residency.
 // PF (single tensors, A/B round 6): the next iteration's loads issued before this one computes.
-template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false>
+// EC (round 6; packed codes from a table that embeds them, lut_codes_embedded): each pair's codes are
+// the entries' low E + M bits plus the sign moved from bit 15 to bit E + M -- one shift and one and-or
+// per pair instead of codes_of_values.  Table reads (round 6, D16 -- the name of its first form): the
+// two entries' LDS addresses by one SDWA add each.
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false,
+          bool EC = false, bool D16 = true>
 __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
   static_assert(!E2A || CODEC == CODEC_FP, "closed form: the FP codec's E2M1");
+  static_assert(!EC || (CODES != 0 && !E2A && (CODEC == CODEC_FP || CODEC == CODEC_GRID)), "embedded codes");
   using F = Fmt<DT_F16>;
   extern __shared__ u32x4 lut_dyn[];
   __shared__ uint16_t tab_buf[120];
@@ -492,6 +527,10 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
   const u16x2 bound2x = {bnd2, bnd2};
   const _Float16 rb16 = (_Float16)__builtin_ldexpf(1.0f, a.f.bias - 15);
   const h2 rebias = {rb16, rb16};
+  const uint32_t vmask = E2A ? 0x7FFF7FFFu : a.lut_vmask;  // the entries' value bits
+  const uint32_t cmask2 = vmask ^ 0x7FFF7FFFu;              // EC: the entries' code bits
+  const u16x2 csh = {(uint16_t)(15 - a.f.E - a.f.M), (uint16_t)(15 - a.f.E - a.f.M)};  // EC: sign bit 15 -> E + M
+  const uint32_t lbase = (uint32_t)(uintptr_t)lut;
   bool any_nan = false;
   // current tensor (batched: wave-uniform cursor over the table, entries ordered by unit_begin)
   const char* tw = a.w;
@@ -546,29 +585,53 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
           a2[j] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, tb[j]) << (u16x2)1,
                                                                          bound2x));
       }
+      if constexpr (E2A) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (E2A) {
-          r[j] = e2m1_mag2(a2[j]);
-        } else {
+        for (int j = 0; j < 4; ++j) r[j] = e2m1_mag2(a2[j]);
+      } else if constexpr (!D16) {  // A/B: the compiler's reads, joined by v_perm
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
           const h2 rv = {*(lds_h*)(lut + (a2[j] & 0xFFFFu)), *(lds_h*)(lut + (a2[j] >> 16))};
           r[j] = as_u32(rv);
         }
+      } else {
+        // entries 2j / 2j + 1 into the halves of r[j]: each address is lbase + one half of a2 by one SDWA
+        // add (the compiler spends an and + add on the low half), and the two zero-extended reads are
+        // joined by one shift-or.  (D16 reads into the halves of one register do not save that op:
+        // gfx950 has no d16-preserve -- a d16 / d16_hi load zeroes the other half.)  The reads are
+        // inline asm, so the wait that ends them also carries their registers into the code below.
+        uint32_t lo[4], hi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t alo, ahi;
+          asm("v_add_u32_sdwa %0, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+              "v_add_u32_sdwa %1, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+              : "=&v"(alo), "=&v"(ahi) : "v"(a2[j]), "s"(lbase));
+          asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(lo[j]), "=&v"(hi[j]) : "v"(alo), "v"(ahi));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = lo[j] | (hi[j] << 16);
       }
       uint32_t cp[4];  // the codes of elements 2j, 2j+1 in the 16-bit halves of cp[j]
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint32_t rb = r[j];
+        uint32_t sg;  // the value's sign bits
         if constexpr (CODEC == CODEC_GRID) {
-          rb |= tb[j] & 0x80008000u;
+          sg = tb[j] & 0x80008000u;
         } else {  // sign where |t| != 0: bit 15 of (tb + 0x7FFF) is clear exactly for negative nonzero t
           const uint32_t sum = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, tb[j]) + (u16x2)0x7FFF);
-          rb |= tb[j] & ~sum & 0x80008000u;
+          sg = tb[j] & ~sum & 0x80008000u;
         }
+        const uint32_t rb = (r[j] & vmask) | sg;
         h2 y = as_h2(rb) * s16;                                             // RN16(exact product)
         if constexpr (!SYM) y = y + z16;                                    // RN16(exact sum)
         o.u[j] = as_u32(y);
-        if constexpr (CODES != 0) cp[j] = codes_of_values(rb, a.f, rebias);
+        if constexpr (EC)
+          cp[j] = (r[j] & cmask2) | __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, sg) >> csh);
+        else if constexpr (CODES != 0)
+          cp[j] = codes_of_values(rb, a.f, rebias);
       }
       if (e0 < tnumel) {
         if (tout) o.store(tout + e0 * F::BYTES);
@@ -681,9 +744,10 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
   }
   fp_flag_nan(a.nan_flag, any_nan);
 }
-template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false>
+template <int CODEC, int G, bool SYM, bool GS, bool BATCHED = false, int CODES = 0, bool E2A = false, bool PF = false,
+          bool EC = false, bool D16 = true>
 __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
-  fp_group_lut_body<CODEC, G, SYM, GS, BATCHED, CODES, E2A, PF>(a);
+  fp_group_lut_body<CODEC, G, SYM, GS, BATCHED, CODES, E2A, PF, EC, D16>(a);
 }
 #if IWQ_AB
 // A/B (round 6): the same kernel held to 8 waves per SIMD (<= 64 VGPRs, 4 workgroups per CU) -- the
@@ -980,7 +1044,8 @@ inline hipError_t launch_fp_lut_kern(void (*kern)(FpArgs), void (*kern_gs)(FpArg
   else hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(LUT_QBLOCK), lds, st, a);
   return hipGetLastError();
 }
-template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool PF = false, bool W8 = false>
+template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool PF = false, bool W8 = false, bool EC = false,
+          bool D16 = true>
 hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
   const size_t lds = E2A ? 0 : (size_t)a.lut_n8 * 2;
 #if IWQ_AB
@@ -990,18 +1055,21 @@ hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
 #else
   static_assert(!W8, "A/B form");
 #endif
-  return launch_fp_lut_kern(k_fp_group_lut<CODEC, G, SYM, false, false, CODES, E2A, PF>,
-                            k_fp_group_lut<CODEC, G, SYM, true, false, CODES, E2A, PF>, lds, a, st);
+  return launch_fp_lut_kern(k_fp_group_lut<CODEC, G, SYM, false, false, CODES, E2A, PF, EC, D16>,
+                            k_fp_group_lut<CODEC, G, SYM, true, false, CODES, E2A, PF, EC, D16>, lds, a, st);
 }
-// A/B (round 6): variant 3 = the next iteration's loads prefetched (PF); E2M1: 4 = PF + closed form
-template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false>
+// A/B (round 6): variant 3 = the next iteration's loads prefetched (PF); E2M1: 4 = PF + closed form;
+// 7 = the table reads joined by v_perm and the codes re-encoded from the values (before EC / D16)
+template <int CODEC, int G, bool SYM, int CODES = 0, bool E2A = false, bool EC = false>
 hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
 #if IWQ_AB
-  if (a.variant == 3 || (E2A && a.variant == 4)) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, true>(a, st);
+  if (a.variant == 3 || (E2A && a.variant == 4)) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, true, false, EC>(a, st);
   if constexpr (G == 128)  // 5 / 6: held to 8 waves per SIMD (the formats rows' group only)
     if (a.variant == 5 || a.variant == 6) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, true>(a, st);
+  if constexpr (!E2A)
+    if (a.variant == 7) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, false, false, false>(a, st);
 #endif
-  return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false>(a, st);
+  return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, false, EC>(a, st);
 }
 
 template <int CODEC, int G, bool SYM>
@@ -1033,16 +1101,16 @@ hipError_t launch_fp_lut_batched(int64_t g, const FpArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int CODEC, bool SYM, int CODES = 0, bool E2A = false>
+template <int CODEC, bool SYM, int CODES = 0, bool E2A = false, bool EC = false>
 hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
   switch (g) {
-    case 8: return launch_fp_lut_t<CODEC, 8, SYM, CODES, E2A>(a, st);
-    case 16: return launch_fp_lut_t<CODEC, 16, SYM, CODES, E2A>(a, st);
-    case 32: return launch_fp_lut_t<CODEC, 32, SYM, CODES, E2A>(a, st);
-    case 64: return launch_fp_lut_t<CODEC, 64, SYM, CODES, E2A>(a, st);
-    case 128: return launch_fp_lut_t<CODEC, 128, SYM, CODES, E2A>(a, st);
-    case 256: return launch_fp_lut_t<CODEC, 256, SYM, CODES, E2A>(a, st);
-    case 512: return launch_fp_lut_t<CODEC, 512, SYM, CODES, E2A>(a, st);
+    case 8: return launch_fp_lut_t<CODEC, 8, SYM, CODES, E2A, EC>(a, st);
+    case 16: return launch_fp_lut_t<CODEC, 16, SYM, CODES, E2A, EC>(a, st);
+    case 32: return launch_fp_lut_t<CODEC, 32, SYM, CODES, E2A, EC>(a, st);
+    case 64: return launch_fp_lut_t<CODEC, 64, SYM, CODES, E2A, EC>(a, st);
+    case 128: return launch_fp_lut_t<CODEC, 128, SYM, CODES, E2A, EC>(a, st);
+    case 256: return launch_fp_lut_t<CODEC, 256, SYM, CODES, E2A, EC>(a, st);
+    case 512: return launch_fp_lut_t<CODEC, 512, SYM, CODES, E2A, EC>(a, st);
   }
   return hipErrorInvalidValue;
 }
@@ -1051,9 +1119,10 @@ hipError_t launch_fp_lut_g(int64_t g, const FpArgs& a, hipStream_t st) {
 // 8 waves per SIMD), 2 forces the table (6: the table form held to 8 waves per SIMD)
 template <bool SYM, int CODES>
 hipError_t launch_fp_e2m1(int64_t g, const FpArgs& a, hipStream_t st) {
-  if (a.variant == 2) return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
+  constexpr bool EC = CODES != 0;  // E2M1 tables always embed the codes (lut_codes_embedded)
+  if (a.variant == 2) return launch_fp_lut_g<CODEC_FP, SYM, CODES, false, EC>(g, a, st);
   if (a.variant == 1 || a.variant == 4 || a.variant == 5) return launch_fp_lut_g<CODEC_FP, SYM, CODES, true>(g, a, st);
-  return launch_fp_lut_g<CODEC_FP, SYM, CODES, false>(g, a, st);
+  return launch_fp_lut_g<CODEC_FP, SYM, CODES, false, EC>(g, a, st);
 }
 
 template <int G, int V>
@@ -1099,11 +1168,15 @@ hipError_t launch_fp_group(int codec, int64_t g, bool sym, int codes, const FpAr
     if (e2m1) return sym ? launch_fp_e2m1<true, 0>(g, a, st) : launch_fp_e2m1<false, 0>(g, a, st);
     return sym ? launch_fp_lut_g<CODEC_FP, true>(g, a, st) : launch_fp_lut_g<CODEC_FP, false>(g, a, st);
   }
-  if (a.lut) {  // codes re-encoded from the table's decoded values (code_of_value)
-    if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true, 4>(g, a, st);
+  if (a.lut) {  // codes from the table entries (EC: every 4-bit format, E4M3 ...) or re-encoded from the values
+    if (codec == CODEC_GRID) return launch_fp_lut_g<CODEC_GRID, true, 4, false, true>(g, a, st);
     if (e2m1) return sym ? launch_fp_e2m1<true, 4>(g, a, st) : launch_fp_e2m1<false, 4>(g, a, st);
-    if (codes == 4)
-      return sym ? launch_fp_lut_g<CODEC_FP, true, 4>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 4>(g, a, st);
+    if (codes == 4)  // 1 + E + M <= 4: E + 2M <= 5, embedded
+      return sym ? launch_fp_lut_g<CODEC_FP, true, 4, false, true>(g, a, st)
+                 : launch_fp_lut_g<CODEC_FP, false, 4, false, true>(g, a, st);
+    if (a.lut_ec)
+      return sym ? launch_fp_lut_g<CODEC_FP, true, 8, false, true>(g, a, st)
+                 : launch_fp_lut_g<CODEC_FP, false, 8, false, true>(g, a, st);
     return sym ? launch_fp_lut_g<CODEC_FP, true, 8>(g, a, st) : launch_fp_lut_g<CODEC_FP, false, 8>(g, a, st);
   }
   if (codec == CODEC_GRID)
@@ -1225,8 +1298,7 @@ int run_fp(int codec, const void* w, int64_t rows, int64_t cols, int64_t ld_w, i
     a.variant = IWQ_AB ? (int32_t)((flags >> 16) & 0xFFu) : 0;  // A/B forms (E2M1: launch_fp_e2m1)
     if (lut) {
       if (!aligned16p(lut)) return IWQ_ERR_ARG;
-      a.lut = static_cast<const uint16_t*>(lut);
-      a.lut_n8 = (int32_t)((lut_bound_bits(codec, f) + 1 + 7) / 8 * 8);
+      lut_fields(codec, f, lut, a);
     }
     IWQ_HIP_FP(launch_fp_group(codec, group, sym, codes, a, s));
     return IWQ_OK;
@@ -1488,8 +1560,7 @@ int iwq_quantize_fp_batched(const iwq_batch_entry* d_entries, int32_t n_entries,
   a.total_units = total_units;
   a.f = f;
   a.nan_flag = nan_flag;
-  a.lut = static_cast<const uint16_t*>(lut);
-  a.lut_n8 = (int32_t)((lut_bound_bits(codec, f) + 1 + 7) / 8 * 8);
+  lut_fields(codec, f, lut, a);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool sym = codec != CODEC_FP || symmetric != 0;
   hipError_t e;

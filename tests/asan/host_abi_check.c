@@ -180,6 +180,25 @@ static void check_fp_validation(void) {
                                2u << 16, NULL) == IWQ_ERR_ARG);
   CHECK(iwq_quantize_fp_approx(w, 64, 128, 128, IWQ_F16, 4, 3, 128, 0, 12, 15, 1, 0, out, 128, s, NULL, 0, flag,
                                1u << 16, NULL) == IWQ_ERR_ARG);
+  /* the table paths (a decode table given): every format's table-argument setup up to the launch --
+   * E4M3 / E3M2 / E2M1 embed the codes in the entries, E3M4 does not; with and without packed codes,
+   * sym / asym, plus the batched form and the approximate decode */
+  void* lut = DEV(6);
+  void* codes = DEV(7);
+  void* z = DEV(8);
+  const int fmts[4][2] = {{4, 3}, {3, 2}, {2, 1}, {3, 4}};
+  for (int i = 0; i < 4; ++i)
+    for (int sym = 0; sym <= 1; ++sym)
+      for (int wc = 0; wc <= 1; ++wc) {
+        const int st = iwq_quantize_fp_lut(w, 64, 128, 128, IWQ_F16, fmts[i][0], fmts[i][1], 128, sym, 0, out, 128,
+                                           wc ? codes : NULL, s, sym ? NULL : z, NULL, 0, flag, 0, NULL, lut);
+        CHECK(st == IWQ_ERR_HIP || st == IWQ_OK);
+      }
+  int st = iwq_quantize_fp_approx_lut(w, 64, 128, 128, IWQ_F16, 4, 3, 128, 0, 12, 15, 1, 0, out, 128, s, NULL, 0, flag,
+                                      0, NULL, lut);
+  CHECK(st == IWQ_ERR_HIP || st == IWQ_OK);
+  st = iwq_fp4_grid_packed(w, 64, 128, 128, 0, out, codes, s, NULL, 0, flag, 0, NULL, lut);
+  CHECK(st == IWQ_ERR_HIP || st == IWQ_OK);
 }
 
 int main(void) {

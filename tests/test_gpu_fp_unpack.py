@@ -162,3 +162,33 @@ def test_unpack_errors(K):
     cd8 = torch.zeros(64 * 64, dtype=torch.uint8, device=DEV)
     with pytest.raises(RuntimeError):  # E5M2: fp_max 114688 overflows fp16 (quant_linear.py:852)
         K.dequant_fp_packed(cd8, sc, None, 5, 2, -2, 64, 64)
+
+
+def _ab_built():
+    try:
+        from iron_weight_only_quant_amd import _lib
+        return _lib.ab_built()
+    except OSError:
+        return False
+
+
+@pytest.mark.skipif(not _ab_built(), reason="A/B kernel variants: IWQ_AB=1 library")
+@pytest.mark.parametrize("em", FORMATS)
+@pytest.mark.parametrize("sym", [True, False])
+@pytest.mark.parametrize("group", [32, 128])
+def test_embedded_codes_equal_reencoded(K, em, sym, group):
+    """Round 6: the table path with the codes embedded in the table entries and the entries read into
+    register halves (variant 0) == the round-5 form (variant 7: v_perm-joined reads, codes re-encoded
+    from the decoded values), codes / outputs / scales / zeros bit for bit, on specials and on a
+    grid-stride-sized tensor."""
+    E, M = em
+    for w in (_specials(64, 1024, 5 + E * 3 + M), weights(2048, 4096, 17 + E)):
+        a = K.quantize_fp(w, E, M, group, sym, 0, want_codes=True, flags=7 << 16)
+        b = K.quantize_fp(w, E, M, group, sym, 0, want_codes=True)
+        c = K.quantize_fp(w, E, M, group, sym, 0)
+        assert torch.equal(a.codes, b.codes), (em, sym, group)
+        for x in (b, c):
+            assert torch.equal(a.out.view(torch.int16), x.out.view(torch.int16)), (em, sym, group)
+            assert torch.equal(a.scales.view(torch.int16), x.scales.view(torch.int16))
+            if not sym:
+                assert torch.equal(a.zeros.view(torch.int16), x.zeros.view(torch.int16))

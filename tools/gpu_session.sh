@@ -42,7 +42,7 @@ IFS=',' read -ra STEPS <<< "${1:-tests,smoke,bench}"
 for s in "${STEPS[@]}"; do
   case $s in
     tests) step pytest_gpu 1000 $PYT tests -m gpu ;;
-    abtests) IWQ_AB=1 step pytest_gpu_ab 700 $PYT tests/test_gpu_parity.py tests/test_gpu_approx.py -m gpu ;;
+    abtests) IWQ_AB=1 step pytest_gpu_ab 700 $PYT tests/test_gpu_parity.py tests/test_gpu_approx.py tests/test_gpu_fp_unpack.py -m gpu ;;
     subset) step pytest_subset 900 $PYT ${PYTEST_FILES:-tests} -m gpu -x -k "$PYTEST_K" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
