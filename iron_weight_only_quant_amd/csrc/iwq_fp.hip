@@ -539,6 +539,13 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
   void* tz = a.zeros;
   int64_t tnumel = a.numel, tbeg = 0, tnext = INT64_MAX;
   int32_t cur = -1;
+  // which outputs the current tensor has, as ONE wave-uniform word (bit 0 out, 1 scales, 2 zeros):
+  // three pointer tests per unit kept 64-bit masks live across the loop, which the compiler spilled
+  // into VGPR lanes (two v_readlane per test per unit)
+  auto outs_of = [&]() {
+    return __builtin_amdgcn_readfirstlane((tout ? 1 : 0) | (tsc ? 2 : 0) | (tz ? 4 : 0));
+  };
+  int32_t has = outs_of();
   auto seek = [&](int64_t u) {
     if constexpr (BATCHED) {
       if (cur < 0 || u >= tnext) {
@@ -553,13 +560,14 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
         tnumel = tab[cur].rows * tab[cur].cols;
         tbeg = tab[cur].unit_begin;
         tnext = cur + 1 < a.n_entries ? tab[cur + 1].unit_begin : INT64_MAX;
+        has = outs_of();
       }
     }
   };
   auto store_params = [&](int64_t e0, const FpParams& p) {
     if ((lane % LPG) == 0) {
-      if (tsc) store_param<DT_F16>(tsc, e0 / G, p.s);
-      if (!SYM && CODEC == CODEC_FP && tz) store_param<DT_F16>(tz, e0 / G, p.z);
+      if (has & 2) store_param<DT_F16>(tsc, e0 / G, p.s);
+      if (!SYM && CODEC == CODEC_FP && (has & 4)) store_param<DT_F16>(tz, e0 / G, p.z);
     }
   };
   auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
@@ -634,7 +642,7 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
           cp[j] = codes_of_values(rb, a.f, rebias);
       }
       if (e0 < tnumel) {
-        if (tout) o.store(tout + e0 * F::BYTES);
+        if (has & 1) o.store(tout + e0 * F::BYTES);
         // the pairs' halves straight into bytes / nibbles (two v_perm for bytes, the INT packing)
         if constexpr (CODES != 0) store_codes8<CODES>(a.codes, e0, cp);
         store_params(e0, p);
@@ -650,7 +658,7 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
       }
       if (e0 < tnumel) {
         any_nan |= nan8;
-        if (tout) o.store(tout + e0 * F::BYTES);
+        if (has & 1) o.store(tout + e0 * F::BYTES);
         if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
         store_params(e0, p);
       }
@@ -752,9 +760,9 @@ __global__ __launch_bounds__(LUT_QBLOCK) void k_fp_group_lut(FpArgs a) {
 #if IWQ_AB
 // A/B (round 6): the same kernel held to 8 waves per SIMD (<= 64 VGPRs, 4 workgroups per CU) -- the
 // closed-form E2M1 form stages no table, so only the registers bound its residency
-template <int CODEC, int G, bool SYM, bool GS, int CODES, bool E2A>
+template <int CODEC, int G, bool SYM, bool GS, int CODES, bool E2A, bool EC = false>
 __global__ __launch_bounds__(LUT_QBLOCK, 8) void k_fp_group_lut_w8(FpArgs a) {
-  fp_group_lut_body<CODEC, G, SYM, GS, false, CODES, E2A, false>(a);
+  fp_group_lut_body<CODEC, G, SYM, GS, false, CODES, E2A, false, EC>(a);
 }
 #endif
 
@@ -1050,7 +1058,7 @@ hipError_t launch_fp_lut_pf(const FpArgs& a, hipStream_t st) {
   const size_t lds = E2A ? 0 : (size_t)a.lut_n8 * 2;
 #if IWQ_AB
   if constexpr (W8)
-    return launch_fp_lut_kern(k_fp_group_lut_w8<CODEC, G, SYM, false, CODES, E2A>, k_fp_group_lut_w8<CODEC, G, SYM, true, CODES, E2A>,
+    return launch_fp_lut_kern(k_fp_group_lut_w8<CODEC, G, SYM, false, CODES, E2A, EC>, k_fp_group_lut_w8<CODEC, G, SYM, true, CODES, E2A, EC>,
                               lds, a, st);
 #else
   static_assert(!W8, "A/B form");
@@ -1065,7 +1073,7 @@ hipError_t launch_fp_lut_t(const FpArgs& a, hipStream_t st) {
 #if IWQ_AB
   if (a.variant == 3 || (E2A && a.variant == 4)) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, true, false, EC>(a, st);
   if constexpr (G == 128)  // 5 / 6: held to 8 waves per SIMD (the formats rows' group only)
-    if (a.variant == 5 || a.variant == 6) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, true>(a, st);
+    if (a.variant == 5 || a.variant == 6) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, true, EC>(a, st);
   if constexpr (!E2A)
     if (a.variant == 7) return launch_fp_lut_pf<CODEC, G, SYM, CODES, E2A, false, false, false, false>(a, st);
 #endif
