@@ -218,7 +218,10 @@ int iwq_quantize_fp_approx(const void* w, int64_t rows, int64_t cols, int64_t ld
  * IWQ_FP_LUT_BYTES, 16-B aligned) for one format, computed on the device by the exact codec.
  * The *_lut entry points take such a table (built with the SAME codec / exp / mant / approximate
  * parameters) and read it through LDS instead of running the bit-level codec per element; lut NULL
- * is the plain entry point.  Packed codes (out_codes) always take the ALU codec.
+ * is the plain entry point.  The table layout is internal to the library: for IWQ_CODEC_FP / GRID
+ * formats with exp_bits + 2 * mant_bits <= 10 each entry also carries the magnitude code of its
+ * decoded value in its low exp_bits + mant_bits bits, which is where packed codes (out_codes) come
+ * from on the table path (bit-identical to the ALU codec's codes).
  * codec: IWQ_CODEC_FP (iwq_quantize_fp), IWQ_CODEC_GRID (iwq_fp4_grid; exp/mant ignored),
  * IWQ_CODEC_APX (iwq_quantize_fp_approx, single-aligned decode), IWQ_CODEC_APX_DOUBLE
  * (iwq_quantize_fp_approx with double_approx: per-code words of the quad decoder; one pass for
