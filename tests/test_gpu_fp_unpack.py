@@ -131,8 +131,9 @@ def _specials(rows, cols, seed):
 @pytest.mark.parametrize("sym", [True, False])
 @pytest.mark.parametrize("group", [32, 128])
 def test_codes_table_path_equals_codec(K, em, sym, group):
-    """quantize_fp(want_codes): codes re-encoded from the LDS table's decoded values (code_of_value)
-    == the bit-level codec's codes, outputs and scales identical too."""
+    """quantize_fp(want_codes): the table path's codes (round 6: carried by the table entries where
+    E + 2M <= 10 -- every format here but E3M4 -- else re-encoded from the decoded values) == the
+    bit-level codec's codes, outputs and scales identical too."""
     E, M = em
     w = _specials(64, 1024, 3 + E * 5 + M)
     a = K.quantize_fp(w, E, M, group, sym, 0, want_codes=True, use_lut=False)
