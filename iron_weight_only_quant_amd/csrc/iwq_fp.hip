@@ -564,13 +564,17 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
       }
     }
   };
-  auto store_params = [&](int64_t e0, const FpParams& p) {
+  // Addresses (round 6, session 2): the iteration's unit 0 is addressed once (output, codes, group
+  // index of this lane) and unit k adds a compile-time offset that folds into the memory instruction
+  // -- instead of a 64-bit address chain per unit and store.
+  auto store_params = [&](int64_t gi, const FpParams& p) {
     if ((lane % LPG) == 0) {
-      if (has & 2) store_param<DT_F16>(tsc, e0 / G, p.s);
-      if (!SYM && CODEC == CODEC_FP && (has & 4)) store_param<DT_F16>(tz, e0 / G, p.z);
+      if (has & 2) store_param<DT_F16>(tsc, gi, p.s);
+      if (!SYM && CODEC == CODEC_FP && (has & 4)) store_param<DT_F16>(tz, gi, p.z);
     }
   };
-  auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table) {
+  auto unit_out = [&](int k, int64_t e0, const FpParams& p, const Vec8<DT_F16>& vk, bool table, char* po,
+                      uint8_t* pc, int64_t gi) {
     Vec8<DT_F16> o;
     if (table) {  // finite group (grid: S > 0): table path, no NaN possible
       // in three phases so that the unit's eight table reads are in flight together (one LDS wait per
@@ -606,19 +610,21 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
         // entries 2j / 2j + 1 into the halves of r[j]: each address is lbase + one half of a2 by one SDWA
         // add (the compiler spends an and + add on the low half), and the two zero-extended reads are
         // joined by one shift-or.  (D16 reads into the halves of one register do not save that op:
-        // gfx950 has no d16-preserve -- a d16 / d16_hi load zeroes the other half.)  The reads are
-        // inline asm, so the wait that ends them also carries their registers into the code below.
-        uint32_t lo[4], hi[4];
+        // gfx950 has no d16-preserve -- a d16 / d16_hi load zeroes the other half.)
+        uint32_t lo[4], hi[4], al[4], ah[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t alo, ahi;
+        for (int j = 0; j < 4; ++j)
           asm("v_add_u32_sdwa %0, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
               "v_add_u32_sdwa %1, %2, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
-              : "=&v"(alo), "=&v"(ahi) : "v"(a2[j]), "s"(lbase));
-          asm volatile("ds_read_u16 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(lo[j]), "=&v"(hi[j]) : "v"(alo), "v"(ahi));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]), "+v"(hi[3]));
+              : "=&v"(al[j]), "=&v"(ah[j]) : "v"(a2[j]), "s"(lbase));
+        // the eight reads and the wait that ends them in ONE statement: no instruction the compiler
+        // places can touch a destination register before its data has landed
+        asm volatile(
+            "ds_read_u16 %0, %8\n\tds_read_u16 %4, %12\n\tds_read_u16 %1, %9\n\tds_read_u16 %5, %13\n\t"
+            "ds_read_u16 %2, %10\n\tds_read_u16 %6, %14\n\tds_read_u16 %3, %11\n\tds_read_u16 %7, %15\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(lo[0]), "=&v"(lo[1]), "=&v"(lo[2]), "=&v"(lo[3]), "=&v"(hi[0]), "=&v"(hi[1]), "=&v"(hi[2]), "=&v"(hi[3])
+            : "v"(al[0]), "v"(al[1]), "v"(al[2]), "v"(al[3]), "v"(ah[0]), "v"(ah[1]), "v"(ah[2]), "v"(ah[3]));
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = lo[j] | (hi[j] << 16);
       }
@@ -642,10 +648,10 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
           cp[j] = codes_of_values(rb, a.f, rebias);
       }
       if (e0 < tnumel) {
-        if (has & 1) o.store(tout + e0 * F::BYTES);
+        if (has & 1) o.store(po);
         // the pairs' halves straight into bytes / nibbles (two v_perm for bytes, the INT packing)
-        if constexpr (CODES != 0) store_codes8<CODES>(a.codes, e0, cp);
-        store_params(e0, p);
+        if constexpr (CODES != 0) store_codes8<CODES>(pc, 0, cp);
+        store_params(gi, p);
       }
     } else {
       bool nan8 = false;
@@ -658,9 +664,9 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
       }
       if (e0 < tnumel) {
         any_nan |= nan8;
-        if (has & 1) o.store(tout + e0 * F::BYTES);
-        if constexpr (CODES != 0) store_fp_codes8<CODES>(a.codes, e0, c);
-        store_params(e0, p);
+        if (has & 1) o.store(po);
+        if constexpr (CODES != 0) store_fp_codes8<CODES>(pc, 0, c);
+        store_params(gi, p);
       }
     }
   };
@@ -684,25 +690,33 @@ __device__ __forceinline__ void fp_group_lut_body(const FpArgs& a) {
       ps = fp_group_params<CODEC, SYM>(smn, smx, a.f);
       shared_ok = __ballot(kk < nu && !(ps.fast && ps.s > 0.0f)) == 0;
     }
+    // (integer arithmetic: tout may be null -- a codes-only call -- and is then never dereferenced)
+    char* po = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(tout) + (uintptr_t)(eb * F::BYTES));
+    uint8_t* pc = CODES == 0 ? nullptr : a.codes + (CODES == 4 ? eb / 2 : eb);
+    const int64_t g0 = eb / G;
+    constexpr int CB = CODES == 4 ? UNIT / 2 : UNIT;                     // code bytes per unit
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
       if (k < nu) {
         const int64_t e0 = eb + (int64_t)k * UNIT;
+        char* pok = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(po) + k * UNIT * F::BYTES);
+        uint8_t* pck = CODES == 0 ? nullptr : pc + k * CB;
+        const int64_t gik = g0 + k * (UNIT / G);
         if (SHARE && shared_ok) {
-          unit_out(k, e0, bcast_fp_params(ps, k), v[k], true);
+          unit_out(k, e0, bcast_fp_params(ps, k), v[k], true, pok, pck, gik);
         } else {
           const FpParams p = fp_group_params<CODEC, SYM>(mn[k], mx[k], a.f);
-          unit_out(k, e0, p, v[k], p.fast && p.s > 0.0f);
+          unit_out(k, e0, p, v[k], p.fast && p.s > 0.0f, pok, pck, gik);
         }
       }
     }
   };
   auto load_iter = [&](int32_t nu, int64_t eb, Vec8<DT_F16> (&v)[UNROLL]) {
+    const char* pw = tw + eb * F::BYTES;
 #pragma unroll
     for (int k = 0; k < UNROLL; ++k) {
-      const int64_t e = eb + (int64_t)k * UNIT;
-      const bool ok = (k < nu) && e < tnumel;
-      v[k].load(tw + (ok ? e : 0) * F::BYTES);
+      const bool ok = (k < nu) && eb + (int64_t)k * UNIT < tnumel;
+      v[k].load(ok ? pw + k * UNIT * F::BYTES : tw);
     }
   };
   auto advance = [&](int32_t nu) {
