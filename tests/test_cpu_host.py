@@ -420,3 +420,28 @@ def test_e2m1_closed_form():
     gtq = np.where(((a + 0x4BFF) & 0x8000) != 0, 0xFFFF, 0)
     got = np.maximum(nb & ge1, gtq & 0x3800)
     assert np.array_equal(got[dom], ref[dom])
+
+
+def test_bench_summary_is_last_and_compact():
+    """bench.py's record ends with `summary` (the driver keeps only the stdout tail): the headline
+    roofline figures, every section's key fraction, a few hundred bytes; missing sections are skipped."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location(
+        "bench_for_summary", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    rec = {"roofline": {"frac": 0.76, "kernel_over_ceiling": 0.99, "fresh_ceiling": {"GBps": 6200.0},
+                        "kernel_over_fresh_ceiling": 0.98, "other_placement": {"placement": "in-place", "frac": 0.74},
+                        "traffic": 2.0e9, "alg_bytes_per_launch": 1.0e9},
+           "shapes": {"4096x4096": {"frac": 0.61, "frac_beyond_launch_floor": 0.71}},
+           "fused_forward": {"rows": [{"shape": "q_proj", "weights": "per-channel", "M": 1, "fused_vs_F_linear": 3.1}]},
+           "formats": {"rows": [{"path": "fp4_e2m1_g128_asym_pack", "frac_of_hbm_peak": 0.67}]},
+           "llama2_70b": {"roofline": {"frac": 0.74}}, "cpu_baseline": {"value": 0.45}}
+    s = b.summary_of(rec)
+    assert s["frac"] == 0.76 and s["traffic_over_alg"] == 2.0 and s["other_placement"] == ["in-place", 0.74]
+    assert s["shapes_frac"]["4096x4096"] == [0.61, 0.71]
+    assert s["fused_vs_F_linear"]["q_proj/pc/M1"] == 3.1
+    assert s["formats_frac"]["fp4_e2m1_g128_asym_pack"] == 0.67 and s["llama2_70b_frac"] == 0.74
+    assert len(json.dumps(s)) < 2000
+    assert set(b.summary_of({"roofline": {"frac": 0.7}})) >= {"frac"}  # sections absent (N > 1 runs)
